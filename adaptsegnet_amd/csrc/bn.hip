@@ -1,0 +1,312 @@
+// BatchNorm2d (train mode, batch statistics) for NHWC activations [rows][C] on gfx950.
+// Reference: nn.BatchNorm2d(affine, frozen) + ReLU + residual add in
+// model/deeplab_multi.py:65-101 (Bottleneck), :130-134 (stem), :160-162 (downsample).
+//
+// Forward = stats pass (per-block shifted sums -> fp64 combine, one deterministic finalize
+// that also updates running_mean / running_var with the unbiased variance, as torch does)
+// + one fused apply pass y = relu(xhat*w + b + res).  Backward = one reduction pass
+// (sum g, sum g*(x-mean), with g = dy * [y > 0] when the forward had a ReLU) + one apply
+// pass that also emits the residual gradient.  All passes are float4-vectorised and
+// HBM-bound.
+#include "common.hpp"
+#include <algorithm>
+
+namespace adaptseg {
+
+// Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
+// Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
+template <int MODE>  // 0: stats (shifted by pivot x[0][c]), 1: backward sums
+__global__ void __launch_bounds__(256)
+bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const float *__restrict__ dy,
+                 const float *__restrict__ y, const float *__restrict__ mean, int relu,
+                 int64_t rows_per_split, float *__restrict__ partial) {
+  const int tr = 256 / tc;
+  const int cq = threadIdx.x % tc;   // channel quad within block
+  const int rl = threadIdx.x / tc;   // row lane
+  const int c0 = (blockIdx.x * tc + cq) * 4;
+  const bool cok = c0 < C;
+  const int64_t r0 = blockIdx.y * rows_per_split;
+  const int64_t r1 = min(rows, r0 + rows_per_split);
+  float4 s1 = make_float4(0, 0, 0, 0), s2 = make_float4(0, 0, 0, 0);
+  float4 piv = make_float4(0, 0, 0, 0);
+  if (cok) {
+    if (MODE == 0) piv = *reinterpret_cast<const float4 *>(x + c0);
+    else piv = *reinterpret_cast<const float4 *>(mean + c0);
+    for (int64_t r = r0 + rl; r < r1; r += tr) {
+      float4 v = *reinterpret_cast<const float4 *>(x + r * C + c0);
+      float4 d = make_float4(v.x - piv.x, v.y - piv.y, v.z - piv.z, v.w - piv.w);
+      if (MODE == 0) {
+        s1.x += d.x; s1.y += d.y; s1.z += d.z; s1.w += d.w;
+        s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
+      } else {
+        float4 g = *reinterpret_cast<const float4 *>(dy + r * C + c0);
+        if (relu) {
+          float4 o = *reinterpret_cast<const float4 *>(y + r * C + c0);
+          g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
+          g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
+        }
+        s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
+        s2.x += g.x * d.x; s2.y += g.y * d.y; s2.z += g.z * d.z; s2.w += g.w * d.w;
+      }
+    }
+  }
+  __shared__ float4 red1[256], red2[256];
+  red1[threadIdx.x] = s1;
+  red2[threadIdx.x] = s2;
+  __syncthreads();
+  if (rl == 0 && cok) {
+    float4 a = red1[threadIdx.x], b = red2[threadIdx.x];
+    for (int i = 1; i < tr; ++i) {
+      float4 u = red1[threadIdx.x + i * tc], v = red2[threadIdx.x + i * tc];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    }
+    float *p1 = partial + (size_t)blockIdx.y * 2 * C;
+    *reinterpret_cast<float4 *>(p1 + c0) = a;
+    *reinterpret_cast<float4 *>(p1 + C + c0) = b;
+  }
+}
+
+// Finalise forward statistics: mean, invstd, running-stat update.
+__global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ x,
+                                      const float *__restrict__ partial, float *mean_out,
+                                      float *invstd_out, float *running_mean, float *running_var,
+                                      float momentum, float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int i = 0; i < splits; ++i) {
+    s1 += partial[(size_t)i * 2 * C + c];
+    s2 += partial[(size_t)i * 2 * C + C + c];
+  }
+  double n = (double)rows;
+  double dm = s1 / n;
+  double var = s2 / n - dm * dm;
+  if (var < 0) var = 0;
+  double mean = (double)x[c] + dm;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+  if (running_var) {
+    double unb = rows > 1 ? var * n / (n - 1.0) : var;
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+  }
+}
+
+// Finalise backward sums: store mean(g) and mean(g*xhat) per channel.
+__global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ partial,
+                                    const float *__restrict__ invstd, float *coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int i = 0; i < splits; ++i) {
+    s1 += partial[(size_t)i * 2 * C + c];
+    s2 += partial[(size_t)i * 2 * C + C + c];
+  }
+  double n = (double)rows;
+  coef[c] = (float)(s1 / n);                       // mean(g)
+  coef[C + c] = (float)(s2 / n * (double)invstd[c]);  // mean(g * xhat)
+}
+
+__global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
+                                const float *__restrict__ mean, const float *__restrict__ invstd,
+                                const float *__restrict__ w, const float *__restrict__ b,
+                                const float *__restrict__ res, float *__restrict__ y, int relu) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)((i * 4) % C);
+    float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float4 m = *reinterpret_cast<const float4 *>(mean + c);
+    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
+    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
+    float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
+    float4 o;
+    o.x = (v.x - m.x) * is.x * ww.x + bb.x;
+    o.y = (v.y - m.y) * is.y * ww.y + bb.y;
+    o.z = (v.z - m.z) * is.z * ww.z + bb.z;
+    o.w = (v.w - m.w) * is.w * ww.w + bb.w;
+    if (res) {
+      float4 r = reinterpret_cast<const float4 *>(res)[i];
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    if (relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    reinterpret_cast<float4 *>(y)[i] = o;
+  }
+}
+
+// dx / dres may alias dy (in-place gradient): each element is read before it is written.
+__global__ void bn_bwd_apply_kernel(int64_t total4, int C, const float *dy,
+                                    const float *__restrict__ y, const float *__restrict__ x,
+                                    const float *__restrict__ w, const float *__restrict__ mean,
+                                    const float *__restrict__ invstd, const float *__restrict__ coef,
+                                    float *dx, float *dres, int relu, int train) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)((i * 4) % C);
+    float4 g = reinterpret_cast<const float4 *>(dy)[i];
+    if (relu) {
+      float4 o = reinterpret_cast<const float4 *>(y)[i];
+      g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
+      g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
+    }
+    if (dres) reinterpret_cast<float4 *>(dres)[i] = g;
+    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
+    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
+    float4 o;
+    if (train) {
+      float4 v = reinterpret_cast<const float4 *>(x)[i];
+      float4 m = *reinterpret_cast<const float4 *>(mean + c);
+      float4 mg = *reinterpret_cast<const float4 *>(coef + c);
+      float4 mgx = *reinterpret_cast<const float4 *>(coef + C + c);
+      o.x = ww.x * is.x * (g.x - mg.x - (v.x - m.x) * is.x * mgx.x);
+      o.y = ww.y * is.y * (g.y - mg.y - (v.y - m.y) * is.y * mgx.y);
+      o.z = ww.z * is.z * (g.z - mg.z - (v.z - m.z) * is.z * mgx.z);
+      o.w = ww.w * is.w * (g.w - mg.w - (v.w - m.w) * is.w * mgx.w);
+    } else {
+      o.x = g.x * ww.x * is.x; o.y = g.y * ww.y * is.y; o.z = g.z * ww.z * is.z; o.w = g.w * ww.w * is.w;
+    }
+    reinterpret_cast<float4 *>(dx)[i] = o;
+  }
+}
+
+__global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
+                                      const float *__restrict__ rm, const float *__restrict__ rv, float eps,
+                                      const float *__restrict__ w, const float *__restrict__ b,
+                                      const float *__restrict__ res, float *__restrict__ y, int relu) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)((i * 4) % C);
+    float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float o[4] = {v.x, v.y, v.z, v.w};
+    float r4[4] = {0, 0, 0, 0};
+    if (res) {
+      float4 r = reinterpret_cast<const float4 *>(res)[i];
+      r4[0] = r.x; r4[1] = r.y; r4[2] = r.z; r4[3] = r.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float is = 1.0f / sqrtf(rv[c + j] + eps);
+      float t = (o[j] - rm[c + j]) * is * (w ? w[c + j] : 1.f) + (b ? b[c + j] : 0.f) + r4[j];
+      o[j] = relu ? fmaxf(t, 0.f) : t;
+    }
+    reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+struct ReducePlan {
+  int tc, cblocks, splits;
+  int64_t per;
+};
+
+static ReducePlan reduce_plan(int64_t rows, int C) {
+  ReducePlan r;
+  r.tc = std::min(C / 4, 64);
+  if (r.tc < 1) r.tc = 1;
+  // tc must divide 256
+  while (256 % r.tc) --r.tc;
+  r.cblocks = (int)ceil_div(C, 4 * r.tc);
+  int want = std::max(1, 1024 / r.cblocks);
+  int tr = 256 / r.tc;
+  int64_t max_splits = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * 8));
+  r.splits = (int)std::min<int64_t>(want, max_splits);
+  r.per = ceil_div(rows, r.splits);
+  r.splits = (int)ceil_div(rows, r.per);
+  return r;
+}
+
+static size_t bn_ws_bytes(int64_t rows, int C) {
+  ReducePlan r = reduce_plan(rows, C);
+  // partial [splits][2][C] + coef [2][C]
+  return ((size_t)r.splits * 2 * C + 2 * (size_t)C) * sizeof(float);
+}
+
+static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(total4, 256), 8192); }
+
+}  // namespace adaptseg
+
+using namespace adaptseg;
+
+extern "C" {
+
+int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes) {
+  AS_CHECK_ARG(bytes && rows > 0 && c > 0, "bn_workspace_size: bad args");
+  *bytes = bn_ws_bytes(rows, c);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          float *running_mean, float *running_var, float momentum, float eps,
+                          float *save_mean, float *save_invstd, const float *res, float *y, int relu,
+                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
+  AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
+  AS_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: null pointer");
+  size_t need = bn_ws_bytes(rows, c);
+  if (!ws || ws_bytes < need) {
+    set_error("bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
+    return ADAPTSEG_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  ReducePlan r = reduce_plan(rows, c);
+  float *partial = reinterpret_cast<float *>(ws);
+  bn_reduce_kernel<0><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
+                                                                0, r.per, partial);
+  AS_CHECK_LAUNCH("bn_reduce<stats>");
+  bn_stats_final_kernel<<<(unsigned)ceil_div(c, 256), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
+                                                                   save_invstd, running_mean, running_var,
+                                                                   momentum, eps);
+  AS_CHECK_LAUNCH("bn_stats_final");
+  int64_t total4 = rows * c / 4;
+  bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
+                                                   relu);
+  AS_CHECK_LAUNCH("bn_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          const float *running_mean, const float *running_var, float eps, const float *res,
+                          float *y, int relu, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
+  AS_CHECK_ARG(x && y && running_mean && running_var, "bn_fwd_infer: null pointer");
+  hipStream_t s = as_stream(stream);
+  int64_t total4 = rows * c / 4;
+  bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight,
+                                                         bias, res, y, relu);
+  AS_CHECK_LAUNCH("bn_infer_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
+                    const float *save_mean, const float *save_invstd, float *dx, float *dres, int relu, int train,
+                    void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
+  AS_CHECK_ARG(dy && dx && save_invstd && (!relu || y) && (!train || (x && save_mean)), "bn_bwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  float *coef = nullptr;
+  if (train) {
+    size_t need = bn_ws_bytes(rows, c);
+    if (!ws || ws_bytes < need) {
+      set_error("bn_bwd: workspace %zu < %zu", ws_bytes, need);
+      return ADAPTSEG_ERR_WORKSPACE;
+    }
+    ReducePlan r = reduce_plan(rows, c);
+    float *partial = reinterpret_cast<float *>(ws);
+    coef = partial + (size_t)r.splits * 2 * c;
+    bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean, relu,
+                                                                  r.per, partial);
+    AS_CHECK_LAUNCH("bn_reduce<bwd>");
+    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 256), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
+                                                                   coef);
+    AS_CHECK_LAUNCH("bn_bwd_final");
+  }
+  int64_t total4 = rows * c / 4;
+  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, y, x, weight, save_mean, save_invstd, coef,
+                                                       dx, dres, relu, train);
+  AS_CHECK_LAUNCH("bn_bwd_apply");
+  return ADAPTSEG_OK;
+}
+
+}  // extern "C"
+

@@ -1,0 +1,58 @@
+// Shared helpers for the adaptseg gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+#include "../../include/adaptseg.h"
+
+namespace adaptseg {
+
+void set_error(const char *fmt, ...);
+
+#define AS_CHECK_ARG(cond, ...)                                                              \
+  do {                                                                                       \
+    if (!(cond)) {                                                                           \
+      ::adaptseg::set_error(__VA_ARGS__);                                                    \
+      return ADAPTSEG_ERR_ARG;                                                               \
+    }                                                                                        \
+  } while (0)
+
+#define AS_CHECK_LAUNCH(name)                                                                \
+  do {                                                                                       \
+    hipError_t e_ = hipGetLastError();                                                       \
+    if (e_ != hipSuccess) {                                                                  \
+      ::adaptseg::set_error("%s: %s", name, hipGetErrorString(e_));                          \
+      return ADAPTSEG_ERR_HIP;                                                               \
+    }                                                                                        \
+  } while (0)
+
+inline hipStream_t as_stream(adaptseg_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Unsigned division by a runtime constant: q = (umulhi(n, m) + n) >> s, valid for n < 2^31.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  uint64_t num = ((1ull << 32) * ((1ull << s) - d));
+  f.m = (uint32_t)(num / d + 1);
+  if (d == 1) f.m = 0;  // (0 + n) >> 0 == n
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+  uint32_t hi = __umulhi(n, f.m);
+  return (hi + n) >> f.s;
+}
+
+constexpr int kWave = 64;
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace adaptseg

@@ -1,0 +1,645 @@
+// HBM-bound kernels of the AdaptSegNet step on gfx950 (NHWC fp32 activations):
+//   max-pool fwd/bwd           model/deeplab_multi.py:135,178
+//   bilinear upsample fwd/bwd  model/deeplab_multi.py:188-189 (align_corners=True)
+//   channel softmax fwd/bwd    train_gta2cityscapes_multi.py:423,442,454,617-618
+//   cross entropy (ignore 255) utils/loss.py:14-36, train_gta2cityscapes_multi.py:359,546
+//   BCE-with-logits / MSE vs a constant target   train_gta2cityscapes_multi.py:542-545
+//   SGD(momentum, wd) / Adam   train_gta2cityscapes_multi.py:532-540
+// Every reduction is block-partial + one ordered finalize (no float atomics), so results
+// are bitwise reproducible run to run.
+#include "common.hpp"
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+
+namespace adaptseg {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+static int grid1d(int64_t n, int per_block = 256, int cap = 8192) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, per_block), cap));
+}
+
+// ------------------------------------------------------------------------------------
+// MaxPool2d NHWC.  argmax stores the window position (kh*k + kw) of the first maximum
+// in (kh, kw) scan order — the torch CPU tie rule.  Padding acts as -inf.
+// ------------------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(int n, int C, int H, int W, int OH, int OW, int k, int s, int p,
+                                   const float *__restrict__ x, float *__restrict__ y,
+                                   uint8_t *__restrict__ am) {
+  const int64_t total = (int64_t)n * OH * OW * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int ow = (int)(t % OW); t /= OW;
+    int oh = (int)(t % OH);
+    int b = (int)(t / OH);
+    float best = -INFINITY;
+    int bi = -1;
+    for (int kh = 0; kh < k; ++kh) {
+      int ih = oh * s - p + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        int iw = ow * s - p + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v = x[(((int64_t)b * H + ih) * W + iw) * C + c];
+        if (bi < 0) bi = kh * k + kw;
+        if (v > best || isnan(v)) {
+          best = v;
+          bi = kh * k + kw;
+        }
+      }
+    }
+    y[i] = best;
+    am[i] = (uint8_t)bi;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(int n, int C, int H, int W, int OH, int OW, int k, int s, int p,
+                                   const float *__restrict__ dy, const uint8_t *__restrict__ am,
+                                   float *__restrict__ dx) {
+  const int64_t total = (int64_t)n * H * W * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int iw = (int)(t % W); t /= W;
+    int ih = (int)(t % H);
+    int b = (int)(t / H);
+    // output rows whose window covers ih: oh*s - p <= ih <= oh*s - p + k - 1
+    int oh_lo = std::max(0, (ih + p - (k - 1) + s - 1) / s);
+    if (ih + p - (k - 1) < 0) oh_lo = 0;
+    int oh_hi = std::min(OH - 1, (ih + p) / s);
+    int ow_lo = std::max(0, (iw + p - (k - 1) + s - 1) / s);
+    if (iw + p - (k - 1) < 0) ow_lo = 0;
+    int ow_hi = std::min(OW - 1, (iw + p) / s);
+    float acc = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      int kh = ih + p - oh * s;
+      if (kh < 0 || kh >= k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        int kw = iw + p - ow * s;
+        if (kw < 0 || kw >= k) continue;
+        int64_t o = (((int64_t)b * OH + oh) * OW + ow) * C + c;
+        if (am[o] == kh * k + kw) acc += dy[o];
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Bilinear upsample, align_corners=True (torch area_pixel_compute_scale semantics).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ float ac_scale(int in, int out) {
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+}
+
+__device__ __forceinline__ void ac_src(float scale, int dst, int in, int &i0, int &i1, float &l1) {
+  float src = scale * (float)dst;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+__global__ void upsample_fwd_kernel(int n, int C, int h, int w, int OH, int OW, const float *__restrict__ x,
+                                    float *__restrict__ y) {
+  const float sh = ac_scale(h, OH), sw = ac_scale(w, OW);
+  const int64_t total = (int64_t)n * OH * OW * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int X = (int)(t % OW); t /= OW;
+    int Y = (int)(t % OH);
+    int b = (int)(t / OH);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    ac_src(sh, Y, h, y0, y1, ly);
+    ac_src(sw, X, w, x0, x1, lx);
+    const float *base = x + (int64_t)b * h * w * C + c;
+    float a00 = base[((int64_t)y0 * w + x0) * C], a01 = base[((int64_t)y0 * w + x1) * C];
+    float a10 = base[((int64_t)y1 * w + x0) * C], a11 = base[((int64_t)y1 * w + x1) * C];
+    y[i] = (1.f - ly) * ((1.f - lx) * a00 + lx * a01) + ly * ((1.f - lx) * a10 + lx * a11);
+  }
+}
+
+// Candidate range of destination indices D whose source taps can touch index `v`.
+__device__ __forceinline__ void ac_range(float scale, int v, int out, int &lo, int &hi) {
+  if (scale <= 0.f) {
+    lo = 0;
+    hi = out - 1;
+    return;
+  }
+  lo = (int)floorf((float)(v - 1) / scale) - 2;
+  hi = (int)ceilf((float)(v + 1) / scale) + 2;
+  lo = std::max(lo, 0);
+  hi = std::min(hi, out - 1);
+}
+
+// pass 1: tmp[b][Y][x][c] = sum_X wx(X -> x) * dy[b][Y][X][c]
+__global__ void upsample_bwd_x_kernel(int n, int C, int w, int OH, int OW, const float *__restrict__ dy,
+                                      float *__restrict__ tmp) {
+  const float sw = ac_scale(w, OW);
+  const int64_t total = (int64_t)n * OH * w * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int xx = (int)(t % w);
+    int64_t row = t / w;  // b*OH + Y
+    int lo, hi;
+    ac_range(sw, xx, OW, lo, hi);
+    const float *g = dy + row * OW * C + c;
+    float acc = 0.f;
+    for (int X = lo; X <= hi; ++X) {
+      int x0, x1;
+      float lx;
+      ac_src(sw, X, w, x0, x1, lx);
+      float wt = (x0 == xx ? 1.f - lx : 0.f) + (x1 == xx ? lx : 0.f);
+      if (wt != 0.f) acc += wt * g[(int64_t)X * C];
+    }
+    tmp[i] = acc;
+  }
+}
+
+// pass 2: dx[b][y][x][c] (+)= sum_Y wy(Y -> y) * tmp[b][Y][x][c]
+__global__ void upsample_bwd_y_kernel(int n, int C, int h, int w, int OH, const float *__restrict__ tmp,
+                                      float *__restrict__ dx, int accumulate) {
+  const float sh = ac_scale(h, OH);
+  const int64_t total = (int64_t)n * h * w * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t inner = i % ((int64_t)w * C);  // x*C + c
+    int64_t t = i / ((int64_t)w * C);
+    int yy = (int)(t % h);
+    int b = (int)(t / h);
+    int lo, hi;
+    ac_range(sh, yy, OH, lo, hi);
+    const float *g = tmp + (int64_t)b * OH * w * C + inner;
+    float acc = 0.f;
+    for (int Y = lo; Y <= hi; ++Y) {
+      int y0, y1;
+      float ly;
+      ac_src(sh, Y, h, y0, y1, ly);
+      float wt = (y0 == yy ? 1.f - ly : 0.f) + (y1 == yy ? ly : 0.f);
+      if (wt != 0.f) acc += wt * g[(int64_t)Y * w * C];
+    }
+    dx[i] = accumulate ? dx[i] + acc : acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Channel softmax over contiguous rows of C.
+// ------------------------------------------------------------------------------------
+__global__ void softmax_fwd_kernel(int64_t rows, int C, const float *__restrict__ x, float *__restrict__ y) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const float *xr = x + r * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, xr[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(xr[c] - m);
+    float inv = 1.f / s;
+    float *yr = y + r * C;
+    for (int c = 0; c < C; ++c) yr[c] = __expf(xr[c] - m) * inv;
+  }
+}
+
+__global__ void softmax_bwd_kernel(int64_t rows, int C, const float *__restrict__ y, const float *__restrict__ dy,
+                                   float *dx, int accumulate) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const float *yr = y + r * C;
+    const float *gr = dy + r * C;
+    float dot = 0.f;
+    for (int c = 0; c < C; ++c) dot += yr[c] * gr[c];
+    float *dr = dx + r * C;
+    for (int c = 0; c < C; ++c) {
+      float v = yr[c] * (gr[c] - dot);
+      dr[c] = accumulate ? dr[c] + v : v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Softmax cross entropy with ignore label.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ bool ce_valid(int64_t lab, int ignore, int C) {
+  return lab >= 0 && lab != ignore && lab < C;
+}
+
+__global__ void __launch_bounds__(256) ce_fwd_partial_kernel(int64_t rows, int C, const float *__restrict__ logits,
+                                                             const int64_t *__restrict__ labels, int ignore,
+                                                             const float *__restrict__ cw, float *partial) {
+  float num = 0.f, den = 0.f;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lab = labels[r];
+    if (!ce_valid(lab, ignore, C)) continue;
+    const float *xr = logits + r * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, xr[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(xr[c] - m);
+    float nll = m + __logf(s) - xr[lab];
+    float wt = cw ? cw[lab] : 1.f;
+    num += wt * nll;
+    den += wt;
+  }
+  __shared__ float sn[256], sd[256];
+  sn[threadIdx.x] = num;
+  sd[threadIdx.x] = den;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sn[threadIdx.x] += sn[threadIdx.x + o];
+      sd[threadIdx.x] += sd[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = sn[0];
+    partial[2 * blockIdx.x + 1] = sd[0];
+  }
+}
+
+__global__ void pair_final_kernel(const float *partial, int nparts, float *out, int mode, double scale) {
+  // mode 0: out[0] = num/den, out[1] = den (CE);  mode 1: out[0] = num*scale (mean losses)
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double num = 0, den = 0;
+  for (int i = 0; i < nparts; ++i) {
+    num += partial[2 * i];
+    den += partial[2 * i + 1];
+  }
+  if (mode == 0) {
+    out[0] = (float)(num / den);
+    out[1] = (float)den;
+  } else {
+    out[0] = (float)(num * scale);
+  }
+}
+
+__global__ void ce_bwd_kernel(int64_t rows, int C, const float *__restrict__ logits, const int64_t *__restrict__ labels,
+                              int ignore, const float *__restrict__ cw, const float *__restrict__ out,
+                              const float *__restrict__ grad_loss, float *dl, int accumulate) {
+  const float scale = grad_loss[0] / out[1];
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lab = labels[r];
+    float *dr = dl + r * C;
+    if (!ce_valid(lab, ignore, C)) {
+      if (!accumulate)
+        for (int c = 0; c < C; ++c) dr[c] = 0.f;
+      continue;
+    }
+    const float *xr = logits + r * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, xr[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(xr[c] - m);
+    float inv = 1.f / s;
+    float k = scale * (cw ? cw[lab] : 1.f);
+    for (int c = 0; c < C; ++c) {
+      float v = k * (__expf(xr[c] - m) * inv - (c == lab ? 1.f : 0.f));
+      dr[c] = accumulate ? dr[c] + v : v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Adversarial losses vs constant target t.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ float adv_elem(float x, float t, int kind) {
+  if (kind == 0) {
+    // BCEWithLogits: (1-t)*x + max(-x,0) + log(exp(-max(-x,0)) + exp(-x-max(-x,0)))
+    float mv = fmaxf(-x, 0.f);
+    return (1.f - t) * x + mv + __logf(__expf(-mv) + __expf(-x - mv));
+  }
+  float d = x - t;
+  return d * d;
+}
+
+__global__ void __launch_bounds__(256) adv_fwd_partial_kernel(int64_t n, const float *__restrict__ x, float t,
+                                                              int kind, float *partial) {
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    s += adv_elem(x[i], t, kind);
+  __shared__ float sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = sh[0];
+    partial[2 * blockIdx.x + 1] = 0.f;
+  }
+}
+
+__global__ void adv_bwd_kernel(int64_t n, const float *__restrict__ x, float t, int kind,
+                               const float *__restrict__ grad_loss, float *dx, int accumulate) {
+  const float g = grad_loss[0] / (float)n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float xi = x[i];
+    float d = kind == 0 ? (1.f / (1.f + __expf(-xi)) - t) : 2.f * (xi - t);
+    float v = g * d;
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Optimisers over flat arenas.
+// ------------------------------------------------------------------------------------
+__global__ void sgd_kernel(int64_t n, float *__restrict__ p, const float *__restrict__ g, float *__restrict__ buf,
+                           float lr, float mom, float wd, float gs, int mult, int first) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float pi = p[i];
+    const float gi = g[i] * gs;
+    float b = buf[i];
+    for (int r = 0; r < mult; ++r) {
+      float d = gi + wd * pi;         // grad.add(param, alpha=wd)
+      b = first ? d : b * mom + d;    // clone on first step, else buf.mul_(m).add_(d)
+      pi = pi - lr * b;               // param.add_(buf, alpha=-lr)
+    }
+    buf[i] = b;
+    p[i] = pi;
+  }
+}
+
+__global__ void adam_kernel(int64_t n, float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
+                            float *__restrict__ v, float b1, float b2, float eps, float step_size, float bc2_sqrt,
+                            float gs) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gs;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);  // torch lerp_ (weight < 0.5 branch)
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Plumbing.
+// ------------------------------------------------------------------------------------
+struct Strides4 {
+  int64_t s[4];
+};
+
+__global__ void to_nhwc_kernel(int n, int C, int H, int W, Strides4 st, const float *__restrict__ src,
+                               float *__restrict__ dst) {
+  const int64_t total = (int64_t)n * C * H * W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int x = (int)(t % W); t /= W;
+    int y = (int)(t % H);
+    int b = (int)(t / H);
+    dst[i] = src[b * st.s[0] + c * st.s[1] + y * st.s[2] + x * st.s[3]];
+  }
+}
+
+__global__ void add_i64_kernel(int64_t *p, int64_t n, int64_t v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] += v;
+}
+
+__global__ void axpy_kernel(int64_t n, float a, const float *__restrict__ src, float *dst, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = accumulate ? dst[i] + a * src[i] : a * src[i];
+}
+
+}  // namespace adaptseg
+
+using namespace adaptseg;
+
+extern "C" {
+
+const char *adaptseg_last_error(void) { return g_err; }
+const char *adaptseg_version(void) { return "adaptseg 0.1 gfx950 fp32-mfma"; }
+
+int adaptseg_maxpool2d_fwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *x,
+                           float *y, uint8_t *argmax, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && k > 0 && k * k <= 255 && s > 0 && p >= 0,
+               "maxpool_fwd: bad geometry");
+  AS_CHECK_ARG(x && y && argmax, "maxpool_fwd: null pointer");
+  AS_CHECK_ARG((h + 2 * p - k) / s + 1 == oh && (w + 2 * p - k) / s + 1 == ow, "maxpool_fwd: output size mismatch");
+  int64_t total = (int64_t)n * oh * ow * c;
+  maxpool_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, x, y, argmax);
+  AS_CHECK_LAUNCH("maxpool_fwd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_maxpool2d_bwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *dy,
+                           const uint8_t *argmax, float *dx, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && k > 0 && s > 0 && p >= 0,
+               "maxpool_bwd: bad geometry");
+  AS_CHECK_ARG(dy && argmax && dx, "maxpool_bwd: null pointer");
+  int64_t total = (int64_t)n * h * w * c;
+  maxpool_bwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, dy, argmax, dx);
+  AS_CHECK_LAUNCH("maxpool_bwd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_upsample_workspace_size(int n, int c, int h, int w, int oh, int ow, size_t *bytes) {
+  AS_CHECK_ARG(bytes && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "upsample_workspace_size: bad args");
+  *bytes = (size_t)n * oh * w * c * sizeof(float);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_upsample_bilinear_fwd(int n, int c, int h, int w, int oh, int ow, const float *x, float *y,
+                                   adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "upsample_fwd: bad geometry");
+  AS_CHECK_ARG(x && y, "upsample_fwd: null pointer");
+  int64_t total = (int64_t)n * oh * ow * c;
+  upsample_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, x, y);
+  AS_CHECK_LAUNCH("upsample_fwd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_upsample_bilinear_bwd(int n, int c, int h, int w, int oh, int ow, const float *dy, float *dx, int flags,
+                                   void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "upsample_bwd: bad geometry");
+  AS_CHECK_ARG(dy && dx, "upsample_bwd: null pointer");
+  size_t need = (size_t)n * oh * w * c * sizeof(float);
+  if (!ws || ws_bytes < need) {
+    set_error("upsample_bwd: workspace %zu < %zu", ws_bytes, need);
+    return ADAPTSEG_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  float *tmp = reinterpret_cast<float *>(ws);
+  int64_t t1 = (int64_t)n * oh * w * c;
+  upsample_bwd_x_kernel<<<grid1d(t1), 256, 0, s>>>(n, c, w, oh, ow, dy, tmp);
+  AS_CHECK_LAUNCH("upsample_bwd_x");
+  int64_t t2 = (int64_t)n * h * w * c;
+  upsample_bwd_y_kernel<<<grid1d(t2), 256, 0, s>>>(n, c, h, w, oh, tmp, dx,
+                                                    (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  AS_CHECK_LAUNCH("upsample_bwd_y");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_softmax_fwd(int64_t rows, int c, const float *x, float *y, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && x && y, "softmax_fwd: bad args");
+  softmax_fwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, x, y);
+  AS_CHECK_LAUNCH("softmax_fwd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_softmax_bwd(int64_t rows, int c, const float *y, const float *dy, float *dx, int flags,
+                         adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && y && dy && dx, "softmax_bwd: bad args");
+  softmax_bwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, y, dy, dx,
+                                                                  (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  AS_CHECK_LAUNCH("softmax_bwd");
+  return ADAPTSEG_OK;
+}
+
+static int ce_parts(int64_t rows) { return grid1d(rows, 256 * 4, 2048); }
+
+int adaptseg_ce_workspace_size(int64_t rows, size_t *bytes) {
+  AS_CHECK_ARG(bytes && rows > 0, "ce_workspace_size: bad args");
+  *bytes = (size_t)ce_parts(rows) * 2 * sizeof(float);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_softmax_ce_fwd(int64_t rows, int c, const float *logits, const int64_t *labels, int ignore,
+                            const float *class_weight, float *out, void *ws, size_t ws_bytes,
+                            adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && logits && labels && out, "softmax_ce_fwd: bad args");
+  int parts = ce_parts(rows);
+  if (!ws || ws_bytes < (size_t)parts * 2 * sizeof(float)) {
+    set_error("softmax_ce_fwd: workspace too small");
+    return ADAPTSEG_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  float *partial = reinterpret_cast<float *>(ws);
+  ce_fwd_partial_kernel<<<parts, 256, 0, s>>>(rows, c, logits, labels, ignore, class_weight, partial);
+  AS_CHECK_LAUNCH("ce_fwd_partial");
+  pair_final_kernel<<<1, 64, 0, s>>>(partial, parts, out, 0, 1.0);
+  AS_CHECK_LAUNCH("ce_final");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_softmax_ce_bwd(int64_t rows, int c, const float *logits, const int64_t *labels, int ignore,
+                            const float *class_weight, const float *out, const float *grad_loss, float *dlogits,
+                            int flags, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && logits && labels && out && grad_loss && dlogits, "softmax_ce_bwd: bad args");
+  ce_bwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, logits, labels, ignore, class_weight, out,
+                                                             grad_loss, dlogits,
+                                                             (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  AS_CHECK_LAUNCH("ce_bwd");
+  return ADAPTSEG_OK;
+}
+
+static int adv_parts(int64_t n) { return grid1d(n, 256 * 4, 256); }
+
+int adaptseg_adv_workspace_size(int64_t n, size_t *bytes) {
+  AS_CHECK_ARG(bytes && n > 0, "adv_workspace_size: bad args");
+  *bytes = (size_t)adv_parts(n) * 2 * sizeof(float);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_adv_loss_fwd(int64_t n, const float *x, float target, int kind, float *loss, void *ws,
+                          size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && x && loss && (kind == 0 || kind == 1), "adv_loss_fwd: bad args");
+  int parts = adv_parts(n);
+  if (!ws || ws_bytes < (size_t)parts * 2 * sizeof(float)) {
+    set_error("adv_loss_fwd: workspace too small");
+    return ADAPTSEG_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  float *partial = reinterpret_cast<float *>(ws);
+  adv_fwd_partial_kernel<<<parts, 256, 0, s>>>(n, x, target, kind, partial);
+  AS_CHECK_LAUNCH("adv_fwd_partial");
+  pair_final_kernel<<<1, 64, 0, s>>>(partial, parts, loss, 1, 1.0 / (double)n);
+  AS_CHECK_LAUNCH("adv_final");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_adv_loss_bwd(int64_t n, const float *x, float target, int kind, const float *grad_loss, float *dx,
+                          int flags, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && x && grad_loss && dx && (kind == 0 || kind == 1), "adv_loss_bwd: bad args");
+  adv_bwd_kernel<<<grid1d(n), 256, 0, as_stream(stream)>>>(n, x, target, kind, grad_loss, dx,
+                                                           (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  AS_CHECK_LAUNCH("adv_bwd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_sgd_step(int64_t n, float *param, const float *grad, float *mom, float lr, float momentum,
+                      float weight_decay, float grad_scale, int multiplicity, int first_step,
+                      adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n >= 0 && (n == 0 || (param && grad && mom)) && multiplicity >= 1, "sgd_step: bad args");
+  if (n == 0) return ADAPTSEG_OK;
+  sgd_kernel<<<grid1d(n), 256, 0, as_stream(stream)>>>(n, param, grad, mom, lr, momentum, weight_decay, grad_scale,
+                                                       multiplicity, first_step ? 1 : 0);
+  AS_CHECK_LAUNCH("sgd");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_adam_step(int64_t n, float *param, const float *grad, float *exp_avg, float *exp_avg_sq, float lr,
+                       float beta1, float beta2, float eps, int step, float grad_scale, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n >= 0 && step >= 1 && (n == 0 || (param && grad && exp_avg && exp_avg_sq)), "adam_step: bad args");
+  if (n == 0) return ADAPTSEG_OK;
+  double bc1 = 1.0 - std::pow((double)beta1, step);
+  double bc2 = 1.0 - std::pow((double)beta2, step);
+  float step_size = (float)((double)lr / bc1);
+  float bc2_sqrt = (float)std::sqrt(bc2);
+  adam_kernel<<<grid1d(n), 256, 0, as_stream(stream)>>>(n, param, grad, exp_avg, exp_avg_sq, beta1, beta2, eps,
+                                                        step_size, bc2_sqrt, grad_scale);
+  AS_CHECK_LAUNCH("adam");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_zero(void *ptr, size_t bytes, adaptseg_stream_t stream) {
+  if (bytes == 0) return ADAPTSEG_OK;
+  AS_CHECK_ARG(ptr, "zero: null pointer");
+  hipError_t e = hipMemsetAsync(ptr, 0, bytes, as_stream(stream));
+  if (e != hipSuccess) {
+    set_error("zero: %s", hipGetErrorString(e));
+    return ADAPTSEG_ERR_HIP;
+  }
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_to_nhwc(int n, int c, int h, int w, const int64_t *src_stride, const float *src, float *dst,
+                     adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && src_stride && src && dst, "to_nhwc: bad args");
+  Strides4 st;
+  for (int i = 0; i < 4; ++i) st.s[i] = src_stride[i];
+  int64_t total = (int64_t)n * c * h * w;
+  to_nhwc_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, st, src, dst);
+  AS_CHECK_LAUNCH("to_nhwc");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_axpy(int64_t n, float alpha, const float *src, float *dst, int flags, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n >= 0 && (n == 0 || (src && dst)), "axpy: bad args");
+  if (n == 0) return ADAPTSEG_OK;
+  axpy_kernel<<<grid1d(n), 256, 0, as_stream(stream)>>>(n, alpha, src, dst, (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  AS_CHECK_LAUNCH("axpy");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n >= 0 && (n == 0 || p), "add_i64: bad args");
+  if (n == 0) return ADAPTSEG_OK;
+  add_i64_kernel<<<grid1d(n), 256, 0, as_stream(stream)>>>(p, n, v);
+  AS_CHECK_LAUNCH("add_i64");
+  return ADAPTSEG_OK;
+}
+
+}  // extern "C"

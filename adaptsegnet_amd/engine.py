@@ -1,0 +1,327 @@
+"""Forward/backward programs of the DeeplabMulti generator and FCDiscriminator on the HIP kernels.
+
+Each public model (``model/deeplab_multi.py``, ``model/discriminator.py``) is ONE
+``torch.autograd.Function`` whose forward runs the whole network as a fixed program of
+native launches and whose backward replays it in reverse.  Owning the whole backward lets
+the engine
+
+* write weight gradients straight into the flat gradient arena (no per-parameter
+  AccumulateGrad adds),
+* fold residual-gradient sums into the data-gradient epilogue (``EPI_RESIDUAL`` /
+  ``EPI_ACCUMULATE``) and run BN backward in place, and
+* release each block's saved activations as soon as its backward is done.
+
+Reference semantics followed (file:line in /root/reference):
+  Bottleneck.forward                     model/deeplab_multi.py:83-103
+  Classifier_Module.forward (ASPP sum)   model/deeplab_multi.py:117-121
+  ResNetMulti.forward                    model/deeplab_multi.py:174-194
+  FCDiscriminator.forward                model/discriminator.py:21-34
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+# ---------------------------------------------------------------------------------------
+# BatchNorm (train: batch statistics; eval: running statistics)
+# ---------------------------------------------------------------------------------------
+
+
+def bn_forward(bn, x, res, relu, training):
+    if training:
+        y, mean, invstd = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                         bn.momentum, bn.eps, res=res, relu=relu)
+        return y, (mean, invstd, True)
+    y = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
+                       relu=relu)
+    return y, (bn.running_mean, None, False)
+
+
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None):
+    mean, invstd, train = st
+    if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
+        invstd = torch.rsqrt(bn.running_var + bn.eps)
+    return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train)
+
+
+# ---------------------------------------------------------------------------------------
+# Bottleneck
+# ---------------------------------------------------------------------------------------
+
+
+class BlockRec:
+    __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
+                 "n", "h", "w", "oh", "ow")
+
+
+def block_forward(blk, x, n, h, w, training, save):
+    g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
+    oh, ow = g1.out_hw(h, w)
+    c1 = K.conv_fwd(g1, x, n, h, w, [blk.conv1.weight])
+    y1, s1 = bn_forward(blk.bn1, c1, None, True, training)
+    c2 = K.conv_fwd(g2, y1, n, oh, ow, [blk.conv2.weight])
+    y2, s2 = bn_forward(blk.bn2, c2, None, True, training)
+    c3 = K.conv_fwd(g3, y2, n, oh, ow, [blk.conv3.weight])
+    cd = sd = None
+    if blk.downsample is not None:
+        dconv, dbn = blk.downsample[0], blk.downsample[1]
+        cd = K.conv_fwd(dconv.geom(), x, n, h, w, [dconv.weight])
+        r, sd = bn_forward(dbn, cd, None, False, training)
+    else:
+        r = x
+    out, s3 = bn_forward(blk.bn3, c3, r, True, training)
+    rec = None
+    if save:
+        rec = BlockRec()
+        rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
+        rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
+        rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
+    return out, rec
+
+
+def block_backward(blk, rec, gout, need_w):
+    """gout: grad of the block output (owned, modified in place).  Returns grad of the input."""
+    n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
+    g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
+    # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
+    dc3 = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout)
+    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight])
+    if need_w and blk.conv3.weight.grad is not None:
+        K.conv_wgrad(g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
+    del dc3
+    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2)
+    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
+    if need_w and blk.conv2.weight.grad is not None:
+        K.conv_wgrad(g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
+    del dy2
+    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1)
+    if need_w and blk.conv1.weight.grad is not None:
+        K.conv_wgrad(g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
+    if blk.downsample is not None:
+        dconv, dbn = blk.downsample[0], blk.downsample[1]
+        gd = dconv.geom()
+        bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout)
+        if need_w and dconv.weight.grad is not None:
+            K.conv_wgrad(gd, gout, rec.x, n, h, w, [dconv.weight.grad])
+        dx = K.conv_dgrad(gd, gout, n, h, w, [dconv.weight])
+        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE)
+    else:
+        # identity residual: dx = dgrad(conv1) + g, written over g in place
+        dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout)
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# ASPP classifier (4 dilated 3x3 branches summed = one 4-segment conv)
+# ---------------------------------------------------------------------------------------
+
+
+def aspp_geom(cls):
+    c0 = cls.conv2d_list[0]
+    return K.ConvGeom(c0.in_channels, c0.out_channels, 3, 3, 1,
+                      tuple(c.padding for c in cls.conv2d_list),
+                      tuple(c.dilation for c in cls.conv2d_list))
+
+
+def aspp_forward(cls, x, n, h, w):
+    return K.conv_fwd(aspp_geom(cls), x, n, h, w, [c.weight for c in cls.conv2d_list],
+                      [c.bias for c in cls.conv2d_list])
+
+
+def aspp_backward(cls, gy, x, n, h, w, need_w, gx_out=None):
+    g = aspp_geom(cls)
+    if need_w and cls.conv2d_list[0].weight.grad is not None:
+        K.conv_wgrad(g, gy, x, n, h, w, [c.weight.grad for c in cls.conv2d_list],
+                     [c.bias.grad for c in cls.conv2d_list])
+    if gx_out is None:
+        return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list])
+    return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list], out=gx_out,
+                        flags=K.EPI_ACCUMULATE)
+
+
+# ---------------------------------------------------------------------------------------
+# ResNetMulti
+# ---------------------------------------------------------------------------------------
+
+
+def _input_strides(x):
+    # (n, c, h, w) element strides of an NCHW-shaped tensor of any layout
+    return tuple(x.stride())
+
+
+class _DeeplabMultiFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, model, out_h, out_w, save):
+        ctx.set_materialize_grads(False)
+        training = model.training
+        n, c, h, w = x.shape
+        xs = _input_strides(x)
+        if training:
+            K.add_i64(model._bn_counter)
+        # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
+        gs = model.conv1.geom()
+        h0, w0 = gs.out_hw(h, w)
+        c0 = K.conv_fwd(gs, x, n, h, w, [model.conv1.weight], strides=xs)
+        y0, s0 = bn_forward(model.bn1, c0, None, True, training)
+        p, am = K.maxpool_fwd(y0)
+        ph, pw = p.shape[1], p.shape[2]
+        recs = []
+        cur, ch, cw = p, ph, pw
+        for layer in (model.layer1, model.layer2, model.layer3):
+            for blk in layer:
+                nh, nw = blk.conv1.geom().out_hw(ch, cw)
+                cur, rec = block_forward(blk, cur, n, ch, cw, training, save)
+                recs.append(rec)
+                ch, cw = nh, nw
+        p3, h3, w3 = cur, ch, cw
+        x1 = aspp_forward(model.layer5, p3, n, h3, w3)
+        q = p3
+        recs4 = []
+        for blk in model.layer4:
+            q, rec = block_forward(blk, q, n, h3, w3, training, save)
+            recs4.append(rec)
+        x2 = aspp_forward(model.layer6, q, n, h3, w3)
+        x1_up = K.upsample_fwd(x1, out_h, out_w)
+        x2_up = K.upsample_fwd(x2, out_h, out_w)
+        if save:
+            ctx.model = model
+            ctx.x = x
+            ctx.xs = xs
+            ctx.dims = (n, h, w, h0, w0, h3, w3)
+            ctx.stem = (c0, y0, s0, am)
+            ctx.recs, ctx.recs4 = recs, recs4
+            ctx.p3, ctx.q = p3, q
+            ctx.need_w = anchor.requires_grad
+        return K.as_nchw(x1_up), K.as_nchw(x2_up)
+
+    @staticmethod
+    def backward(ctx, g1_up, g2_up):
+        model = ctx.model
+        need_w = ctx.need_w
+        n, h, w, h0, w0, h3, w3 = ctx.dims
+        if need_w:
+            idx = list(model._pidx["trunk"])
+            if g2_up is not None:
+                idx += model._pidx["layer4"] + model._pidx["layer6"]
+            if g1_up is not None:
+                idx += model._pidx["layer5"]
+            model._arena.claim(idx)
+        gp3 = None
+        if g2_up is not None:
+            gx2 = K.upsample_bwd(K.nhwc_view(g2_up), h3, w3)
+            gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w)
+            del gx2
+            ctx.q = None
+            for i in reversed(range(len(model.layer4))):
+                gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w)
+                ctx.recs4[i] = None
+            gp3 = gq
+        if g1_up is not None:
+            gx1 = K.upsample_bwd(K.nhwc_view(g1_up), h3, w3)
+            gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3)
+            del gx1
+        ctx.p3 = None
+        if gp3 is None:
+            return None, None, None, None, None, None
+        blocks = [b for layer in (model.layer1, model.layer2, model.layer3) for b in layer]
+        g = gp3
+        for i in reversed(range(len(blocks))):
+            g = block_backward(blocks[i], ctx.recs[i], g, need_w)
+            ctx.recs[i] = None
+        c0, y0, s0, am = ctx.stem
+        ctx.stem = None
+        dy0 = K.maxpool_bwd(g, am, h0, w0)
+        del g
+        bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0)
+        gs = model.conv1.geom()
+        if need_w and model.conv1.weight.grad is not None:
+            K.conv_wgrad(gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
+        dx = None
+        if ctx.needs_input_grad[1]:
+            dx = K.as_nchw(K.conv_dgrad(gs, dy0, n, h, w, [model.conv1.weight]))
+        ctx.x = None
+        return None, dx, None, None, None, None
+
+
+def deeplab_multi_forward(model, x, input_size):
+    """ResNetMulti.forward(x, input_size) (model/deeplab_multi.py:174-194) on the HIP engine."""
+    if not x.is_cuda:
+        raise RuntimeError("adaptsegnet_amd DeeplabMulti runs on the HIP engine only; "
+                           f"got input on {x.device}")
+    if x.dtype != torch.float32:
+        raise RuntimeError(f"expected float32 input, got {x.dtype}")
+    model._ensure_arena(x.device)
+    need_w = any(p.requires_grad for p in model._arena.params)
+    grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
+    anchor = model._anchors[need_w]
+    out_w, out_h = int(input_size[0]), int(input_size[1])
+    return _DeeplabMultiFn.apply(anchor, x, model, out_h, out_w, grad)
+
+
+# ---------------------------------------------------------------------------------------
+# FCDiscriminator
+# ---------------------------------------------------------------------------------------
+
+
+class _FCDiscriminatorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, model, save):
+        ctx.set_materialize_grads(False)
+        convs = model._convs()
+        n, c, h, w = x.shape
+        xs = _input_strides(x)
+        acts, dims = [], []
+        cur, ch, cw, cs = x, h, w, xs
+        for i, conv in enumerate(convs):
+            g = conv.geom()
+            last = i == len(convs) - 1
+            out = K.conv_fwd(g, cur, n, ch, cw, [conv.weight], [conv.bias], strides=cs,
+                             flags=0 if last else K.EPI_LEAKY)
+            dims.append((ch, cw, cs))
+            acts.append(cur)
+            cur = out
+            ch, cw = g.out_hw(ch, cw)
+            cs = K.nhwc_strides(n, ch, cw, g.cout)
+        if save:
+            ctx.model, ctx.acts, ctx.dims, ctx.n = model, acts, dims, n
+            ctx.need_w = anchor.requires_grad
+        return K.as_nchw(cur)
+
+    @staticmethod
+    def backward(ctx, gout):
+        if gout is None:
+            return None, None, None, None
+        model, acts, dims, n = ctx.model, ctx.acts, ctx.dims, ctx.n
+        convs = model._convs()
+        need_w = ctx.need_w
+        if need_w:
+            model._arena.claim(model._pidx["all"])
+        g = K.nhwc_view(gout)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        dx = None
+        for i in reversed(range(len(convs))):
+            conv = convs[i]
+            geo = conv.geom()
+            ch, cw, cs = dims[i]
+            if need_w and conv.weight.grad is not None:
+                K.conv_wgrad(geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
+                             strides=cs)
+            if i > 0:
+                # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
+                g = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i])
+            elif ctx.needs_input_grad[1]:
+                dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight]))
+            acts[i] = None
+        return None, dx, None, None
+
+
+def discriminator_forward(model, x):
+    if not x.is_cuda:
+        raise RuntimeError("adaptsegnet_amd FCDiscriminator runs on the HIP engine only; "
+                           f"got input on {x.device}")
+    model._ensure_arena(x.device)
+    need_w = any(p.requires_grad for p in model._arena.params)
+    grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
+    return _FCDiscriminatorFn.apply(model._anchors[need_w], x, model, grad)

@@ -1,0 +1,387 @@
+"""Tensor-level wrappers over the C ABI (include/adaptseg.h).
+
+Activations handed to these functions are contiguous NHWC fp32 CUDA tensors of shape
+``[n, h, w, c]`` (the physical layout of a channels_last NCHW tensor) unless a function
+says otherwise.  Every call is asynchronous on the current HIP stream; none synchronises.
+These are the only functions that launch compute on the hot path — there is no CPU or
+eager-PyTorch fallback, and a missing ``libadaptseg.so`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
+                   EPI_LEAKY_GRAD, EPI_RESIDUAL, ConvDesc, check)
+
+__all__ = [
+    "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_fwd_train", "bn_fwd_infer", "bn_bwd",
+    "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
+    "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
+    "axpy", "add_i64", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RESIDUAL",
+]
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _require(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: expected a CUDA (HIP) tensor, got device {t.device}")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{what}: expected float32, got {t.dtype}")
+
+
+# ---------------------------------------------------------------------------------------
+# Workspace: one growing scratch buffer per (device, stream).  Ops on one stream run in
+# order, so reusing it across consecutive calls is race-free.
+# ---------------------------------------------------------------------------------------
+_WS: dict = {}
+
+
+def workspace(nbytes: int, device: torch.device) -> torch.Tensor | None:
+    if nbytes == 0:
+        return None
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        cap = max(nbytes, 0 if buf is None else int(buf.numel() * 1.25))
+        buf = torch.empty(cap, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _ws_args(nbytes: int, device):
+    w = workspace(nbytes, device)
+    return (ctypes.c_void_p(w.data_ptr()) if w is not None else None), ctypes.c_size_t(nbytes)
+
+
+# ---------------------------------------------------------------------------------------
+# Convolution
+# ---------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class ConvGeom:
+    """Static geometry of one (possibly multi-segment) convolution."""
+
+    cin: int
+    cout: int
+    kh: int
+    kw: int
+    stride: int = 1
+    pads: tuple = (0,)
+    dils: tuple = (1,)
+
+    @property
+    def nseg(self) -> int:
+        return len(self.pads)
+
+    def out_hw(self, h: int, w: int):
+        p, d = self.pads[0], self.dils[0]
+        oh = (h + 2 * p - d * (self.kh - 1) - 1) // self.stride + 1
+        ow = (w + 2 * p - d * (self.kw - 1) - 1) // self.stride + 1
+        return oh, ow
+
+    def flops(self, n: int, h: int, w: int) -> float:
+        oh, ow = self.out_hw(h, w)
+        return 2.0 * n * oh * ow * self.cout * self.cin * self.kh * self.kw * self.nseg
+
+
+_DESC_CACHE: dict = {}
+
+
+def _desc(g: ConvGeom, n, h, w, strides):
+    key = (g, n, h, w, strides)
+    d = _DESC_CACHE.get(key)
+    if d is None:
+        oh, ow = g.out_hw(h, w)
+        d = ConvDesc()
+        d.n, d.c, d.h, d.w = n, g.cin, h, w
+        for i in range(4):
+            d.in_stride[i] = strides[i]
+        d.k, d.oh, d.ow = g.cout, oh, ow
+        d.kh, d.kw, d.stride, d.nseg = g.kh, g.kw, g.stride, g.nseg
+        for i in range(g.nseg):
+            d.pad[i] = g.pads[i]
+            d.dil[i] = g.dils[i]
+        ws = {}
+        for op in (CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT):
+            b = ctypes.c_size_t(0)
+            check(_lib.lib().adaptseg_conv2d_workspace_size(ctypes.byref(d), op, ctypes.byref(b)),
+                  "conv2d_workspace_size")
+            ws[op] = b.value
+        d = (d, ws, oh, ow)
+        _DESC_CACHE[key] = d
+    return d
+
+
+def nhwc_strides(n, h, w, c):
+    """(n, c, h, w) element strides of a contiguous NHWC buffer."""
+    return (h * w * c, 1, w * c, c)
+
+
+def _ptrs(ts):
+    return _lib.ptr_array([None if t is None else t.data_ptr() for t in ts])
+
+
+def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, biases=None,
+             strides=None, out=None, res=None, flags: int = 0) -> torch.Tensor:
+    """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (leaky if EPI_LEAKY)."""
+    strides = strides or nhwc_strides(n, h, w, g.cin)
+    d, ws, oh, ow = _desc(g, n, h, w, tuple(strides))
+    if out is None:
+        out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
+    if res is not None:
+        flags |= EPI_RESIDUAL
+    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    check(_lib.lib().adaptseg_conv2d_fwd(
+        ctypes.byref(d), _p(x), _ptrs(weights), _ptrs(biases) if biases is not None else None,
+        _p(res), _p(out), flags, wp, wsz, _stream()), "conv2d_fwd")
+    return out
+
+
+def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
+               res=None, aux=None, flags: int = 0) -> torch.Tensor:
+    """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux))."""
+    d, ws, oh, ow = _desc(g, n, h, w, nhwc_strides(n, h, w, g.cin))
+    if out is None:
+        out = torch.empty((n, h, w, g.cin), device=dy.device, dtype=torch.float32)
+    if res is not None:
+        flags |= EPI_RESIDUAL
+    if aux is not None:
+        flags |= EPI_LEAKY_GRAD
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
+    check(_lib.lib().adaptseg_conv2d_bwd_data(
+        ctypes.byref(d), _p(dy), _ptrs(weights), _p(res), _p(aux), _p(out), flags, wp, wsz,
+        _stream()), "conv2d_bwd_data")
+    return out
+
+
+def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
+               dbs=None, strides=None, accumulate: bool = True) -> None:
+    """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy."""
+    strides = strides or nhwc_strides(n, h, w, g.cin)
+    d, ws, oh, ow = _desc(g, n, h, w, tuple(strides))
+    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dy.device)
+    check(_lib.lib().adaptseg_conv2d_bwd_weight(
+        ctypes.byref(d), _p(dy), _p(x), _ptrs(dws), _ptrs(dbs) if dbs is not None else None,
+        EPI_ACCUMULATE if accumulate else 0, wp, wsz, _stream()), "conv2d_bwd_weight")
+
+
+# ---------------------------------------------------------------------------------------
+# BatchNorm (x as [rows, C])
+# ---------------------------------------------------------------------------------------
+_BN_WS: dict = {}
+
+
+def _bn_ws(rows, c):
+    key = (rows, c)
+    v = _BN_WS.get(key)
+    if v is None:
+        b = ctypes.c_size_t(0)
+        check(_lib.lib().adaptseg_bn_workspace_size(rows, c, ctypes.byref(b)), "bn_workspace_size")
+        v = _BN_WS[key] = b.value
+    return v
+
+
+def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=None,
+                 relu=True, out=None):
+    rows, c = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    mean = torch.empty(c, device=x.device, dtype=torch.float32)
+    invstd = torch.empty(c, device=x.device, dtype=torch.float32)
+    wp, wsz = _ws_args(_bn_ws(rows, c), x.device)
+    check(_lib.lib().adaptseg_bn_fwd_train(
+        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
+        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), 1 if relu else 0,
+        wp, wsz, _stream()), "bn_fwd_train")
+    return y, mean, invstd
+
+
+def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None):
+    rows, c = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    check(_lib.lib().adaptseg_bn_fwd_infer(
+        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps),
+        _p(res), _p(y), 1 if relu else 0, _stream()), "bn_fwd_infer")
+    return y
+
+
+def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True):
+    """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy."""
+    rows, c = dy.numel() // dy.shape[-1], dy.shape[-1]
+    if dx is None:
+        dx = torch.empty_like(dy)
+    wp, wsz = _ws_args(_bn_ws(rows, c) if train else 0, dy.device)
+    check(_lib.lib().adaptseg_bn_bwd(
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(mean), _p(invstd), _p(dx), _p(dres),
+        1 if relu else 0, 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# Pooling / interpolation / softmax / losses
+# ---------------------------------------------------------------------------------------
+def maxpool_fwd(x, k=3, s=2, p=1):
+    n, h, w, c = x.shape
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    y = torch.empty((n, oh, ow, c), device=x.device, dtype=torch.float32)
+    am = torch.empty((n, oh, ow, c), device=x.device, dtype=torch.uint8)
+    check(_lib.lib().adaptseg_maxpool2d_fwd(n, c, h, w, oh, ow, k, s, p, _p(x), _p(y), _p(am),
+                                            _stream()), "maxpool2d_fwd")
+    return y, am
+
+
+def maxpool_bwd(dy, am, h, w, k=3, s=2, p=1):
+    n, oh, ow, c = dy.shape
+    dx = torch.empty((n, h, w, c), device=dy.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_maxpool2d_bwd(n, c, h, w, oh, ow, k, s, p, _p(dy), _p(am), _p(dx),
+                                            _stream()), "maxpool2d_bwd")
+    return dx
+
+
+def upsample_fwd(x, oh, ow):
+    n, h, w, c = x.shape
+    y = torch.empty((n, oh, ow, c), device=x.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_upsample_bilinear_fwd(n, c, h, w, oh, ow, _p(x), _p(y), _stream()),
+          "upsample_bilinear_fwd")
+    return y
+
+
+def upsample_bwd(dy, h, w, out=None, accumulate=False):
+    n, oh, ow, c = dy.shape
+    if out is None:
+        out = torch.empty((n, h, w, c), device=dy.device, dtype=torch.float32)
+    nbytes = n * oh * w * c * 4
+    wp, wsz = _ws_args(nbytes, dy.device)
+    check(_lib.lib().adaptseg_upsample_bilinear_bwd(
+        n, c, h, w, oh, ow, _p(dy), _p(out), EPI_ACCUMULATE if accumulate else 0, wp, wsz,
+        _stream()), "upsample_bilinear_bwd")
+    return out
+
+
+def softmax_fwd(x):
+    c = x.shape[-1]
+    y = torch.empty_like(x)
+    check(_lib.lib().adaptseg_softmax_fwd(x.numel() // c, c, _p(x), _p(y), _stream()),
+          "softmax_fwd")
+    return y
+
+
+def softmax_bwd(y, dy, out=None, accumulate=False):
+    c = y.shape[-1]
+    if out is None:
+        out = torch.empty_like(y)
+    check(_lib.lib().adaptseg_softmax_bwd(y.numel() // c, c, _p(y), _p(dy), _p(out),
+                                          EPI_ACCUMULATE if accumulate else 0, _stream()),
+          "softmax_bwd")
+    return out
+
+
+def ce_fwd(logits, labels, ignore=255, class_weight=None):
+    """Returns a 2-element device tensor [loss, denominator]."""
+    c = logits.shape[-1]
+    rows = logits.numel() // c
+    out = torch.empty(2, device=logits.device, dtype=torch.float32)
+    b = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_ce_workspace_size(rows, ctypes.byref(b)), "ce_workspace_size")
+    wp, wsz = _ws_args(b.value, logits.device)
+    check(_lib.lib().adaptseg_softmax_ce_fwd(rows, c, _p(logits), _p(labels), int(ignore),
+                                             _p(class_weight), _p(out), wp, wsz, _stream()),
+          "softmax_ce_fwd")
+    return out
+
+
+def ce_bwd(logits, labels, out2, grad_loss, ignore=255, class_weight=None, dl=None,
+           accumulate=False):
+    c = logits.shape[-1]
+    rows = logits.numel() // c
+    if dl is None:
+        dl = torch.empty_like(logits)
+    check(_lib.lib().adaptseg_softmax_ce_bwd(rows, c, _p(logits), _p(labels), int(ignore),
+                                             _p(class_weight), _p(out2), _p(grad_loss), _p(dl),
+                                             EPI_ACCUMULATE if accumulate else 0, _stream()),
+          "softmax_ce_bwd")
+    return dl
+
+
+def adv_fwd(x, target: float, kind: int):
+    n = x.numel()
+    loss = torch.empty(1, device=x.device, dtype=torch.float32)
+    b = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_adv_workspace_size(n, ctypes.byref(b)), "adv_workspace_size")
+    wp, wsz = _ws_args(b.value, x.device)
+    check(_lib.lib().adaptseg_adv_loss_fwd(n, _p(x), float(target), int(kind), _p(loss), wp, wsz,
+                                           _stream()), "adv_loss_fwd")
+    return loss
+
+
+def adv_bwd(x, target: float, kind: int, grad_loss, dx=None, accumulate=False):
+    if dx is None:
+        dx = torch.empty_like(x)
+    check(_lib.lib().adaptseg_adv_loss_bwd(x.numel(), _p(x), float(target), int(kind),
+                                           _p(grad_loss), _p(dx),
+                                           EPI_ACCUMULATE if accumulate else 0, _stream()),
+          "adv_loss_bwd")
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# Optimisers and plumbing
+# ---------------------------------------------------------------------------------------
+def sgd_step(param, grad, mom, lr, momentum, weight_decay, grad_scale=1.0, multiplicity=1,
+             first_step=False):
+    check(_lib.lib().adaptseg_sgd_step(param.numel(), _p(param), _p(grad), _p(mom), float(lr),
+                                       float(momentum), float(weight_decay), float(grad_scale),
+                                       int(multiplicity), 1 if first_step else 0, _stream()),
+          "sgd_step")
+
+
+def adam_step(param, grad, m, v, lr, beta1, beta2, eps, step, grad_scale=1.0):
+    check(_lib.lib().adaptseg_adam_step(param.numel(), _p(param), _p(grad), _p(m), _p(v),
+                                        float(lr), float(beta1), float(beta2), float(eps),
+                                        int(step), float(grad_scale), _stream()), "adam_step")
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    check(_lib.lib().adaptseg_zero(_p(t), t.numel() * t.element_size(), _stream()), "zero")
+    return t
+
+
+def to_nhwc(t: torch.Tensor) -> torch.Tensor:
+    """NCHW-shaped tensor (any strides) -> contiguous NHWC buffer [n, h, w, c]."""
+    _require(t, "to_nhwc")
+    n, c, h, w = t.shape
+    st = (ctypes.c_int64 * 4)(*t.stride())
+    out = torch.empty((n, h, w, c), device=t.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_to_nhwc(n, c, h, w, st, _p(t), _p(out), _stream()), "to_nhwc")
+    return out
+
+
+def axpy(alpha, src, dst, accumulate=True):
+    check(_lib.lib().adaptseg_axpy(src.numel(), float(alpha), _p(src), _p(dst),
+                                   EPI_ACCUMULATE if accumulate else 0, _stream()), "axpy")
+    return dst
+
+
+def add_i64(t: torch.Tensor, v: int = 1):
+    check(_lib.lib().adaptseg_add_i64(_p(t), t.numel(), int(v), _stream()), "add_i64")
+
+
+def nhwc_view(t: torch.Tensor) -> torch.Tensor:
+    """NCHW-shaped tensor -> its NHWC buffer (no copy if channels_last-contiguous)."""
+    if t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous():
+        return t.permute(0, 2, 3, 1)
+    return to_nhwc(t)
+
+
+def as_nchw(t: torch.Tensor) -> torch.Tensor:
+    """NHWC buffer [n, h, w, c] -> NCHW-shaped channels_last view."""
+    return t.permute(0, 3, 1, 2)

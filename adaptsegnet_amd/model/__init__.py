@@ -1,0 +1,2 @@
+from .deeplab_multi import DeeplabMulti, ResNetMulti, Bottleneck, Classifier_Module  # noqa: F401
+from .discriminator import FCDiscriminator  # noqa: F401

@@ -1,0 +1,213 @@
+"""The AdaptSegNet adversarial training step on the HIP engine (single- and multi-level).
+
+Restates the per-iteration body of /root/reference/train_gta2cityscapes_multi.py:
+  single-level  :379-464  (G: seg loss on source, adversarial loss on target through the
+                            frozen D2; D2: source -> 0, target -> 1, each loss / 2)
+  multi-level   :570-683  (two heads, two discriminators, loss_seg2 + lambda_seg*loss_seg1)
+  poly LR       :162-177,  SGD(momentum .9, wd 5e-4) + Adam(.9, .99)  :532-540
+Resolved reference gaps:
+  * the multi-level call ``model(images)`` (:597,615) lacks ``input_size`` and raises in the
+    reference; here source predictions are upsampled to ``input_size`` and target ones to
+    ``input_size_target`` (``target_size='target'``), or to the source size as the fork's
+    single-level branch does (:421, ``target_size='source'``, the single-level default);
+  * ``SOURCE_ONLY = True`` (:24) is not hard-wired: the adversarial step always runs;
+  * the fork's warper (:217-220,401-405) is out of scope.
+Differences that do not change results: loss scalings (``lambda * loss / iter_size``) are
+passed as the initial gradient of ``backward`` instead of multiplying the loss tensors, the
+constant label tensors (:621, ...) are folded into the loss kernels, and the per-loss
+``.item()`` host syncs are deferred to ``StepLosses.values()``.
+
+Data parallel (one process per GPU): every rank runs the step on its own shard, then ONE
+all-reduce (SUM) per parameter arena replaces DataParallel's gradient gather; the 1/world
+average is folded into the optimiser.  BN statistics stay per-rank, as in the reference's
+per-replica DataParallel semantics.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from . import functional as F
+from .optim import SGD, Adam, lr_poly
+
+
+@dataclass
+class StepConfig:
+    level: str = "single-level"          # or "multi-level"
+    gan: str = "Vanilla"                 # "Vanilla" (BCEWithLogits) or "LS" (MSE)
+    num_classes: int = 19
+    input_size: tuple = (1024, 512)      # (W, H) of source images
+    input_size_target: tuple = (1024, 512)
+    target_size: str = "auto"            # "source" | "target" | "auto" (single: source, multi: target)
+    iter_size: int = 1
+    learning_rate: float = 2.5e-4
+    learning_rate_D: float = 1e-4
+    momentum: float = 0.9
+    weight_decay: float = 5e-4
+    power: float = 0.9
+    num_steps: int = 250000
+    lambda_seg: float = 0.1
+    lambda_adv_target1: float = 0.0002
+    lambda_adv_target2: float = 0.001
+    ignore_label: int = 255
+
+
+@dataclass
+class StepLosses:
+    tensors: dict = field(default_factory=dict)
+
+    def add(self, name, t, scale):
+        self.tensors.setdefault(name, []).append((t, scale))
+
+    def values(self) -> dict:
+        """Host values (one device sync), summed like the reference's *_value accumulators."""
+        return {k: sum(float(t) * s for t, s in v) for k, v in self.tensors.items()}
+
+
+class AdaptSegTrainer:
+    """Owns the optimisers and runs one adversarial iteration per ``step()`` call."""
+
+    def __init__(self, model, model_D1, model_D2, cfg: StepConfig, process_group=None):
+        self.model, self.D1, self.D2, self.cfg = model, model_D1, model_D2, cfg
+        if cfg.level == "multi-level" and model_D1 is None:
+            raise ValueError("multi-level needs model_D1")
+        self.opt = SGD(model, cfg.learning_rate, cfg.momentum, cfg.weight_decay)
+        self.opt_D1 = Adam(model_D1, cfg.learning_rate_D, betas=(0.9, 0.99)) if model_D1 is not None else None
+        self.opt_D2 = Adam(model_D2, cfg.learning_rate_D, betas=(0.9, 0.99))
+        self.kind = F.BCE if cfg.gan == "Vanilla" else F.MSE
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self._consts = {}
+
+    # -- helpers -------------------------------------------------------------------------
+    def _c(self, v: float, device):
+        key = (float(v), device)
+        t = self._consts.get(key)
+        if t is None:
+            t = self._consts[key] = torch.full((), float(v), dtype=torch.float32, device=device)
+        return t
+
+    def _backward(self, losses, scales):
+        dev = losses[0].device
+        torch.autograd.backward(list(losses), grad_tensors=[self._c(s, dev) for s in scales])
+
+    @staticmethod
+    def _set_requires_grad(model, flag):
+        for p in model.parameters():
+            p.requires_grad = flag
+
+    def adjust_learning_rate(self, i_iter):
+        c = self.cfg
+        lr = lr_poly(c.learning_rate, i_iter, c.num_steps, c.power)
+        self.opt.param_groups[0]["lr"] = lr
+        self.opt.param_groups[1]["lr"] = lr * 10
+        lr_d = lr_poly(c.learning_rate_D, i_iter, c.num_steps, c.power)
+        for o in (self.opt_D1, self.opt_D2):
+            if o is not None:
+                o.param_groups[0]["lr"] = lr_d
+
+    def _target_size(self):
+        c = self.cfg
+        mode = c.target_size
+        if mode == "auto":
+            mode = "source" if c.level == "single-level" else "target"
+        return c.input_size if mode == "source" else c.input_size_target
+
+    def sync_gradients(self):
+        """SUM all-reduce of each parameter arena's gradients (RCCL on ROCm)."""
+        if self.world == 1:
+            return
+        for m in (self.model, self.D1, self.D2):
+            if m is not None and m.arena is not None:
+                dist.all_reduce(m.arena.grad, op=dist.ReduceOp.SUM, group=self.pg)
+
+    # -- the step --------------------------------------------------------------------------
+    def step(self, i_iter, batches):
+        """batches: iterable of ``iter_size`` tuples (images, labels, images_target)."""
+        c = self.cfg
+        L = StepLosses()
+        self.opt.zero_grad()
+        self.opt_D2.zero_grad()
+        if self.opt_D1 is not None:
+            self.opt_D1.zero_grad()
+        self.adjust_learning_rate(i_iter)
+        inv = 1.0 / c.iter_size
+        tsize = self._target_size()
+        for images, labels, images_t in batches:
+            if c.level == "single-level":
+                self._sub_single(images, labels, images_t, inv, tsize, L)
+            else:
+                self._sub_multi(images, labels, images_t, inv, tsize, L)
+        self.sync_gradients()
+        gs = 1.0 / self.world
+        self.opt.step(grad_scale=gs)
+        if self.opt_D1 is not None:
+            self.opt_D1.step(grad_scale=gs)
+        self.opt_D2.step(grad_scale=gs)
+        return L
+
+    def _sub_single(self, images, labels, images_t, inv, tsize, L):
+        """train_gta2cityscapes_multi.py:385-461."""
+        c, D2 = self.cfg, self.D2
+        self._set_requires_grad(D2, False)
+        _, pred2 = self.model(images, c.input_size)
+        loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
+        self._backward([loss_seg2], [inv])
+        L.add("loss_seg2", loss_seg2, inv)
+
+        _, pred_target2 = self.model(images_t, tsize)
+        d_out2 = D2(F.softmax2d(pred_target2))
+        loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
+        self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])
+        L.add("loss_adv_target2", loss_adv_target2, inv)
+
+        self._set_requires_grad(D2, True)
+        pred2 = pred2.detach()
+        loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
+        self._backward([loss_d2], [inv / 2])
+        L.add("loss_D2", loss_d2, inv / 2)
+        pred_target2 = pred_target2.detach()
+        loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+        self._backward([loss_d2], [inv / 2])
+        L.add("loss_D2", loss_d2, inv / 2)
+
+    def _sub_multi(self, images, labels, images_t, inv, tsize, L):
+        """train_gta2cityscapes_multi.py:578-679."""
+        c, D1, D2 = self.cfg, self.D1, self.D2
+        self._set_requires_grad(D1, False)
+        self._set_requires_grad(D2, False)
+        pred1, pred2 = self.model(images, c.input_size)
+        loss_seg1 = F.cross_entropy2d(pred1, labels, c.ignore_label)
+        loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
+        self._backward([loss_seg2, loss_seg1], [inv, c.lambda_seg * inv])
+        L.add("loss_seg1", loss_seg1, inv)
+        L.add("loss_seg2", loss_seg2, inv)
+
+        pred_target1, pred_target2 = self.model(images_t, tsize)
+        d_out1 = D1(F.softmax2d(pred_target1))
+        d_out2 = D2(F.softmax2d(pred_target2))
+        loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
+        loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
+        self._backward([loss_adv1, loss_adv2],
+                       [c.lambda_adv_target1 * inv, c.lambda_adv_target2 * inv])
+        L.add("loss_adv_target1", loss_adv1, inv)
+        L.add("loss_adv_target2", loss_adv2, inv)
+
+        self._set_requires_grad(D1, True)
+        self._set_requires_grad(D2, True)
+        pred1, pred2 = pred1.detach(), pred2.detach()
+        loss_d1 = F.adv_loss(D1(F.softmax2d(pred1)), 0.0, self.kind)
+        loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
+        self._backward([loss_d1], [inv / 2])
+        self._backward([loss_d2], [inv / 2])
+        L.add("loss_D1", loss_d1, inv / 2)
+        L.add("loss_D2", loss_d2, inv / 2)
+        pred_target1, pred_target2 = pred_target1.detach(), pred_target2.detach()
+        loss_d1 = F.adv_loss(D1(F.softmax2d(pred_target1)), 1.0, self.kind)
+        loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+        self._backward([loss_d1], [inv / 2])
+        self._backward([loss_d2], [inv / 2])
+        L.add("loss_D1", loss_d1, inv / 2)
+        L.add("loss_D2", loss_d2, inv / 2)

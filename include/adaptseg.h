@@ -1,0 +1,214 @@
+/*
+ * adaptseg.h — C ABI of the MI355X-native AdaptSegNet adversarial-step kernels.
+ *
+ * One shared library (adaptsegnet_amd/lib/libadaptseg.so), gfx950 only.  Every entry
+ * point takes plain device pointers, sizes and a hipStream_t (passed as void*), returns
+ * an int status (ADAPTSEG_OK = 0) and never throws.  No global allocation happens
+ * behind the caller's back: ops that need scratch take a caller-owned workspace whose
+ * size is reported by the matching *_workspace_size() call.  Nothing here synchronises
+ * the device, so every call is graph-capturable.
+ *
+ * Activation layout: NHWC fp32 ("channels_last" of the reference's NCHW tensors).
+ * Weight layout: [Cout][KH][KW][Cin] (= torch channels_last of the reference's
+ * [Cout][Cin][KH][KW] parameters, so state_dict shapes are unchanged).
+ *
+ * The reference (sahngmin/AdaptSegNet) is pure PyTorch; each entry point below names
+ * the torch.nn call site whose arithmetic it replaces.
+ */
+#ifndef ADAPTSEG_H
+#define ADAPTSEG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *adaptseg_stream_t; /* hipStream_t */
+
+enum adaptseg_status {
+  ADAPTSEG_OK = 0,
+  ADAPTSEG_ERR_ARG = 1,         /* bad shape / null pointer / misaligned */
+  ADAPTSEG_ERR_UNSUPPORTED = 2, /* valid request this build does not implement */
+  ADAPTSEG_ERR_HIP = 3,         /* launch or runtime error (see adaptseg_last_error) */
+  ADAPTSEG_ERR_WORKSPACE = 4    /* workspace smaller than *_workspace_size() */
+};
+
+/* Human-readable description of the last error raised on the calling thread. */
+const char *adaptseg_last_error(void);
+/* Library build string, e.g. "adaptseg 0.1 gfx950". */
+const char *adaptseg_version(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* Convolution (implicit GEMM on fp32 MFMA v_mfma_f32_32x32x2_f32).                      */
+/* Replaces nn.Conv2d in model/deeplab_multi.py:64,70-71,75,128,158-159 (Bottleneck,    */
+/* stem, downsample), Classifier_Module model/deeplab_multi.py:106-121 (ASPP: nseg=4    */
+/* branches summed into one GEMM with concatenated K) and model/discriminator.py:10-14.  */
+/* ------------------------------------------------------------------------------------ */
+typedef struct adaptseg_conv_desc {
+  int n, c, h, w;          /* input batch, channels, height, width                       */
+  int64_t in_stride[4];    /* input element strides for (n, c, h, w); NHWC = {HWC,1,WC,C} */
+  int k, oh, ow;           /* output channels and spatial size; output is NHWC-contiguous */
+  int kh, kw;              /* kernel size (same for every segment)                       */
+  int stride;              /* spatial stride (both dims)                                 */
+  int nseg;                /* 1, or the number of summed branches (ASPP: 4)              */
+  int pad[4];              /* per-segment padding (both dims)                            */
+  int dil[4];              /* per-segment dilation (both dims)                           */
+} adaptseg_conv_desc;
+
+enum adaptseg_conv_op { ADAPTSEG_CONV_FWD = 0, ADAPTSEG_CONV_BWD_DATA = 1, ADAPTSEG_CONV_BWD_WEIGHT = 2 };
+
+/* Epilogue flags (bitwise OR). */
+enum adaptseg_conv_flags {
+  ADAPTSEG_EPI_LEAKY = 1,      /* fwd: y = leaky_relu(y, 0.2)  (discriminator.py:21-29)    */
+  ADAPTSEG_EPI_ACCUMULATE = 2, /* out += result instead of out = result                    */
+  ADAPTSEG_EPI_LEAKY_GRAD = 4, /* bwd_data: dx *= (aux > 0 ? 1 : 0.2)                      */
+  ADAPTSEG_EPI_RESIDUAL = 8    /* out = result + res (same NHWC shape as out)              */
+};
+
+int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
+
+/* y[n,oh,ow,k] = sum_seg conv(x, w[seg]) + sum_seg bias[seg]   (bias may be NULL) */
+int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
+                        const float *const *bias, const float *res, float *y, int flags,
+                        void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+
+/* dx[n,h,w,c] = conv_transpose(dy, w)  (NHWC, contiguous).  aux: LEAKY_GRAD source. */
+int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
+                             const float *res, const float *aux, float *dx, int flags, void *ws,
+                             size_t ws_bytes, adaptseg_stream_t stream);
+
+/* dw[seg][k,kh,kw,c] (+)= sum_{n,oh,ow} dy * x_gathered; db[seg][k] (+)= sum dy.
+   db may be NULL.  Only ADAPTSEG_EPI_ACCUMULATE is honoured. */
+int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
+                               float *const *dw, float *const *db, int flags, void *ws,
+                               size_t ws_bytes, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* BatchNorm2d, train mode (batch statistics) with fused residual add and ReLU.          */
+/* Replaces nn.BatchNorm2d + ReLU + "out += residual" in model/deeplab_multi.py:65-101, */
+/* 130-134, 160 (affine params frozen, eps 1e-5, momentum 0.1).                          */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes);
+
+/* x,y: [rows][c].  Writes save_mean/save_invstd[c]; updates running stats (may be NULL).
+   y = (x-mean)*invstd*weight + bias (+ res) then ReLU if relu != 0. */
+int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight,
+                          const float *bias, float *running_mean, float *running_var,
+                          float momentum, float eps, float *save_mean, float *save_invstd,
+                          const float *res, float *y, int relu, void *ws, size_t ws_bytes,
+                          adaptseg_stream_t stream);
+
+/* Eval-mode BN (running statistics): y = (x-rm)/sqrt(rv+eps)*w + b (+res), ReLU if relu. */
+int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight,
+                          const float *bias, const float *running_mean, const float *running_var,
+                          float eps, const float *res, float *y, int relu,
+                          adaptseg_stream_t stream);
+
+/* Backward of bn_fwd_train.  g = dy * (relu ? (y > 0) : 1).
+   dx = weight*invstd*(g - mean(g) - xhat*mean(g*xhat)); dres = g if dres != NULL.
+   If train == 0 the eval-mode backward dx = g*weight*invstd is computed. */
+int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x,
+                    const float *weight, const float *save_mean, const float *save_invstd,
+                    float *dx, float *dres, int relu, int train, void *ws, size_t ws_bytes,
+                    adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* MaxPool2d (model/deeplab_multi.py:135: kernel 3, stride 2, pad 1, floor mode), NHWC.  */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_maxpool2d_fwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,
+                           const float *x, float *y, uint8_t *argmax, adaptseg_stream_t stream);
+int adaptseg_maxpool2d_bwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,
+                           const float *dy, const uint8_t *argmax, float *dx,
+                           adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* nn.Upsample(mode='bilinear', align_corners=True), NHWC (model/deeplab_multi.py:188). */
+/* The backward is a deterministic two-pass gather (no atomics).                         */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_upsample_workspace_size(int n, int c, int h, int w, int oh, int ow, size_t *bytes);
+int adaptseg_upsample_bilinear_fwd(int n, int c, int h, int w, int oh, int ow, const float *x,
+                                   float *y, adaptseg_stream_t stream);
+int adaptseg_upsample_bilinear_bwd(int n, int c, int h, int w, int oh, int ow, const float *dy,
+                                   float *dx, int flags, void *ws, size_t ws_bytes,
+                                   adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Channel softmax (F.softmax(pred), train_gta2cityscapes_multi.py:423,617-618), NHWC.   */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_softmax_fwd(int64_t rows, int c, const float *x, float *y, adaptseg_stream_t stream);
+int adaptseg_softmax_bwd(int64_t rows, int c, const float *y, const float *dy, float *dx,
+                         int flags, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Cross entropy over channels with ignore label (utils/loss.py:14-36 CrossEntropy2d;    */
+/* nn.CrossEntropyLoss(ignore_index=255), train_gta2cityscapes_multi.py:359,546).        */
+/* logits [rows][c], labels int64 [rows].  A label < 0 or == ignore is skipped.           */
+/* class_weight may be NULL.  out[0] = loss, out[1] = denominator (valid count or         */
+/* summed class weight).  All-ignored input gives NaN, as the reference does.            */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_ce_workspace_size(int64_t rows, size_t *bytes);
+int adaptseg_softmax_ce_fwd(int64_t rows, int c, const float *logits, const int64_t *labels,
+                            int ignore, const float *class_weight, float *out, void *ws,
+                            size_t ws_bytes, adaptseg_stream_t stream);
+/* dlogits = grad_loss[0] / out[1] * w[label] * (softmax - onehot); grad_loss, out on device */
+int adaptseg_softmax_ce_bwd(int64_t rows, int c, const float *logits, const int64_t *labels,
+                            int ignore, const float *class_weight, const float *out,
+                            const float *grad_loss, float *dlogits, int flags,
+                            adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Adversarial losses against a constant target (train_gta2cityscapes_multi.py:542-545, */
+/* 620-624, 648-650, 668-670): kind 0 = BCEWithLogitsLoss, 1 = MSELoss, mean reduction.  */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_adv_workspace_size(int64_t n, size_t *bytes);
+int adaptseg_adv_loss_fwd(int64_t n, const float *x, float target, int kind, float *loss,
+                          void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+int adaptseg_adv_loss_bwd(int64_t n, const float *x, float target, int kind,
+                          const float *grad_loss, float *dx, int flags, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Optimisers over flat fp32 arenas (train_gta2cityscapes_multi.py:532-540).             */
+/* ------------------------------------------------------------------------------------ */
+/* torch.optim.SGD(momentum, weight_decay, dampening 0, nesterov False) applied `multiplicity`
+   times in sequence, as torch does for a parameter listed that many times in its group
+   (the reference's get_1x_lr_params_NOscale yields block weights 3x and downsample weights
+   4x, model/deeplab_multi.py:216-222).  first_step != 0: no momentum buffer exists yet, so
+   every repetition starts from a fresh copy of its own d_p (torch's clone path).
+   grad is multiplied by grad_scale first (1/world for data-parallel averaging). */
+int adaptseg_sgd_step(int64_t n, float *param, const float *grad, float *mom, float lr,
+                      float momentum, float weight_decay, float grad_scale, int multiplicity,
+                      int first_step, adaptseg_stream_t stream);
+/* torch.optim.Adam(betas, eps, weight_decay 0, amsgrad False); step counts from 1. */
+int adaptseg_adam_step(int64_t n, float *param, const float *grad, float *exp_avg,
+                       float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
+                       int step, float grad_scale, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Plumbing kernels.                                                                      */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_zero(void *ptr, size_t bytes, adaptseg_stream_t stream);
+/* dst[n][h][w][c] = src(n, c, h, w) read through arbitrary element strides. */
+int adaptseg_to_nhwc(int n, int c, int h, int w, const int64_t *src_stride, const float *src,
+                     float *dst, adaptseg_stream_t stream);
+/* dst[i] += src[i] (or dst = src when flags lacks ADAPTSEG_EPI_ACCUMULATE). */
+int adaptseg_axpy(int64_t n, float alpha, const float *src, float *dst, int flags,
+                  adaptseg_stream_t stream);
+
+/* p[i] += v for i < n (BatchNorm num_batches_tracked counters, kept in one arena). */
+int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Live kernel timing for the benchmark: when enabled, every launch of the conv kernels   */
+/* of the selected class is bracketed by hipEvents on its stream; the summed durations   */
+/* and summed algorithmic FLOPs are read back after a device synchronise.                */
+/* class: 0 = all conv launches, 1 = 3x3 dilated convs (dil > 1, nseg == 1).             */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_timing_enable(int enable, int conv_class);
+int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADAPTSEG_H */

@@ -1,0 +1,356 @@
+"""TEST INFRASTRUCTURE ONLY — functional CPU restatement of the AdaptSegNet hot path.
+
+Stock PyTorch CPU ops over explicit name->tensor dicts whose keys are the reference's
+state_dict keys.  Runs in fp32 or fp64.  Used as the numerical checker for the HIP engine
+(tests/, __graft_entry__.smoke) and as the timed CPU baseline of bench.py.  Pinned against
+tests/golden/*.npz, which gen_golden.py captured from the reference modules themselves.
+
+Restated reference code (file:line in /root/reference):
+  DeeplabMulti / ResNetMulti layout            model/deeplab_multi.py:124-172, 258-260
+  Bottleneck.forward                           model/deeplab_multi.py:83-103
+  Classifier_Module.forward                    model/deeplab_multi.py:117-121
+  ResNetMulti.forward (+ bilinear upsample)    model/deeplab_multi.py:174-194
+  get_1x_lr_params_NOscale multiplicity        model/deeplab_multi.py:196-222
+  FCDiscriminator.forward                      model/discriminator.py:21-34
+  CrossEntropy2d.forward                       utils/loss.py:14-36
+  step bodies, losses, optimisers, poly LR     train_gta2cityscapes_multi.py:162-177,
+                                               355-359, 379-464, 532-546, 570-683
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+# (planes, blocks, stride, dilation) of layer1..layer4 — deeplab_multi.py:137-140, 259
+RESNET101 = ((64, 3, 1, 1), (128, 4, 2, 1), (256, 23, 1, 2), (512, 3, 1, 4))
+ASPP_RATES = (6, 12, 18, 24)  # deeplab_multi.py:141-142
+BN_EPS, BN_MOMENTUM = 1e-5, 0.1
+
+
+# ---------------------------------------------------------------------------------------
+# Parameter specs and deterministic values
+# ---------------------------------------------------------------------------------------
+
+
+def g_specs(num_classes=19, layout=RESNET101):
+    """[(state_dict key, shape, kind)] of DeeplabMulti in registration order."""
+    out = []
+
+    def conv(key, co, ci, k, bias=False):
+        out.append((key + ".weight", (co, ci, k, k), "conv"))
+        if bias:
+            out.append((key + ".bias", (co,), "bias"))
+
+    def bn(key, c):
+        out.extend([(key + ".weight", (c,), "bn_w"), (key + ".bias", (c,), "bn_b"),
+                    (key + ".running_mean", (c,), "bn_rm"), (key + ".running_var", (c,), "bn_rv"),
+                    (key + ".num_batches_tracked", (), "bn_n")])
+
+    conv("conv1", 64, 3, 7)
+    bn("bn1", 64)
+    cin = 64
+    for li, (planes, nblk, _stride, _dil) in enumerate(layout, 1):
+        for b in range(nblk):
+            pre = f"layer{li}.{b}."
+            bin_ = cin if b == 0 else planes * 4
+            conv(pre + "conv1", planes, bin_, 1)
+            bn(pre + "bn1", planes)
+            conv(pre + "conv2", planes, planes, 3)
+            bn(pre + "bn2", planes)
+            conv(pre + "conv3", planes * 4, planes, 1)
+            bn(pre + "bn3", planes * 4)
+            if b == 0:
+                conv(pre + "downsample.0", planes * 4, bin_, 1)
+                bn(pre + "downsample.1", planes * 4)
+        cin = planes * 4
+    for li, ci in ((5, 1024), (6, 2048)):
+        for r in range(len(ASPP_RATES)):
+            conv(f"layer{li}.conv2d_list.{r}", num_classes, ci, 3, bias=True)
+    return out
+
+
+def d_specs(num_classes=19, ndf=64):
+    chans = (num_classes, ndf, ndf * 2, ndf * 4, ndf * 8, 1)
+    names = ("conv1", "conv2", "conv3", "conv4", "classifier")
+    out = []
+    for i, nm in enumerate(names):
+        out.append((nm + ".weight", (chans[i + 1], chans[i], 4, 4), "dconv"))
+        out.append((nm + ".bias", (chans[i + 1],), "dbias"))
+    return out
+
+
+def det_state(specs, seed, conv_std=0.01, bn_random=True):
+    """Deterministic numpy values (PCG64) for every spec; identical on every machine."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = {}
+    for key, shape, kind in specs:
+        if kind == "conv":
+            v = rng.normal(0.0, conv_std, shape)
+        elif kind == "bias":
+            fan_in = None
+            v = rng.uniform(-0.05, 0.05, shape)
+        elif kind in ("dconv", "dbias"):
+            wshape = [s for k2, s, kd in specs if k2 == key.rsplit(".", 1)[0] + ".weight"][0]
+            bound = 1.0 / np.sqrt(wshape[1] * wshape[2] * wshape[3])
+            v = rng.uniform(-bound, bound, shape)
+        elif kind == "bn_w":
+            v = 1.0 + (0.1 * rng.standard_normal(shape) if bn_random else 0.0 * np.zeros(shape))
+        elif kind == "bn_b":
+            v = 0.1 * rng.standard_normal(shape) if bn_random else np.zeros(shape)
+        elif kind == "bn_rm":
+            v = 0.1 * rng.standard_normal(shape) if bn_random else np.zeros(shape)
+        elif kind == "bn_rv":
+            v = 1.0 + 0.2 * rng.uniform(0, 1, shape) if bn_random else np.ones(shape)
+        elif kind == "bn_n":
+            v = np.zeros(shape, dtype=np.int64)
+        else:  # pragma: no cover
+            raise ValueError(kind)
+        sd[key] = np.asarray(v, dtype=np.int64 if kind == "bn_n" else np.float64)
+    return sd
+
+
+def det_images(shape, seed):
+    """Mean-subtracted BGR-like pixels (train_gta2cityscapes_multi.py:30): U[-122.7, 151]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return rng.uniform(-122.7, 151.0, shape)
+
+
+def det_labels(shape, seed, num_classes=19, ignore_frac=0.1, ignore=255):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lab = rng.integers(0, num_classes, shape)
+    lab[rng.uniform(0, 1, shape) < ignore_frac] = ignore
+    return lab.astype(np.int64)
+
+
+def to_torch(sd, dtype=torch.float64, trainable=None):
+    """numpy state -> torch dict; float entries become leaves (requires_grad per `trainable`)."""
+    out = {}
+    for k, v in sd.items():
+        if v.dtype == np.int64:
+            out[k] = torch.from_numpy(v.copy())
+        else:
+            t = torch.from_numpy(v.copy()).to(dtype)
+            if trainable is not None and trainable(k):
+                t.requires_grad_(True)
+            out[k] = t
+    return out
+
+
+def g_trainable(key):
+    """BN affine parameters are frozen (deeplab_multi.py:66-78,131-132,161-162)."""
+    if ".running_" in key or key.endswith("num_batches_tracked"):
+        return False
+    parts = key.split(".")
+    mod = parts[-2]
+    is_bn = mod.startswith("bn") or (mod == "1" and "downsample" in key)
+    return not is_bn
+
+
+# ---------------------------------------------------------------------------------------
+# Forward passes
+# ---------------------------------------------------------------------------------------
+
+
+def _bn(x, P, key, train):
+    if train:
+        P[key + ".num_batches_tracked"] += 1
+    return F.batch_norm(x, P[key + ".running_mean"], P[key + ".running_var"], P[key + ".weight"],
+                        P[key + ".bias"], train, BN_MOMENTUM, BN_EPS)
+
+
+def _bottleneck(y, P, pre, stride, dil, has_ds, train):
+    """deeplab_multi.py:83-103 — the stride sits on the first 1x1 conv (:64)."""
+    t = F.conv2d(y, P[pre + "conv1.weight"], None, stride)
+    t = F.relu(_bn(t, P, pre + "bn1", train))
+    t = F.conv2d(t, P[pre + "conv2.weight"], None, 1, dil, dil)
+    t = F.relu(_bn(t, P, pre + "bn2", train))
+    t = _bn(F.conv2d(t, P[pre + "conv3.weight"]), P, pre + "bn3", train)
+    if has_ds:
+        sc = _bn(F.conv2d(y, P[pre + "downsample.0.weight"], None, stride), P,
+                 pre + "downsample.1", train)
+    else:
+        sc = y
+    return F.relu(t + sc)
+
+
+def _aspp(y, P, pre, rates=ASPP_RATES):
+    """deeplab_multi.py:117-121: branch 0, then += branches 1..3 (padding = dilation)."""
+    out = None
+    for r_i, r in enumerate(rates):
+        b = F.conv2d(y, P[f"{pre}.conv2d_list.{r_i}.weight"], P[f"{pre}.conv2d_list.{r_i}.bias"],
+                     1, r, r)
+        out = b if out is None else out + b
+    return out
+
+
+def g_forward(P, x, input_size, train=True, layout=RESNET101):
+    """ResNetMulti.forward(x, input_size) — deeplab_multi.py:174-194. input_size = (W, H)."""
+    y = F.conv2d(x, P["conv1.weight"], None, 2, 3)
+    y = F.relu(_bn(y, P, "bn1", train))
+    y = F.max_pool2d(y, 3, 2, 1, ceil_mode=False)
+    x1 = None
+    for li, (planes, nblk, stride, dil) in enumerate(layout, 1):
+        if li == 4:
+            x1 = _aspp(y, P, "layer5")
+        for b in range(nblk):
+            y = _bottleneck(y, P, f"layer{li}.{b}.", stride if b == 0 else 1, dil, b == 0, train)
+    x2 = _aspp(y, P, "layer6")
+    size = (int(input_size[1]), int(input_size[0]))
+    up = lambda t: F.interpolate(t, size=size, mode="bilinear", align_corners=True)  # noqa: E731
+    return up(x1), up(x2)
+
+
+def d_forward(Q, x, slope=0.2):
+    """FCDiscriminator.forward — discriminator.py:21-34 (4x4/2 convs, LeakyReLU 0.2)."""
+    for nm in ("conv1", "conv2", "conv3", "conv4"):
+        x = F.leaky_relu(F.conv2d(x, Q[nm + ".weight"], Q[nm + ".bias"], 2, 1), slope)
+    return F.conv2d(x, Q["classifier.weight"], Q["classifier.bias"], 2, 1)
+
+
+# ---------------------------------------------------------------------------------------
+# Losses
+# ---------------------------------------------------------------------------------------
+
+
+def cross_entropy2d(predict, target, ignore_label=255, weight=None):
+    """utils/loss.py:14-36: keep pixels with 0 <= target != ignore, mean cross entropy."""
+    n, c, h, w = predict.shape
+    keep = (target >= 0) & (target != ignore_label)
+    logits = predict.permute(0, 2, 3, 1)[keep]
+    return F.cross_entropy(logits, target[keep], weight=weight)
+
+
+def adv_loss(d_out, label, gan):
+    """BCEWithLogitsLoss / MSELoss against a constant label — train:542-545, 620-624."""
+    tgt = torch.full_like(d_out, float(label))
+    if gan == "Vanilla":
+        return F.binary_cross_entropy_with_logits(d_out, tgt)
+    return F.mse_loss(d_out, tgt)
+
+
+# ---------------------------------------------------------------------------------------
+# Optimisers and the step
+# ---------------------------------------------------------------------------------------
+
+
+def lr_poly(base_lr, it, max_iter, power):
+    return base_lr * ((1 - float(it) / max_iter) ** power)
+
+
+def g_param_multiplicity(key):
+    """How often get_1x_lr_params_NOscale yields a parameter (deeplab_multi.py:216-222):
+    it walks modules() of conv1, bn1, layer1..4 and takes the RECURSIVE parameters() of
+    each, so a weight is yielded once per ancestor inside its layerN."""
+    if key.startswith("layer5") or key.startswith("layer6") or key == "conv1.weight":
+        return 1
+    return 4 if ".downsample." in key else 3
+
+
+def make_optimizers(G, D1, D2, cfg):
+    """SGD(optim_parameters) + Adam x2 — train:532-540 (duplicate params, like the reference)."""
+    g0, g1 = [], []
+    for k, t in G.items():
+        if not (isinstance(t, torch.Tensor) and t.requires_grad):
+            continue
+        if k.startswith("layer5") or k.startswith("layer6"):
+            g1.append(t)
+        else:
+            g0.extend([t] * g_param_multiplicity(k))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        opt = torch.optim.SGD([{"params": g0, "lr": cfg["learning_rate"]},
+                               {"params": g1, "lr": 10 * cfg["learning_rate"]}],
+                              lr=cfg["learning_rate"], momentum=cfg["momentum"],
+                              weight_decay=cfg["weight_decay"], foreach=False)
+    mk = lambda Q: torch.optim.Adam([t for t in Q.values() if t.requires_grad],  # noqa: E731
+                                    lr=cfg["learning_rate_D"], betas=(0.9, 0.99), foreach=False)
+    return opt, (mk(D1) if D1 is not None else None), mk(D2)
+
+
+DEFAULT_CFG = dict(level="single-level", gan="Vanilla", learning_rate=2.5e-4, learning_rate_D=1e-4,
+                   momentum=0.9, weight_decay=5e-4, power=0.9, num_steps=250000, lambda_seg=0.1,
+                   lambda_adv_target1=2e-4, lambda_adv_target2=1e-3, iter_size=1,
+                   input_size=(1024, 512), input_size_target=(1024, 512), target_size="auto")
+
+
+def _set_rg(Q, flag):
+    for t in Q.values():
+        t.requires_grad_(flag)
+
+
+def oracle_step(G, D1, D2, opts, cfg, i_iter, batches):
+    """One iteration of train_gta2cityscapes_multi.py:373-464 (single) or :560-683 (multi).
+
+    Returns a dict of host loss values accumulated like the reference's *_value sums.
+    """
+    opt, opt_d1, opt_d2 = opts
+    c = dict(DEFAULT_CFG)
+    c.update(cfg)
+    vals = {}
+
+    def acc(name, v):
+        vals[name] = vals.get(name, 0.0) + float(v)
+
+    opt.zero_grad()
+    lr = lr_poly(c["learning_rate"], i_iter, c["num_steps"], c["power"])
+    opt.param_groups[0]["lr"], opt.param_groups[1]["lr"] = lr, lr * 10
+    lr_d = lr_poly(c["learning_rate_D"], i_iter, c["num_steps"], c["power"])
+    for o in (opt_d1, opt_d2):
+        if o is not None:
+            o.zero_grad()
+            o.param_groups[0]["lr"] = lr_d
+    n_sub = c["iter_size"]
+    tmode = c["target_size"]
+    if tmode == "auto":
+        tmode = "source" if c["level"] == "single-level" else "target"
+    tsize = c["input_size"] if tmode == "source" else c["input_size_target"]
+    src_lbl, tgt_lbl = 0, 1
+    for images, labels, images_t in batches:
+        if c["level"] == "single-level":
+            _set_rg(D2, False)
+            _, pred2 = g_forward(G, images, c["input_size"])
+            loss_seg2 = F.cross_entropy(pred2, labels, ignore_index=255)
+            (loss_seg2 / n_sub).backward()
+            acc("loss_seg2", loss_seg2.item() / n_sub)
+            _, pred_t2 = g_forward(G, images_t, tsize)
+            l_adv = adv_loss(d_forward(D2, F.softmax(pred_t2, dim=1)), src_lbl, c["gan"])
+            (c["lambda_adv_target2"] * l_adv / n_sub).backward()
+            acc("loss_adv_target2", l_adv.item() / n_sub)
+            _set_rg(D2, True)
+            for pred, lbl in ((pred2.detach(), src_lbl), (pred_t2.detach(), tgt_lbl)):
+                l_d = adv_loss(d_forward(D2, F.softmax(pred, dim=1)), lbl, c["gan"]) / n_sub / 2
+                l_d.backward()
+                acc("loss_D2", l_d.item())
+        else:
+            _set_rg(D1, False)
+            _set_rg(D2, False)
+            pred1, pred2 = g_forward(G, images, c["input_size"])
+            loss_seg1 = F.cross_entropy(pred1, labels, ignore_index=255)
+            loss_seg2 = F.cross_entropy(pred2, labels, ignore_index=255)
+            ((loss_seg2 + c["lambda_seg"] * loss_seg1) / n_sub).backward()
+            acc("loss_seg1", loss_seg1.item() / n_sub)
+            acc("loss_seg2", loss_seg2.item() / n_sub)
+            pt1, pt2 = g_forward(G, images_t, tsize)
+            a1 = adv_loss(d_forward(D1, F.softmax(pt1, dim=1)), src_lbl, c["gan"])
+            a2 = adv_loss(d_forward(D2, F.softmax(pt2, dim=1)), src_lbl, c["gan"])
+            ((c["lambda_adv_target1"] * a1 + c["lambda_adv_target2"] * a2) / n_sub).backward()
+            acc("loss_adv_target1", a1.item() / n_sub)
+            acc("loss_adv_target2", a2.item() / n_sub)
+            _set_rg(D1, True)
+            _set_rg(D2, True)
+            for (p1, p2), lbl in (((pred1.detach(), pred2.detach()), src_lbl),
+                                  ((pt1.detach(), pt2.detach()), tgt_lbl)):
+                l1 = adv_loss(d_forward(D1, F.softmax(p1, dim=1)), lbl, c["gan"]) / n_sub / 2
+                l2 = adv_loss(d_forward(D2, F.softmax(p2, dim=1)), lbl, c["gan"]) / n_sub / 2
+                l1.backward()
+                l2.backward()
+                acc("loss_D1", l1.item())
+                acc("loss_D2", l2.item())
+    opt.step()
+    if opt_d1 is not None:
+        opt_d1.step()
+    opt_d2.step()
+    return vals

@@ -1,0 +1,308 @@
+"""GPU parity of every HIP kernel against the fp64 CPU oracle (torch CPU ops).
+
+Tolerances (stated per op): the kernels compute in fp32 (fp32 MFMA = an exact fp32 fmaf
+chain), the oracle in fp64.  Convolutions: max|err| <= 2e-5 * max|ref| (K up to 36*2048);
+pointwise / reductions: <= 1e-5 relative; integer-exact where the op is a selection
+(max-pool argmax routing).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def K():
+    from adaptsegnet_amd import kernels
+    return kernels
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def nhwc(t):  # NCHW cpu -> NHWC contiguous cuda fp32
+    return t.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+
+
+def nchw(t):  # NHWC cuda -> NCHW cpu fp64
+    return t.permute(0, 3, 1, 2).double().cpu()
+
+
+def w_cl(w):  # [co,ci,kh,kw] cpu -> device [co,kh,kw,ci] contiguous
+    return w.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+
+
+CONV_CASES = [
+    # (n, cin, h, w, cout, k, stride, pads, dils, bias)
+    (2, 64, 17, 23, 256, 1, 1, (0,), (1,), False),        # bottleneck conv1/conv3 (1x1)
+    (2, 256, 17, 23, 128, 1, 2, (0,), (1,), False),       # layer2 stride-2 1x1
+    (2, 64, 15, 21, 64, 3, 1, (1,), (1,), False),         # layer1 3x3
+    (2, 128, 13, 11, 128, 3, 1, (2,), (2,), False),       # layer3 atrous d2
+    (1, 256, 9, 12, 256, 3, 1, (4,), (4,), False),        # layer4 atrous d4
+    (2, 3, 37, 45, 64, 7, 2, (3,), (1,), False),          # stem 7x7/2
+    (2, 19, 32, 40, 64, 4, 2, (1,), (1,), True),          # D conv1 (Cin 19)
+    (2, 64, 16, 20, 128, 4, 2, (1,), (1,), True),         # D conv2
+    (2, 128, 6, 8, 1, 4, 2, (1,), (1,), True),            # D classifier (Cout 1)
+    (2, 64, 7, 9, 19, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP, dil > spatial
+    (1, 2048, 3, 5, 7, 1, 1, (0,), (1,), False),          # split-K path (M=15, K=2048)
+]
+
+
+def _ref_conv(x, ws, bs, stride, pads, dils):
+    out = None
+    for i, (p, d) in enumerate(zip(pads, dils)):
+        y = F.conv2d(x, ws[i], bs[i] if bs is not None else None, stride, p, d)
+        out = y if out is None else out + y
+    return out
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{i}" for i in range(len(CONV_CASES))])
+def test_conv_fwd_dgrad_wgrad(case):
+    k = K()
+    n, cin, h, w, cout, ks, stride, pads, dils, bias = case
+    g = torch.Generator().manual_seed(hash(case) % (2 ** 31))
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    nseg = len(pads)
+    ws = [torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.1 for _ in range(nseg)]
+    bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in range(nseg)] if bias else None
+    xr = x.clone().requires_grad_(True)
+    wr = [t.clone().requires_grad_(True) for t in ws]
+    br = [t.clone().requires_grad_(True) for t in bs] if bias else None
+    ref = _ref_conv(xr, wr, br, stride, pads, dils)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+
+    geom = k.ConvGeom(cin, cout, ks, ks, stride, pads, dils)
+    xd = nhwc(x)
+    wd = [w_cl(t) for t in ws]
+    bd = [t.float().to(DEV) for t in bs] if bias else None
+    y = k.conv_fwd(geom, xd, n, h, w, wd, bd)
+    assert rel(nchw(y), ref) < 2e-5
+    # NCHW-strided input (the stem reads the user's NCHW tensor directly)
+    xc = x.float().to(DEV).contiguous()
+    y2 = k.conv_fwd(geom, xc, n, h, w, wd, bd, strides=tuple(xc.stride()))
+    assert rel(nchw(y2), ref) < 2e-5
+
+    gyd = nhwc(gy)
+    dx = k.conv_dgrad(geom, gyd, n, h, w, wd)
+    assert rel(nchw(dx), xr.grad) < 2e-5
+    dws = [torch.zeros_like(t) for t in wd]
+    dbs = [torch.zeros(cout, device=DEV) for _ in range(nseg)] if bias else None
+    k.conv_wgrad(geom, gyd, xd, n, h, w, dws, dbs)
+    for i in range(nseg):
+        assert rel(dws[i].permute(0, 3, 1, 2).cpu(), wr[i].grad) < 2e-5
+        if bias:
+            assert rel(dbs[i].cpu(), br[i].grad) < 1e-5
+    # accumulate: a second wgrad doubles the result
+    k.conv_wgrad(geom, gyd, xd, n, h, w, dws, dbs, accumulate=True)
+    assert rel(dws[0].permute(0, 3, 1, 2).cpu(), 2 * wr[0].grad) < 2e-5
+
+
+def test_conv_epilogues():
+    k = K()
+    g = torch.Generator().manual_seed(5)
+    n, cin, h, w, cout = 2, 32, 10, 12, 64
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    geom = k.ConvGeom(cin, cout, 4, 4, 2, (1,), (1,))
+    y = k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)], [b.float().to(DEV)], flags=k.EPI_LEAKY)
+    ref = F.leaky_relu(F.conv2d(x, wt, b, 2, 1), 0.2)
+    assert rel(nchw(y), ref) < 2e-5
+    # residual + accumulate on dgrad, leaky-grad multiplier
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, wt, None, 2, 1).backward(gy)
+    res = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    out = nhwc(res)
+    k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)], out=out, res=out)
+    assert rel(nchw(out), xr.grad + res) < 2e-5
+    out2 = nhwc(res)
+    k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)], out=out2, flags=k.EPI_ACCUMULATE)
+    assert rel(nchw(out2), xr.grad + res) < 2e-5
+    aux = nhwc(res)
+    dxl = k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)], aux=aux)
+    assert rel(nchw(dxl), xr.grad * torch.where(res > 0, 1.0, 0.2)) < 2e-5
+
+
+@pytest.mark.parametrize("relu,with_res", [(True, False), (False, False), (True, True)])
+def test_batchnorm_train(relu, with_res):
+    k = K()
+    g = torch.Generator().manual_seed(7)
+    n, c, h, w = 3, 64, 9, 11
+    x = (torch.randn(n, c, h, w, generator=g, dtype=torch.float64) * 3 + 5)
+    wt = 1 + 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    b = 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    rm, rv = torch.zeros(c, dtype=torch.float64), torch.ones(c, dtype=torch.float64)
+    res = torch.randn(n, c, h, w, generator=g, dtype=torch.float64) if with_res else None
+    xr = x.clone().requires_grad_(True)
+    y = F.batch_norm(xr, rm, rv, wt, b, True, 0.1, 1e-5)
+    if with_res:
+        y = y + res
+    if relu:
+        y = F.relu(y)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy)
+    xd = nhwc(x)
+    rmd, rvd = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    yd, mean, invstd = k.bn_fwd_train(xd, wt.float().to(DEV), b.float().to(DEV), rmd, rvd, 0.1, 1e-5,
+                                      res=nhwc(res) if with_res else None, relu=relu)
+    assert rel(nchw(yd), y) < 1e-5
+    assert rel(rmd.cpu(), rm) < 1e-5 and rel(rvd.cpu(), rv) < 1e-5
+    gyd = nhwc(gy)
+    dres = torch.empty_like(gyd) if with_res else None
+    dx = k.bn_bwd(gyd, yd, xd, wt.float().to(DEV), mean, invstd, relu=relu, dres=dres)
+    assert rel(nchw(dx), xr.grad) < 1e-5
+    if with_res:
+        assert rel(nchw(dres), gy * (y > 0)) < 1e-6
+
+
+def test_batchnorm_eval_and_inplace_bwd():
+    k = K()
+    g = torch.Generator().manual_seed(8)
+    n, c, h, w = 2, 32, 5, 7
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    wt = 1 + 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    b = 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    rm = 0.1 * torch.randn(c, generator=g, dtype=torch.float64)
+    rv = 1 + 0.2 * torch.rand(c, generator=g, dtype=torch.float64)
+    ref = F.relu(F.batch_norm(x, rm, rv, wt, b, False, 0.1, 1e-5))
+    yd = k.bn_fwd_infer(nhwc(x), wt.float().to(DEV), b.float().to(DEV), rm.float().to(DEV),
+                        rv.float().to(DEV), 1e-5, relu=True)
+    assert rel(nchw(yd), ref) < 1e-5
+    # in-place train backward (dx aliases dy)
+    xr = x.clone().requires_grad_(True)
+    y = F.relu(F.batch_norm(xr, None, None, wt, b, True, 0.1, 1e-5))
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy)
+    xd = nhwc(x)
+    yd, mean, invstd = k.bn_fwd_train(xd, wt.float().to(DEV), b.float().to(DEV), None, None, 0.1, 1e-5)
+    gyd = nhwc(gy)
+    k.bn_bwd(gyd, yd, xd, wt.float().to(DEV), mean, invstd, relu=True, dx=gyd)
+    assert rel(nchw(gyd), xr.grad) < 1e-5
+
+
+def test_maxpool():
+    k = K()
+    g = torch.Generator().manual_seed(9)
+    x = F.relu(torch.randn(2, 64, 21, 29, generator=g, dtype=torch.float64))  # ties at 0
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 3, 2, 1)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy)
+    yd, am = k.maxpool_fwd(nhwc(x))
+    assert torch.equal(nchw(yd).float(), y.detach().float())
+    dx = k.maxpool_bwd(nhwc(gy), am, 21, 29)
+    # gradient routing is exact wherever the max is unique (>0); zero ties only feed ReLU zeros
+    mask = (x > 0)
+    assert rel(nchw(dx) * mask, xr.grad * mask) < 1e-6
+
+
+@pytest.mark.parametrize("hw,out", [((9, 13), (65, 97)), ((64, 128), (512, 1024)),
+                                    ((90, 160), (720, 1280)), ((1, 5), (3, 9)), ((7, 7), (7, 7))])
+def test_upsample(hw, out):
+    k = K()
+    g = torch.Generator().manual_seed(10)
+    n, c = 2, 19
+    x = torch.randn(n, c, *hw, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    y = F.interpolate(xr, size=out, mode="bilinear", align_corners=True)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy)
+    yd = k.upsample_fwd(nhwc(x), *out)
+    assert rel(nchw(yd), y) < 1e-5
+    dx = k.upsample_bwd(nhwc(gy), *hw)
+    assert rel(nchw(dx), xr.grad) < 1e-5
+
+
+def test_softmax_ce_adv():
+    k = K()
+    g = torch.Generator().manual_seed(11)
+    n, c, h, w = 2, 19, 33, 41
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64) * 3
+    lab = torch.randint(0, c, (n, h, w), generator=g)
+    lab[torch.rand(n, h, w, generator=g) < 0.1] = 255
+    lab[0, 0, :4] = -1  # CrossEntropy2d also drops negative labels (utils/loss.py:29)
+    xr = x.clone().requires_grad_(True)
+    sm = F.softmax(xr, dim=1)
+    gs = torch.randn(sm.shape, generator=g, dtype=torch.float64)
+    sm.backward(gs)
+    yd = k.softmax_fwd(nhwc(x))
+    assert rel(nchw(yd), sm) < 1e-5
+    dxd = k.softmax_bwd(yd, nhwc(gs))
+    assert rel(nchw(dxd), xr.grad) < 1e-5
+    # CE
+    from oracle.reference_torch import cross_entropy2d
+    xr2 = x.clone().requires_grad_(True)
+    lref = cross_entropy2d(xr2, lab)
+    lref.backward(torch.tensor(0.7, dtype=torch.float64))
+    xd = nhwc(x)
+    labd = lab.to(DEV)
+    out = k.ce_fwd(xd, labd)
+    assert abs(out[0].item() - lref.item()) < 1e-5 * abs(lref.item())
+    gl = torch.tensor([0.7], device=DEV)
+    dl = k.ce_bwd(xd, labd, out, gl)
+    assert rel(nchw(dl), xr2.grad) < 1e-5
+    # all ignored -> NaN (reference behaviour)
+    out2 = k.ce_fwd(xd, torch.full_like(labd, 255))
+    assert torch.isnan(out2[0]).item()
+    # adversarial losses
+    d = torch.randn(2, 1, 16, 32, generator=g, dtype=torch.float64) * 2
+    for kind, tgt in ((0, 0.0), (0, 1.0), (1, 0.0), (1, 1.0)):
+        dr = d.clone().requires_grad_(True)
+        t = torch.full_like(dr, tgt)
+        lr_ = F.binary_cross_entropy_with_logits(dr, t) if kind == 0 else F.mse_loss(dr, t)
+        lr_.backward(torch.tensor(0.3, dtype=torch.float64))
+        dd = d.float().to(DEV).contiguous()
+        lo = k.adv_fwd(dd, tgt, kind)
+        assert abs(lo.item() - lr_.item()) < 1e-5 * max(1.0, abs(lr_.item()))
+        gx = k.adv_bwd(dd, tgt, kind, torch.tensor([0.3], device=DEV))
+        assert rel(gx.cpu(), dr.grad) < 1e-5
+
+
+def test_sgd_multiplicity_and_adam():
+    k = K()
+    g = torch.Generator().manual_seed(12)
+    n = 1000
+    p0 = torch.randn(n, generator=g, dtype=torch.float64)
+    grads = [torch.randn(n, generator=g, dtype=torch.float64) for _ in range(3)]
+    for mult in (1, 3, 4):
+        pr = torch.nn.Parameter(p0.clone())
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            opt = torch.optim.SGD([{"params": [pr] * mult}], lr=0.01, momentum=0.9, weight_decay=5e-4, foreach=False)
+        pd = p0.float().to(DEV)
+        md = torch.zeros(n, device=DEV)
+        for s, gr in enumerate(grads):
+            pr.grad = gr.clone()
+            opt.step()
+            k.sgd_step(pd, (gr * 2).float().to(DEV), md, 0.01, 0.9, 5e-4, grad_scale=0.5,
+                       multiplicity=mult, first_step=(s == 0))
+        assert rel(pd.cpu(), pr.detach()) < 1e-5
+    pr = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.99), foreach=False)
+    pd = p0.float().to(DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    for s, gr in enumerate(grads):
+        pr.grad = gr.clone()
+        opt.step()
+        k.adam_step(pd, gr.float().to(DEV), m, v, 1e-3, 0.9, 0.99, 1e-8, s + 1)
+    assert rel(pd.cpu(), pr.detach()) < 1e-5
+
+
+def test_to_nhwc_and_axpy():
+    k = K()
+    x = torch.randn(2, 19, 7, 9, device=DEV)
+    assert torch.equal(k.to_nhwc(x), x.permute(0, 2, 3, 1).contiguous())
+    a = torch.randn(100, device=DEV)
+    b = torch.randn(100, device=DEV)
+    c = b.clone()
+    k.axpy(0.5, a, c)
+    assert torch.allclose(c, b + 0.5 * a)

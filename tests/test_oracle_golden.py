@@ -1,0 +1,129 @@
+"""CPU: the oracle (oracle/reference_torch.py) against goldens captured from the reference.
+
+The goldens were produced by tests/golden/gen_golden.py importing the reference modules
+(/root/reference/model/deeplab_multi.py, model/discriminator.py, utils/loss.py) with the
+same deterministic weights, so agreement here pins the oracle to the reference.
+"""
+import os
+import warnings
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import reference_torch as R
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD)
+
+
+@pytest.fixture(scope="module")
+def inputs():
+    xs = torch.from_numpy(R.det_images((2, 3, 41, 57), 11))
+    lab = torch.from_numpy(R.det_labels((2, 41, 57), 12))
+    xt = torch.from_numpy(R.det_images((2, 3, 33, 49), 13))
+    return xs, lab, xt
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_g_specs_match_reference_keys(gold):
+    keys = {k.split("/", 3)[3] for k in gold.files if k.startswith("step_single-level_Vanilla/G/")}
+    spec_keys = {k for k, _, _ in R.g_specs()}
+    assert keys == spec_keys
+
+
+def test_forward_train_and_backward(gold, inputs):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    xs, lab, _ = inputs
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), trainable=R.g_trainable)
+    p1, p2 = R.g_forward(G, xs, (57, 41))
+    assert rel(p1.detach(), gold["fwd_train/pred1"]) < 1e-6
+    assert rel(p2.detach(), gold["fwd_train/pred2"]) < 1e-6
+    l2 = R.cross_entropy2d(p2, lab)
+    assert abs(l2.item() - float(gold["ce/crossentropy2d"])) < 1e-10
+    assert abs(F.cross_entropy(p2, lab, ignore_index=255).item() - float(gold["ce/nn_crossentropy"])) < 1e-10
+    (l2 + 0.1 * R.cross_entropy2d(p1, lab)).backward()
+    n = 0
+    for k, t in G.items():
+        key = "bwd_train/gradnorm/" + k
+        if key in gold.files:
+            n += 1
+            assert abs(t.grad.norm().item() - float(gold[key])) <= 1e-9 * float(gold[key]) + 1e-300, k
+    assert n == 120  # 104 convs + 16 ASPP weights/biases
+    assert rel(G["conv1.weight"].grad, gold["bwd_train/grad/conv1.weight"]) < 1e-9
+    for k in G:
+        if "running" in k:
+            assert abs(G[k].sum().item() - float(gold["fwd_train/sum/" + k])) < 1e-9 * max(1, abs(float(gold["fwd_train/sum/" + k])))
+
+
+def test_forward_eval(gold, inputs):
+    xs, _, _ = inputs
+    G = R.to_torch(R.det_state(R.g_specs(), 1338))
+    with torch.no_grad():
+        e1, e2 = R.g_forward(G, xs, (57, 41), train=False)
+    assert rel(e1, gold["fwd_eval/pred1"]) < 1e-6
+    assert rel(e2, gold["fwd_eval/pred2"]) < 1e-6
+
+
+def test_discriminator_and_adv_losses(gold):
+    p2 = torch.from_numpy(gold["fwd_train/pred2"].astype(np.float64))
+    D = R.to_torch(R.det_state(R.d_specs(), 2001), trainable=lambda k: True)
+    sm = F.softmax(p2, dim=1).requires_grad_(True)
+    out = R.d_forward(D, sm)
+    assert rel(out.detach(), gold["d/out"]) < 1e-6  # pred2 stored as fp32
+    bce = R.adv_loss(out, 0, "Vanilla")
+    mse = R.adv_loss(out, 1, "LS")
+    assert abs(bce.item() - float(gold["d/bce0"])) < 1e-6
+    assert abs(mse.item() - float(gold["d/mse1"])) < 1e-6
+    (bce + mse).backward()
+    assert rel(sm.grad, gold["d/input_grad"]) < 1e-5
+
+
+def test_crossentropy2d_edges(gold):
+    rng = np.random.Generator(np.random.PCG64(99))
+    logits = torch.from_numpy(rng.standard_normal((2, 19, 5, 7)))
+    tl = torch.from_numpy(rng.integers(-1, 19, (2, 5, 7)).astype(np.int64))
+    tl[0, 0, :3] = 255
+    assert abs(R.cross_entropy2d(logits, tl).item() - float(gold["ce_edge/loss"])) < 1e-12
+    allign = torch.full((1, 4, 4), 255, dtype=torch.int64)
+    nan = torch.isnan(R.cross_entropy2d(torch.from_numpy(rng.standard_normal((1, 19, 4, 4))), allign))
+    assert bool(nan) == bool(gold["ce_edge/all_ignored_is_nan"])
+
+
+@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+def test_two_steps_match_reference(gold, inputs, level, gan):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    xs, lab, xt = inputs
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), trainable=R.g_trainable)
+    D1 = R.to_torch(R.det_state(R.d_specs(), 2001), trainable=lambda k: True)
+    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), trainable=lambda k: True)
+    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
+    opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
+    pre = f"step_{level}_{gan}/"
+    for it in range(2):
+        vals = R.oracle_step(G, D1, D2, opts, cfg, it, [(xs, lab, xt)])
+        ref = gold[pre + f"losses_iter{it}"]
+        if level == "single-level":
+            got = [vals["loss_seg2"], vals["loss_adv_target2"], vals["loss_D2"]]
+        else:
+            got = [vals["loss_seg1"], vals["loss_seg2"], vals["loss_adv_target1"],
+                   vals["loss_adv_target2"], vals["loss_D1"], vals["loss_D2"]]
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
+    for k, t in G.items():
+        if t.dtype.is_floating_point:
+            np.testing.assert_allclose(t.detach().sum().item(), float(gold[pre + "G/sum/" + k]),
+                                       rtol=1e-9, atol=1e-12, err_msg=k)
+        else:
+            assert int(t) == int(gold[pre + "G/int/" + k]), k
+    for k, t in D2.items():
+        np.testing.assert_allclose(t.detach().norm().item(), float(gold[pre + "D2/norm/" + k]),
+                                   rtol=1e-9, err_msg=k)
