@@ -51,6 +51,7 @@ _SIGS = {
     "adaptseg_last_error": [],
     "adaptseg_version": [],
     "adaptseg_conv2d_workspace_size": [_DESC, _I, ctypes.POINTER(_SZ)],
+    "adaptseg_conv2d_kernel_id": [_DESC, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
     "adaptseg_conv2d_fwd": [_DESC, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data": [_DESC, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight": [_DESC, _P, _P, _PP, _PP, _I, _P, _SZ, _P],

@@ -61,24 +61,40 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
       a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
       b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
     }
-    float *p1 = partial + (size_t)blockIdx.y * 2 * C;
-    *reinterpret_cast<float4 *>(p1 + c0) = a;
-    *reinterpret_cast<float4 *>(p1 + C + c0) = b;
+    // transposed [2][C][splits]: a channel's partials are contiguous for the finalize wave
+    const size_t S = gridDim.y, sp = blockIdx.y;
+    float *p1 = partial + (size_t)c0 * S + sp, *p2 = partial + ((size_t)C + c0) * S + sp;
+    p1[0] = a.x; p1[S] = a.y; p1[2 * S] = a.z; p1[3 * S] = a.w;
+    p2[0] = b.x; p2[S] = b.y; p2[2 * S] = b.z; p2[3 * S] = b.w;
   }
 }
 
-// Finalise forward statistics: mean, invstd, running-stat update.
+// One wave64 per channel sums that channel's `splits` partials (contiguous) in fp64.
+__device__ __forceinline__ void wave_sum2(const float *p1, const float *p2, int splits, double &s1, double &s2) {
+  const int lane = threadIdx.x & 63;
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int i = lane; i < splits; i += 64) {
+    s1 += p1[i];
+    s2 += p2[i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+}
+
+// Finalise forward statistics: mean, invstd, running-stat update.  Block = 256 = 4 channels.
 __global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ x,
                                       const float *__restrict__ partial, float *mean_out,
                                       float *invstd_out, float *running_mean, float *running_var,
                                       float momentum, float eps) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int i = 0; i < splits; ++i) {
-    s1 += partial[(size_t)i * 2 * C + c];
-    s2 += partial[(size_t)i * 2 * C + C + c];
-  }
+  double s1, s2;
+  wave_sum2(partial + (size_t)c * splits, partial + ((size_t)C + c) * splits, splits, s1, s2);
+  if ((threadIdx.x & 63) != 0) return;
   double n = (double)rows;
   double dm = s1 / n;
   double var = s2 / n - dm * dm;
@@ -96,15 +112,13 @@ __global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const flo
 // Finalise backward sums: store mean(g) and mean(g*xhat) per channel.
 __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ partial,
                                     const float *__restrict__ invstd, float *coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int i = 0; i < splits; ++i) {
-    s1 += partial[(size_t)i * 2 * C + c];
-    s2 += partial[(size_t)i * 2 * C + C + c];
-  }
+  double s1, s2;
+  wave_sum2(partial + (size_t)c * splits, partial + ((size_t)C + c) * splits, splits, s1, s2);
+  if ((threadIdx.x & 63) != 0) return;
   double n = (double)rows;
-  coef[c] = (float)(s1 / n);                       // mean(g)
+  coef[c] = (float)(s1 / n);                          // mean(g)
   coef[C + c] = (float)(s2 / n * (double)invstd[c]);  // mean(g * xhat)
 }
 
@@ -207,7 +221,7 @@ static ReducePlan reduce_plan(int64_t rows, int C) {
   // tc must divide 256
   while (256 % r.tc) --r.tc;
   r.cblocks = (int)ceil_div(C, 4 * r.tc);
-  int want = std::max(1, 1024 / r.cblocks);
+  int want = std::max(1, 512 / r.cblocks);
   int tr = 256 / r.tc;
   int64_t max_splits = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * 8));
   r.splits = (int)std::min<int64_t>(want, max_splits);
@@ -254,7 +268,7 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
   bn_reduce_kernel<0><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
                                                                 0, r.per, partial);
   AS_CHECK_LAUNCH("bn_reduce<stats>");
-  bn_stats_final_kernel<<<(unsigned)ceil_div(c, 256), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
+  bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
                                                                    save_invstd, running_mean, running_var,
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
@@ -297,7 +311,7 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
     bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean, relu,
                                                                   r.per, partial);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
-    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 256), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
+    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
                                                                    coef);
     AS_CHECK_LAUNCH("bn_bwd_final");
   }

@@ -50,6 +50,9 @@ struct ConvParams {
   const float *res;            // residual (nullable)
   const float *aux;            // leaky-grad source (nullable)
   int flags;
+  int kw_, kh_;                // kernel width / height (tap -> kh, kw)
+  int pad_[4], dil_[4];        // per-segment padding / dilation
+  FastDiv fd_taps, fd_kw;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
 
@@ -531,6 +534,382 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// FAST path.  Preconditions (checked on the host): every BK-deep K tile of the A operand
+// lies inside ONE tap (FWD: C % BK == 0; DGRAD: Cout % BK == 0 and stride 1), operands are
+// NHWC with 16-B aligned float4 rows.  Then tap, channel offset and weight segment are
+// tile-uniform scalars, and each lane's gather is one clamped, branch-free float4 load:
+//   FWD A   x[b*sxn + (oh*s+dy)*sxh + (ow*s+dx)*sxw + ci0 + kq]   (pix_slot + s_off)
+//   FWD B   w_seg[n*kseg + kk0 + kq]
+//   DGRAD A dy[((b*OH+ih-dy)*OW + iw-dx)*Cout + co0 + kq]
+//   DGRAD B w_seg[((co0+r)*taps + t)*C + n]
+//   WGRAD A dy[m*Cout + co],   WGRAD B x[b, oh*s+dy, ow*s+dx, ci]  (per-column tap)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool S2>
+__global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+  constexpr bool A_KC = MODE != MODE_WGRAD;
+  constexpr bool B_KC = MODE == MODE_FWD;
+  constexpr int SA = A_KC ? BM + 2 : BM + 4;
+  constexpr int SB = B_KC ? BN + 2 : BN + 4;
+  constexpr int STAGE = BK * SA + BK * SB;
+  constexpr int QA = BM * BK / 4, QB = BN * BK / 4;
+  constexpr int NQA = (QA + 255) / 256, NQB = (QB + 255) / 256;
+  constexpr int KQ = BK / 4;  // float4 per k-contiguous row
+  static_assert(QA % 256 == 0 && QB % 256 == 0, "every thread stages whole float4 slots");
+
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  const int bm = tm * BM, bn = tn * BN;
+  const int split = blockIdx.y;
+
+  // Stride-2 data gradient: blockIdx.z = output-pixel parity class (py, px).  The class's
+  // pixels (2i+py, 2j+px) form a dense (Hc x Wc) grid that only the taps kh = kh0 + 2u,
+  // kw = kw0 + 2v reach (dil 1), at dY row i + (py+pad-kh)/2: a stride-1 problem with
+  // K = nkh*nkw*Cout and no zero-stuffed work.
+  int M = p.M, K = p.K, Hc = p.h, Wc = p.w, py = 0, px = 0, kh0 = 0, kw0 = 0, nkw = p.kw_;
+  if constexpr (S2) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (p.h - py + 1) >> 1;
+    Wc = (p.w - px + 1) >> 1;
+    kh0 = (py + p.pad_[0]) & 1;
+    kw0 = (px + p.pad_[0]) & 1;
+    const int nkh = (p.kh_ - kh0 + 1) >> 1;
+    nkw = (p.kw_ - kw0 + 1) >> 1;
+    M = p.n * Hc * Wc;
+    K = nkh * nkw * p.k;
+    if (bm >= M) return;
+  }
+  const int nkt = (K + BK - 1) / BK;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
+
+  // ---- per-slot constants ----
+  int a_pix[NQA], a_y[NQA], a_x[NQA], a_col[NQA], a_k[NQA];
+  bool a_ok[NQA];
+#pragma unroll
+  for (int i = 0; i < NQA; ++i) {
+    const int q = tid + 256 * i;
+    if constexpr (A_KC) {
+      const int row = q / KQ;
+      a_col[i] = row;
+      a_k[i] = (q % KQ) * 4;
+      const int m = bm + row;
+      a_ok[i] = m < M;
+      const int mm = min(m, M - 1);
+      if constexpr (S2) {
+        const int j = mm % Wc, t2 = mm / Wc;
+        const int ii = t2 % Hc, b = t2 / Hc;
+        a_y[i] = ii;
+        a_x[i] = j;
+        a_pix[i] = ((b * p.oh + ii) * p.ow + j) * p.k + a_k[i];
+      } else if constexpr (MODE == MODE_FWD) {
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        a_y[i] = oh * p.stride;
+        a_x[i] = ow * p.stride;
+        a_pix[i] = (int)b * p.sxn + a_y[i] * p.sxh + a_x[i] * p.sxw + a_k[i];
+      } else {  // DGRAD, stride 1
+        uint32_t t = fdiv((uint32_t)mm, p.fd_w);
+        const int iw = mm - (int)t * p.w;
+        uint32_t b = fdiv(t, p.fd_hw);
+        const int ih = (int)t - (int)b * p.h;
+        a_y[i] = ih;
+        a_x[i] = iw;
+        a_pix[i] = (((int)b * p.oh + ih) * p.ow + iw) * p.k + a_k[i];
+      }
+    } else {  // WGRAD A': rows k' = pixel, columns = output channel
+      a_k[i] = q / (BM / 4);
+      a_col[i] = (q % (BM / 4)) * 4;
+      const int col = bm + a_col[i];
+      a_ok[i] = col < p.M;
+      a_pix[i] = a_ok[i] ? col : 0;
+    }
+  }
+  int b_off[NQB], b_col[NQB], b_k[NQB], b_dy[NQB], b_dx[NQB];
+  bool b_ok[NQB];
+#pragma unroll
+  for (int i = 0; i < NQB; ++i) {
+    const int q = tid + 256 * i;
+    if constexpr (B_KC) {  // FWD B: rows n, k contiguous
+      const int row = q / KQ;
+      b_col[i] = row;
+      b_k[i] = (q % KQ) * 4;
+      const int n = bn + row;
+      b_ok[i] = n < p.N;
+      b_off[i] = min(n, p.N - 1) * p.kseg + b_k[i];
+    } else {
+      b_k[i] = q / (BN / 4);
+      b_col[i] = (q % (BN / 4)) * 4;
+      const int n = bn + b_col[i];
+      b_ok[i] = n < p.N;
+      const int nn = b_ok[i] ? n : 0;
+      if constexpr (MODE == MODE_DGRAD) {
+        b_off[i] = b_k[i] * p.taps_per_seg * p.c + nn;
+      } else {  // WGRAD B': column (tap, ci)
+        const int tap = (int)fdiv((uint32_t)nn, p.fd_c);
+        const int ci = nn - tap * p.c;
+        const int seg = (int)fdiv((uint32_t)tap, p.fd_taps);
+        const int t = tap - seg * p.taps_per_seg;
+        const int kh = (int)fdiv((uint32_t)t, p.fd_kw);
+        const int kw = t - kh * p.kw_;
+        const int dil = seg == 0 ? p.dil_[0] : seg == 1 ? p.dil_[1] : seg == 2 ? p.dil_[2] : p.dil_[3];
+        const int pad = seg == 0 ? p.pad_[0] : seg == 1 ? p.pad_[1] : seg == 2 ? p.pad_[2] : p.pad_[3];
+        b_dy[i] = kh * dil - pad;
+        b_dx[i] = kw * dil - pad;
+        b_off[i] = ci;
+      }
+    }
+  }
+
+  float4 ra[NQA], rb[NQB];
+  bool ma[NQA], mb[NQB];  // validity, applied when the staged tile is written to LDS
+
+  // Tile-uniform tap -> (segment, dy, dx) on the scalar unit.
+  auto tap_geom = [&](int tap, int &seg, int &t, int &dy, int &dx) {
+    seg = uni((int)fdiv((uint32_t)tap, p.fd_taps));
+    t = tap - seg * p.taps_per_seg;
+    const int kh = (int)fdiv((uint32_t)t, p.fd_kw);
+    const int kw = t - kh * p.kw_;
+    const int dil = seg == 0 ? p.dil_[0] : seg == 1 ? p.dil_[1] : seg == 2 ? p.dil_[2] : p.dil_[3];
+    const int pad = seg == 0 ? p.pad_[0] : seg == 1 ? p.pad_[1] : seg == 2 ? p.pad_[2] : p.pad_[3];
+    dy = uni(kh * dil - pad);
+    dx = uni(kw * dil - pad);
+  };
+
+  auto load_tile = [&](int kt) {
+    const int kbase = kt * BK;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
+      int seg, t, dy, dx;
+      tap_geom(tap, seg, t, dy, dx);
+      const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
+#pragma unroll
+      for (int i = 0; i < NQA; ++i) {
+        ma[i] = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h &&
+                (unsigned)(a_x[i] + dx) < (unsigned)p.w;
+        ra[i] = ld4(p.x + (ma[i] ? a_pix[i] + soff : 0));
+      }
+      const float *wp = seg_ptr(p, seg) + (kbase - seg * p.kseg);
+#pragma unroll
+      for (int i = 0; i < NQB; ++i) {
+        mb[i] = b_ok[i];
+        rb[i] = ld4(wp + b_off[i]);
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
+      const int co0 = kbase - tap * p.k;
+      int seg, t, dy, dx;
+      if constexpr (S2) {
+        const int u = tap / nkw, v = tap - u * nkw;
+        const int kh = kh0 + 2 * u, kw = kw0 + 2 * v;
+        seg = 0;
+        t = uni(kh * p.kw_ + kw);
+        dy = uni(-((py + p.pad_[0] - kh) >> 1));  // dY row = i - dy
+        dx = uni(-((px + p.pad_[0] - kw) >> 1));
+      } else {
+        tap_geom(tap, seg, t, dy, dx);
+      }
+      const int soff = uni(co0 - (dy * p.ow + dx) * p.k);
+#pragma unroll
+      for (int i = 0; i < NQA; ++i) {
+        ma[i] = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh &&
+                (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
+        ra[i] = ld4(p.dy + (ma[i] ? a_pix[i] + soff : 0));
+      }
+      const float *wp = seg_ptr(p, seg) + (co0 * p.taps_per_seg + t) * p.c;
+#pragma unroll
+      for (int i = 0; i < NQB; ++i) {
+        mb[i] = b_ok[i];
+        rb[i] = ld4(wp + b_off[i]);
+      }
+    } else {  // WGRAD
+#pragma unroll
+      for (int i = 0; i < NQA; ++i) {
+        const int m = kbase + a_k[i];
+        ma[i] = a_ok[i] && m < p.K;
+        ra[i] = ld4(p.dy + (size_t)(ma[i] ? m : 0) * p.k + a_pix[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < NQB; ++i) {
+        const int m = kbase + b_k[i];
+        const int mm = min(m, p.K - 1);
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        const int iy = oh * p.stride + b_dy[i], ix = ow * p.stride + b_dx[i];
+        mb[i] = b_ok[i] && m < p.K && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+        rb[i] = ld4(p.x + (mb[i] ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    float *As = lds + buf * STAGE;
+    float *Bs = As + BK * SA;
+#pragma unroll
+    for (int i = 0; i < NQA; ++i) {
+      const float4 v = sel4(ma[i], ra[i]);
+      if constexpr (A_KC) {
+        float *d = As + a_k[i] * SA + a_col[i];
+        d[0] = v.x;
+        d[SA] = v.y;
+        d[2 * SA] = v.z;
+        d[3 * SA] = v.w;
+      } else {
+        *reinterpret_cast<float4 *>(As + a_k[i] * SA + a_col[i]) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NQB; ++i) {
+      const float4 v = sel4(mb[i], rb[i]);
+      if constexpr (B_KC) {
+        float *d = Bs + b_k[i] * SB + b_col[i];
+        d[0] = v.x;
+        d[SB] = v.y;
+        d[2 * SB] = v.z;
+        d[3 * SB] = v.w;
+      } else {
+        *reinterpret_cast<float4 *>(Bs + b_k[i] * SB + b_col[i]) = v;
+      }
+    }
+  };
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+  const int l32 = lane & 31, hh = lane >> 5;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      const float *As = lds + cur * STAGE + wm * WTM + l32;
+      const float *Bs = lds + cur * STAGE + BK * SA + wn * WTN + l32;
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 2) {
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[(kk + hh) * SA + i * 32];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[(kk + hh) * SB + j * 32];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---- epilogue ----
+  const bool full = (bm + BM <= M) && (bn + BN <= p.N);
+  // output row of GEMM row `row` (S2: scatter the parity class back into the NHWC image)
+  auto out_row = [&](int row) -> size_t {
+    if constexpr (S2) {
+      const int j = row % Wc, t2 = row / Wc;
+      const int ii = t2 % Hc, b = t2 / Hc;
+      return ((size_t)(b * p.h + 2 * ii + py) * p.w + 2 * j + px);
+    } else {
+      return (size_t)row;
+    }
+  };
+  if (p.splits > 1) {
+    float *slab = p.out + (size_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = bn + wn * WTN + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (full || (row < p.M && col < p.N)) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == MODE_WGRAD) {
+    const bool accum = p.flags & ADAPTSEG_EPI_ACCUMULATE;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = bn + wn * WTN + j * 32 + l32;
+      if (!full && col >= p.N) continue;
+      const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
+      const int cc = col - seg * p.kseg;
+      float *dst = (seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3]) + cc;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!full && row >= p.M) continue;
+          float *o = dst + (size_t)row * p.kseg;
+          const float v = acc[i][j][r];
+          *o = accum ? *o + v : v;
+        }
+    }
+  } else {
+    const int flags = p.flags;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = bn + wn * WTN + j * 32 + l32;
+      if (!full && col >= p.N) continue;
+      float bsum = 0.f;
+      if constexpr (MODE == MODE_FWD) {
+        for (int s = 0; s < p.nseg; ++s) {
+          const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
+          if (bp) bsum += bp[col];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!full && row >= M) continue;
+          const size_t idx = out_row(row) * p.N + col;
+          float v = acc[i][j][r] + bsum;
+          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
+          if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
+          if (flags & ADAPTSEG_EPI_LEAKY) v = v > 0.f ? v : 0.2f * v;
+          if (flags & ADAPTSEG_EPI_LEAKY_GRAD) v = p.aux[idx] > 0.f ? v : 0.2f * v;
+          p.out[idx] = v;
+        }
+    }
+  }
+}
+
 // Split-K reduction + epilogue.  One thread per output element, slabs summed in order.
 __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int mode) {
   const size_t total = (size_t)p.M * p.N;
@@ -605,22 +984,17 @@ __global__ void bias_grad_final_kernel(const float *partial, int splits, int cou
 struct TimingState {
   std::mutex mu;
   bool enabled = false;
-  int conv_class = 0;
+  int selector = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
   std::vector<double> flops;
   size_t used = 0;
 };
 static TimingState g_timing;
 
-static bool timing_selected(const adaptseg_conv_desc *d) {
-  if (!g_timing.enabled) return false;
-  if (g_timing.conv_class == 0) return true;
-  return d->nseg == 1 && d->kh == 3 && d->kw == 3 && d->dil[0] > 1;
-}
-
-static void timing_begin(const adaptseg_conv_desc *d, hipStream_t s, double fl, int *slot) {
+static void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
   *slot = -1;
-  if (!timing_selected(d)) return;
+  if (!g_timing.enabled) return;
+  if (g_timing.selector >= 0 && g_timing.selector != kernel_id) return;
   std::lock_guard<std::mutex> lk(g_timing.mu);
   if (g_timing.used == g_timing.events.size()) {
     hipEvent_t a, b;
@@ -630,7 +1004,7 @@ static void timing_begin(const adaptseg_conv_desc *d, hipStream_t s, double fl, 
   }
   *slot = (int)g_timing.used++;
   g_timing.flops[*slot] = fl;
-  hipEventRecord(g_timing.events[*slot].first, s);
+  (void)hipEventRecord(g_timing.events[*slot].first, s);
 }
 
 static void timing_end(int slot, hipStream_t s) {
@@ -645,8 +1019,13 @@ struct Plan {
   ConvParams p;
   int cfg;        // 0: 128x128 (2x2), 1: 256x32 (4x1), 2: 32x256 (1x4), 3: 64x256 (1x4)
   bool va, vb;
+  bool fast;
+  bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
+  int bk;
+  int mode;
   int tiles;
   size_t slab_bytes;
+  double flops;  // algorithmic FLOPs of the conv product this plan computes
 };
 
 static int validate(const adaptseg_conv_desc *d) {
@@ -685,6 +1064,14 @@ static void fill_common(ConvParams &p, const adaptseg_conv_desc *d) {
         p.tap_dy[t] = (short)(i * d->dil[s] - d->pad[s]);
         p.tap_dx[t] = (short)(j * d->dil[s] - d->pad[s]);
       }
+  p.kw_ = d->kw;
+  p.kh_ = d->kh;
+  for (int s = 0; s < 4; ++s) {
+    p.pad_[s] = s < d->nseg ? d->pad[s] : 0;
+    p.dil_[s] = s < d->nseg ? d->dil[s] : 1;
+  }
+  p.fd_taps = make_fastdiv(p.taps_per_seg);
+  p.fd_kw = make_fastdiv(d->kw);
   p.fd_c = make_fastdiv(d->c);
   p.fd_k = make_fastdiv(d->k);
   p.fd_ow = make_fastdiv(d->ow);
@@ -693,14 +1080,55 @@ static void fill_common(ConvParams &p, const adaptseg_conv_desc *d) {
   p.fd_hw = make_fastdiv(d->h);
 }
 
-static const int kCfgBM[4] = {128, 256, 32, 64};
-static const int kCfgBN[4] = {128, 32, 256, 256};
+static double conv_flops(const adaptseg_conv_desc *d) {
+  return 2.0 * d->n * d->oh * d->ow * (double)d->k * d->c * d->kh * d->kw * d->nseg;
+}
+
+// tile configs: 0 = 128x128 (2x2 waves), 1 = 256x32 (4x1), 2 = 32x256 (1x4), 3 = 64x256 (1x4),
+// 4 = 256x64 (4x1).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
+static const int kCfgBM[5] = {128, 256, 32, 64, 256};
+static const int kCfgBN[5] = {128, 32, 256, 256, 64};
+// K step of the FAST kernel per config (LDS: 2 stages x BK x (BM+BN+pad) floats)
+static int fast_bk(int cfg) { return cfg == 4 ? 16 : 32; }
+
+// Grid decomposition: tiles, then split K until the grid has ~2 blocks per CU while keeping
+// >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
+static void set_splits(Plan &pl) {
+  ConvParams &p = pl.p;
+  const int bm = kCfgBM[pl.cfg], bn = kCfgBN[pl.cfg];
+  pl.bk = pl.fast ? fast_bk(pl.cfg) : BK;
+  if (!pl.fast) pl.s2 = false;
+  if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
+    p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
+    p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
+  } else if (pl.mode == MODE_DGRAD) {
+    p.M = p.n * p.h * p.w;
+    p.K = p.ntaps * p.k;
+  }
+  pl.tiles = (int)(ceil_div(p.M, bm) * ceil_div(p.N, bn));
+  const int nkt = (int)ceil_div(p.K, pl.bk);
+  // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~4.
+  // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
+  const int target = pl.mode == MODE_WGRAD ? 1024 : 512;
+  int splits = 1;
+  if (pl.tiles < target && !pl.s2) {
+    splits = (int)ceil_div(target, pl.tiles);
+    splits = std::min(splits, std::max(1, nkt / 4));
+    splits = std::min(splits, 256);
+  }
+  int per = (int)ceil_div(nkt, splits);
+  splits = (int)ceil_div(nkt, per);
+  p.splits = splits;
+  p.ktiles_per_split = per;
+  pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
+}
 
 static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   int st = validate(d);
   if (st) return st;
   ConvParams &p = pl.p;
   fill_common(p, d);
+  pl.mode = op;
   const bool nhwc_in = d->in_stride[1] == 1;
   if (op == ADAPTSEG_CONV_FWD) {
     p.M = d->n * d->oh * d->ow;
@@ -709,7 +1137,7 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     p.kseg = p.taps_per_seg * d->c;
     pl.va = nhwc_in && d->c % 4 == 0;
     pl.vb = d->c % 4 == 0;
-    pl.cfg = p.N <= 32 ? 1 : 0;
+    pl.cfg = p.N <= 32 ? 1 : (p.N <= 64 ? 4 : 0);
   } else if (op == ADAPTSEG_CONV_BWD_DATA) {
     p.M = d->n * d->h * d->w;
     p.N = d->c;
@@ -717,7 +1145,7 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     p.kseg = p.taps_per_seg * d->c;
     pl.va = d->k % 4 == 0;
     pl.vb = d->c % 4 == 0;
-    pl.cfg = p.N <= 32 ? 1 : 0;
+    pl.cfg = p.N <= 32 ? 1 : (p.N <= 64 ? 4 : 0);
   } else if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
     p.M = d->k;
     p.N = p.ntaps * d->c;
@@ -731,43 +1159,55 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     return ADAPTSEG_ERR_ARG;
   }
   p.fd_nseg_k = make_fastdiv(p.kseg);
-  const int bm = kCfgBM[pl.cfg], bn = kCfgBN[pl.cfg];
-  pl.tiles = (int)(ceil_div(p.M, bm) * ceil_div(p.N, bn));
-  const int nkt = (int)ceil_div(p.K, BK);
-  // Split K until the grid has ~2 blocks per CU, keeping >= 8 K-steps per split.
-  const int target = 512;
-  int splits = 1;
-  if (pl.tiles < target) {
-    splits = (int)ceil_div(target, pl.tiles);
-    splits = std::min(splits, std::max(1, nkt / 8));
-    splits = std::min(splits, 64);
+  pl.flops = conv_flops(d);
+  // FAST path eligibility (alignment re-checked at launch)
+  const int fbk = fast_bk(pl.cfg);
+  pl.s2 = false;
+  if (op == ADAPTSEG_CONV_FWD) {
+    pl.fast = nhwc_in && d->c % fbk == 0;
+  } else if (op == ADAPTSEG_CONV_BWD_DATA) {
+    pl.s2 = d->stride == 2 && d->nseg == 1 && d->dil[0] == 1;
+    pl.fast = (d->stride == 1 || pl.s2) && d->k % fbk == 0 && d->c % 4 == 0;
+  } else {
+    pl.fast = nhwc_in && d->c % 4 == 0 && d->k % 4 == 0;
   }
-  int per = (int)ceil_div(nkt, splits);
-  splits = (int)ceil_div(nkt, per);
-  p.splits = splits;
-  p.ktiles_per_split = per;
-  pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
+  set_splits(pl);
   return ADAPTSEG_OK;
 }
 
 template <int MODE>
 static hipError_t launch_cfg(const Plan &pl, hipStream_t s) {
-  dim3 grid(pl.tiles, pl.p.splits), block(256);
-#define AS_LAUNCH(BM_, BN_, WM_, WN_)                                                                   \
-  do {                                                                                                  \
-    if (pl.va && pl.vb) igemm_kernel<MODE, BM_, BN_, WM_, WN_, true, true><<<grid, block, 0, s>>>(pl.p); \
-    else if (pl.va) igemm_kernel<MODE, BM_, BN_, WM_, WN_, true, false><<<grid, block, 0, s>>>(pl.p);   \
-    else if (pl.vb) igemm_kernel<MODE, BM_, BN_, WM_, WN_, false, true><<<grid, block, 0, s>>>(pl.p);   \
-    else igemm_kernel<MODE, BM_, BN_, WM_, WN_, false, false><<<grid, block, 0, s>>>(pl.p);             \
+  dim3 grid(pl.tiles, pl.p.splits, pl.s2 ? 4 : 1), block(256);
+#define AS_LAUNCH(BM_, BN_, WM_, WN_, FBK_)                                                                  \
+  do {                                                                                                       \
+    if (pl.fast && pl.s2) {                                                                                  \
+      if constexpr (MODE == MODE_DGRAD)                                                                      \
+        igemm_fast_kernel<MODE, BM_, BN_, WM_, WN_, FBK_, true><<<grid, block, 0, s>>>(pl.p);               \
+    } else if (pl.fast) {                                                                                    \
+      igemm_fast_kernel<MODE, BM_, BN_, WM_, WN_, FBK_, false><<<grid, block, 0, s>>>(pl.p);                \
+    } else if (pl.va && pl.vb) {                                                                             \
+      igemm_kernel<MODE, BM_, BN_, WM_, WN_, true, true><<<grid, block, 0, s>>>(pl.p);                       \
+    } else if (pl.va) {                                                                                      \
+      igemm_kernel<MODE, BM_, BN_, WM_, WN_, true, false><<<grid, block, 0, s>>>(pl.p);                      \
+    } else if (pl.vb) {                                                                                      \
+      igemm_kernel<MODE, BM_, BN_, WM_, WN_, false, true><<<grid, block, 0, s>>>(pl.p);                      \
+    } else {                                                                                                 \
+      igemm_kernel<MODE, BM_, BN_, WM_, WN_, false, false><<<grid, block, 0, s>>>(pl.p);                     \
+    }                                                                                                        \
   } while (0)
   switch (pl.cfg) {
-    case 0: AS_LAUNCH(128, 128, 2, 2); break;
-    case 1: AS_LAUNCH(256, 32, 4, 1); break;
-    case 2: AS_LAUNCH(32, 256, 1, 4); break;
-    default: AS_LAUNCH(64, 256, 1, 4); break;
+    case 0: AS_LAUNCH(128, 128, 2, 2, 32); break;
+    case 1: AS_LAUNCH(256, 32, 4, 1, 32); break;
+    case 2: AS_LAUNCH(32, 256, 1, 4, 32); break;
+    case 3: AS_LAUNCH(64, 256, 1, 4, 32); break;
+    default: AS_LAUNCH(256, 64, 4, 1, 16); break;
   }
 #undef AS_LAUNCH
   return hipGetLastError();
+}
+
+static int kernel_id(const Plan &pl, int mode) {
+  return 100 * mode + 10 * pl.cfg + (pl.fast ? (pl.s2 ? 5 : 4) : (pl.va ? 2 : 0) + (pl.vb ? 1 : 0));
 }
 
 static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
@@ -780,9 +1220,12 @@ static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s
     pl.p.out = reinterpret_cast<float *>(ws);
   }
   hipError_t e;
+  int slot;
+  timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
   if (mode == MODE_FWD) e = launch_cfg<MODE_FWD>(pl, s);
   else if (mode == MODE_DGRAD) e = launch_cfg<MODE_DGRAD>(pl, s);
   else e = launch_cfg<MODE_WGRAD>(pl, s);
+  timing_end(slot, s);
   if (e != hipSuccess) {
     set_error("igemm launch: %s", hipGetErrorString(e));
     return ADAPTSEG_ERR_HIP;
@@ -799,9 +1242,6 @@ static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s
   return ADAPTSEG_OK;
 }
 
-static double conv_flops(const adaptseg_conv_desc *d) {
-  return 2.0 * d->n * d->oh * d->ow * (double)d->k * d->c * d->kh * d->kw * d->nseg;
-}
 
 }  // namespace adaptseg
 
@@ -815,6 +1255,12 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
   int st = make_plan(d, op, pl);
   if (st) return st;
   size_t b = pl.slab_bytes;
+  if (pl.fast) {  // an unaligned operand at launch time falls back to the generic kernel
+    Plan g = pl;
+    g.fast = false;
+    set_splits(g);
+    b = std::max(b, g.slab_bytes);
+  }
   if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
     // bias-gradient partials
     int rows = d->n * d->oh * d->ow;
@@ -822,6 +1268,17 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
     b = std::max(b, (size_t)splits * d->k * sizeof(float));
   }
   *bytes = b;
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_id, int *splits) {
+  AS_CHECK_ARG(kernel_id && splits, "conv2d_kernel_id: null");
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  // alignment-dependent downgrades are not known here; report the aligned choice
+  *kernel_id = ::adaptseg::kernel_id(pl, op);
+  *splits = pl.p.splits;
   return ADAPTSEG_OK;
 }
 
@@ -840,18 +1297,14 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
     AS_CHECK_ARG(w[s], "conv fwd: null weight %d", s);
     p.wt[s] = w[s];
     p.bias[s] = bias ? bias[s] : nullptr;
-    if (pl.vb && (reinterpret_cast<uintptr_t>(w[s]) & 15)) pl.vb = false;
+    if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
   }
-  if (pl.va && (reinterpret_cast<uintptr_t>(x) & 15)) pl.va = false;
+  if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
+  set_splits(pl);
   p.out = y;
   p.res = res;
   p.flags = flags;
-  int slot;
-  hipStream_t s = as_stream(stream);
-  timing_begin(d, s, conv_flops(d), &slot);
-  st = run_plan(pl, MODE_FWD, ws, ws_bytes, s);
-  timing_end(slot, s);
-  return st;
+  return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
@@ -869,19 +1322,15 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   for (int s = 0; s < d->nseg; ++s) {
     AS_CHECK_ARG(w[s], "conv bwd_data: null weight %d", s);
     p.wt[s] = w[s];
-    if (pl.vb && (reinterpret_cast<uintptr_t>(w[s]) & 15)) pl.vb = false;
+    if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
   }
-  if (pl.va && (reinterpret_cast<uintptr_t>(dy) & 15)) pl.va = false;
+  if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
+  set_splits(pl);
   p.out = dx;
   p.res = res;
   p.aux = aux;
   p.flags = flags;
-  int slot;
-  hipStream_t s = as_stream(stream);
-  timing_begin(d, s, conv_flops(d), &slot);
-  st = run_plan(pl, MODE_DGRAD, ws, ws_bytes, s);
-  timing_end(slot, s);
-  return st;
+  return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
@@ -898,14 +1347,12 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
     AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
     p.dw[s] = dw[s];
   }
-  if (pl.va && (reinterpret_cast<uintptr_t>(dy) & 15)) pl.va = false;
-  if (pl.vb && (reinterpret_cast<uintptr_t>(x) & 15)) pl.vb = false;
+  if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
+  if (reinterpret_cast<uintptr_t>(x) & 15) pl.vb = pl.fast = false;
+  set_splits(pl);
   p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
   hipStream_t s = as_stream(stream);
-  int slot;
-  timing_begin(d, s, conv_flops(d), &slot);
   st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
-  timing_end(slot, s);
   if (st) return st;
   if (db) {
     bool any = false;
@@ -933,11 +1380,11 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
   return ADAPTSEG_OK;
 }
 
-int adaptseg_timing_enable(int enable, int conv_class) {
+int adaptseg_timing_enable(int enable, int selector) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.enabled = enable != 0;
-  g_timing.conv_class = conv_class;
-  g_timing.used = 0;
+  g_timing.selector = selector;
+  if (enable) g_timing.used = 0;  // disabling keeps the recorded launches readable
   return ADAPTSEG_OK;
 }
 

@@ -385,3 +385,28 @@ def nhwc_view(t: torch.Tensor) -> torch.Tensor:
 def as_nchw(t: torch.Tensor) -> torch.Tensor:
     """NHWC buffer [n, h, w, c] -> NCHW-shaped channels_last view."""
     return t.permute(0, 3, 1, 2)
+
+
+# ---------------------------------------------------------------------------------------
+# Live kernel timing (bench.py roofline)
+# ---------------------------------------------------------------------------------------
+def conv_kernel_id(g: ConvGeom, n, h, w, op, strides=None):
+    """(selector, splits) of the igemm kernel that runs this conv product."""
+    strides = strides or nhwc_strides(n, h, w, g.cin)
+    d = _desc(g, n, h, w, tuple(strides))[0]
+    kid, sp = ctypes.c_int(0), ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv2d_kernel_id(ctypes.byref(d), op, ctypes.byref(kid), ctypes.byref(sp)),
+          "conv2d_kernel_id")
+    return kid.value, sp.value
+
+
+def timing_enable(selector: int = -1, enable: bool = True):
+    check(_lib.lib().adaptseg_timing_enable(1 if enable else 0, int(selector)), "timing_enable")
+
+
+def timing_read():
+    """(total_ms, total_flops, launches) of the timed launches since timing_enable()."""
+    ms, fl, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
+    check(_lib.lib().adaptseg_timing_read(ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)),
+          "timing_read")
+    return ms.value, fl.value, n.value

@@ -63,7 +63,7 @@ class StepLosses:
 
     def values(self) -> dict:
         """Host values (one device sync), summed like the reference's *_value accumulators."""
-        return {k: sum(float(t) * s for t, s in v) for k, v in self.tensors.items()}
+        return {k: sum(float(t.detach()) * s for t, s in v) for k, v in self.tensors.items()}
 
 
 class AdaptSegTrainer:

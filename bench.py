@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark: AdaptSegNet adversarial-train images/sec on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+One "step" = one full adversarial iteration of train_gta2cityscapes_multi.py on the HIP
+engine (2 G forwards, 2 G backwards, D forwards/backwards, SGD + Adam) over one synthetic
+batch already resident in HBM.  Default workload = BASELINE config c2: single-level,
+batch 4 per GPU, source and target 1024x512, Vanilla GAN, fp32 (the reference's dtype).
+``value`` = (source, target) pairs per second over all ranks (weak scaling: batch per GPU
+is fixed).  Rank 0 prints ONE JSON line.
+
+roofline: the dominant implicit-GEMM conv kernel symbol (most algorithmic FLOPs per step)
+is bracketed by hipEvents inside the library during the timed steps; achieved = its
+algorithmic FLOPs / its summed launch time, against the fp32 MFMA peak (157.3 TFLOP/s).
+cpu_baseline: the oracle (stock-PyTorch CPU restatement of the reference step, the
+reference's own arithmetic) timed on this host for ONE single-level step at batch 1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X: 256 CU x 2.4 GHz x 256 FLOP/clk/CU (MI355X_MICROARCH.md)
+METRIC = "adversarial-train images/sec at 1024×512, DeeplabMulti+D, 1/2/4/8 MI355X"
+
+CONFIGS = {
+    # name: (level, gan, batch/GPU, source (W,H), target (W,H))
+    "c2": ("single-level", "Vanilla", 4, (1024, 512), (1024, 512)),
+    "c3": ("multi-level", "Vanilla", 2, (1280, 720), (1024, 512)),
+}
+
+
+def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize):
+    """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector."""
+    from adaptsegnet_amd import kernels as K
+    from adaptsegnet_amd import engine
+    inv = {}
+
+    def add(geom, n, h, w, op, strides=None, count=1):
+        kid, _ = K.conv_kernel_id(geom, n, h, w, op, strides)
+        inv[kid] = inv.get(kid, 0.0) + count * geom.flops(n, h, w)
+
+    def g_pass(wh, backward, heads_bwd):
+        w, h = wh
+        gs = model.conv1.geom()
+        add(gs, batch, h, w, 0, (3 * h * w, h * w, w, 1))
+        if backward:
+            add(gs, batch, h, w, 2, (3 * h * w, h * w, w, 1))
+        h, w = gs.out_hw(h, w)
+        h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+        for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4), 1):
+            if li == 4:
+                g5 = engine.aspp_geom(model.layer5)
+                add(g5, batch, h, w, 0)
+                if backward and "l5" in heads_bwd:
+                    add(g5, batch, h, w, 1)
+                    add(g5, batch, h, w, 2)
+            for blk in layer:
+                convs = [(blk.conv1, h, w)]
+                oh, ow = blk.conv1.geom().out_hw(h, w)
+                convs += [(blk.conv2, oh, ow), (blk.conv3, oh, ow)]
+                if blk.downsample is not None:
+                    convs.append((blk.downsample[0], h, w))
+                for conv, ch, cw in convs:
+                    add(conv.geom(), batch, ch, cw, 0)
+                    if backward and (li < 4 or "l6" in heads_bwd):
+                        add(conv.geom(), batch, ch, cw, 1)
+                        add(conv.geom(), batch, ch, cw, 2)
+                h, w = oh, ow
+        g6 = engine.aspp_geom(model.layer6)
+        add(g6, batch, h, w, 0)
+        if backward and "l6" in heads_bwd:
+            add(g6, batch, h, w, 1)
+            add(g6, batch, h, w, 2)
+
+    def d_pass(wh, dgrad_input, wgrad):
+        w, h = wh
+        for i, conv in enumerate(D._convs()):
+            g = conv.geom()
+            st = (19 * h * w, 1, w * 19, 19) if i == 0 else None
+            add(g, batch, h, w, 0, st)
+            if i > 0 or dgrad_input:
+                add(g, batch, h, w, 1)
+            if wgrad:
+                add(g, batch, h, w, 2, st)
+            h, w = g.out_hw(h, w)
+
+    heads = {"l6"} if level == "single-level" else {"l5", "l6"}
+    nD = 1 if level == "single-level" else 2
+    g_pass(src_wh, True, heads)
+    g_pass(tgt_wh, True, heads)
+    for _ in range(nD):
+        d_pass(tsize, True, False)        # G step through the frozen D
+        d_pass(src_wh, False, True)       # D step, source
+        d_pass(tsize, False, True)        # D step, target
+    return inv
+
+
+def cpu_baseline(threads):
+    """The oracle's single-level step at batch 1, 1024x512, fp32 on `threads` host cores."""
+    from oracle import reference_torch as R
+    torch.set_num_threads(threads)
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
+    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
+    cfg = dict(level="single-level", gan="Vanilla", input_size=(1024, 512), input_size_target=(1024, 512))
+    opts = R.make_optimizers(G, None, D2, R.DEFAULT_CFG | cfg)
+    xs = torch.from_numpy(R.det_images((1, 3, 512, 1024), 1)).float()
+    lab = torch.from_numpy(R.det_labels((1, 512, 1024), 2))
+    xt = torch.from_numpy(R.det_images((1, 3, 512, 1024), 3)).float()
+    t0 = time.perf_counter()
+    R.oracle_step(G, None, D2, opts, cfg, 0, [(xs, lab, xt)])
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "1 single-level adversarial step (oracle/reference_torch.py, stock PyTorch "
+                      f"CPU fp32), batch 1, source+target 1024x512; {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from adaptsegnet_amd import kernels as K
+    from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
+    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+
+    level, gan, batch, src_wh, tgt_wh = CONFIGS[args.config]
+    if args.batch:
+        batch = args.batch
+    torch.manual_seed(1338 + rank)
+    model = DeeplabMulti(num_classes=19).to(dev)
+    D1 = FCDiscriminator(num_classes=19).to(dev) if level == "multi-level" else None
+    D2 = FCDiscriminator(num_classes=19).to(dev)
+    if world > 1:  # identical initial weights on every rank (DDP's initial broadcast)
+        for m in (model, D1, D2):
+            if m is not None:
+                for t in list(m.parameters()) + list(m.buffers()):
+                    dist.broadcast(t.data, 0)
+    model.train()
+    scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh)
+    trainer = AdaptSegTrainer(model, D1, D2, scfg)
+    tsize = trainer._target_size()
+
+    g = torch.Generator().manual_seed(1338 + rank)
+    xs = (torch.rand(batch, 3, src_wh[1], src_wh[0], generator=g) * 273.7 - 122.7).to(dev)
+    lab = torch.randint(0, 19, (batch, src_wh[1], src_wh[0]), generator=g)
+    lab[torch.rand(lab.shape, generator=g) < 0.1] = 255
+    lab = lab.to(dev)
+    xt = (torch.rand(batch, 3, tgt_wh[1], tgt_wh[0], generator=g) * 273.7 - 122.7).to(dev)
+    batches = [(xs, lab, xt)]
+
+    for i in range(args.warmup):
+        trainer.step(i, batches)
+    torch.cuda.synchronize()
+
+    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize)
+    step_flops = sum(inv.values())
+    dom = max(inv, key=inv.get)
+    if not args.no_roofline:
+        K.timing_enable(dom)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        L = trainer.step(args.warmup + i, batches)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if not args.no_roofline:
+        K.timing_enable(dom, enable=False)
+        k_ms, k_flops, k_launches = K.timing_read()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = L.values()
+    for k, v in losses.items():
+        if not np.isfinite(v):
+            raise RuntimeError(f"non-finite loss {k}={v}")
+
+    ms_per_step = elapsed / args.steps * 1e3
+    pairs = batch * world * args.steps
+    out = {
+        "metric": METRIC, "value": pairs / elapsed, "unit": "images/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (U[-122.7,151] BGR-mean-subtracted pixels, uniform labels, 10% ignore=255)",
+        "config": {"workload": f"{args.config}: {level} {gan}, batch/GPU {batch}, source "
+                               f"{src_wh[0]}x{src_wh[1]}, target {tgt_wh[0]}x{tgt_wh[1]}",
+                   "global_batch": batch * world, "parallelism": f"dp{world}",
+                   "step_conv_tflop": step_flops / 1e12,
+                   "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
+                   "losses_last_step": losses},
+    }
+    if not args.no_roofline and k_launches:
+        avg_ms = k_ms / k_launches
+        ach = k_flops / (k_ms / 1e3) / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": FP32_MFMA_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": ach / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                           "kernel": f"igemm_kernel selector {dom}", "launches_per_step": k_launches / args.steps,
+                           "avg_launch_ms": avg_ms,
+                           "flop_share_of_step": inv[dom] / step_flops}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            aff = os.cpu_count() or 1
+        threads = min(aff, int(os.environ.get("OMP_NUM_THREADS", aff)))
+        out["cpu_baseline"] = cpu_baseline(threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

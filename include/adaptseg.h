@@ -68,6 +68,8 @@ enum adaptseg_conv_flags {
 };
 
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
+/* Kernel selector (see adaptseg_timing_enable) and K-split count the library would use. */
+int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_id, int *splits);
 
 /* y[n,oh,ow,k] = sum_seg conv(x, w[seg]) + sum_seg bias[seg]   (bias may be NULL) */
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
@@ -200,12 +202,15 @@ int adaptseg_axpy(int64_t n, float alpha, const float *src, float *dst, int flag
 int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
-/* Live kernel timing for the benchmark: when enabled, every launch of the conv kernels   */
-/* of the selected class is bracketed by hipEvents on its stream; the summed durations   */
-/* and summed algorithmic FLOPs are read back after a device synchronise.                */
-/* class: 0 = all conv launches, 1 = 3x3 dilated convs (dil > 1, nseg == 1).             */
+/* Live kernel timing for the benchmark: when enabled, every launch of the selected          */
+/* implicit-GEMM conv kernel symbol is bracketed by hipEvents on its stream; the summed      */
+/* durations and summed algorithmic FLOPs (2*N*OH*OW*K*C*KH*KW*nseg per launch) are read    */
+/* back after a device synchronise.  selector = -1: every igemm launch; otherwise           */
+/* selector = 100*op + 10*tile_cfg + 2*vecA + vecB, which names ONE kernel symbol            */
+/* igemm_kernel<op, tile, vecA, vecB> (op: 0 fwd, 1 bwd-data, 2 bwd-weight;                  */
+/* tile_cfg: 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256).                               */
 /* ------------------------------------------------------------------------------------ */
-int adaptseg_timing_enable(int enable, int conv_class);
+int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
 
 #ifdef __cplusplus

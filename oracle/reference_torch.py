@@ -281,10 +281,11 @@ def _set_rg(Q, flag):
         t.requires_grad_(flag)
 
 
-def oracle_step(G, D1, D2, opts, cfg, i_iter, batches):
+def oracle_step(G, D1, D2, opts, cfg, i_iter, batches, bn_train=True):
     """One iteration of train_gta2cityscapes_multi.py:373-464 (single) or :560-683 (multi).
 
     Returns a dict of host loss values accumulated like the reference's *_value sums.
+    ``bn_train=False`` runs the generator with eval-mode BN (model.eval()).
     """
     opt, opt_d1, opt_d2 = opts
     c = dict(DEFAULT_CFG)
@@ -311,11 +312,11 @@ def oracle_step(G, D1, D2, opts, cfg, i_iter, batches):
     for images, labels, images_t in batches:
         if c["level"] == "single-level":
             _set_rg(D2, False)
-            _, pred2 = g_forward(G, images, c["input_size"])
+            _, pred2 = g_forward(G, images, c["input_size"], bn_train)
             loss_seg2 = F.cross_entropy(pred2, labels, ignore_index=255)
             (loss_seg2 / n_sub).backward()
             acc("loss_seg2", loss_seg2.item() / n_sub)
-            _, pred_t2 = g_forward(G, images_t, tsize)
+            _, pred_t2 = g_forward(G, images_t, tsize, bn_train)
             l_adv = adv_loss(d_forward(D2, F.softmax(pred_t2, dim=1)), src_lbl, c["gan"])
             (c["lambda_adv_target2"] * l_adv / n_sub).backward()
             acc("loss_adv_target2", l_adv.item() / n_sub)
@@ -327,13 +328,13 @@ def oracle_step(G, D1, D2, opts, cfg, i_iter, batches):
         else:
             _set_rg(D1, False)
             _set_rg(D2, False)
-            pred1, pred2 = g_forward(G, images, c["input_size"])
+            pred1, pred2 = g_forward(G, images, c["input_size"], bn_train)
             loss_seg1 = F.cross_entropy(pred1, labels, ignore_index=255)
             loss_seg2 = F.cross_entropy(pred2, labels, ignore_index=255)
             ((loss_seg2 + c["lambda_seg"] * loss_seg1) / n_sub).backward()
             acc("loss_seg1", loss_seg1.item() / n_sub)
             acc("loss_seg2", loss_seg2.item() / n_sub)
-            pt1, pt2 = g_forward(G, images_t, tsize)
+            pt1, pt2 = g_forward(G, images_t, tsize, bn_train)
             a1 = adv_loss(d_forward(D1, F.softmax(pt1, dim=1)), src_lbl, c["gan"])
             a2 = adv_loss(d_forward(D2, F.softmax(pt2, dim=1)), src_lbl, c["gan"])
             ((c["lambda_adv_target1"] * a1 + c["lambda_adv_target2"] * a2) / n_sub).backward()

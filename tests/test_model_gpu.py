@@ -89,6 +89,7 @@ def test_deeplab_forward_backward(data, train):
         worst_f, worst_c = max(worst_f, f), min(worst_c, c)
         if not train:
             assert f < 5e-3, (name, f)
+    print(f"train={train}: worst grad rel-frob {worst_f:.3e}, worst cosine {worst_c:.6f}")
     assert worst_c > 0.99 and worst_f < 0.1, (worst_f, worst_c)
     if train:  # running statistics and the batch counter
         sd = m.state_dict()
@@ -135,41 +136,105 @@ def test_discriminator(data):
         assert rel(p.grad, D[name].grad) < 1e-4, name
 
 
-@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
-def test_adversarial_step(data, level, gan):
-    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
+def _oracle_run(level, gan, cfg, data, dtype, iters, bn_train=True):
     xs, lab, xt = data
-    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
-    G = R.to_torch(R.det_state(R.g_specs(), 1338), trainable=R.g_trainable)
-    D1 = R.to_torch(R.det_state(R.d_specs(), 2001), trainable=lambda k: True)
-    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), trainable=lambda k: True)
-    g_before = {k: v.detach().clone() for k, v in G.items()}
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=dtype, trainable=R.g_trainable)
+    D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=dtype, trainable=lambda k: True)
+    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=dtype, trainable=lambda k: True)
     opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
-    m, d1, d2 = build_g(), build_d(2001), build_d(2002)
-    tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2, StepConfig(**cfg))
-    batch_dev = [(xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))]
-    for it in range(2):
-        ref = R.oracle_step(G, D1, D2, opts, cfg, it, [(xs, lab, xt)])
-        got = tr.step(it, batch_dev).values()
-        for k, v in ref.items():
-            assert abs(got[k] - v) <= 2e-3 * abs(v) + 1e-6, (k, got[k], v)
-    sd = m.state_dict()
+    losses = [R.oracle_step(G, D1, D2, opts, cfg, it, [(xs.to(dtype), lab, xt.to(dtype))], bn_train)
+              for it in range(iters)]
+    return G, D1, D2, losses
+
+
+def _updates(Gs, keys, g0, sd=None):
+    if sd is None:
+        return torch.cat([(Gs[k].detach().double() - torch.from_numpy(g0[k])).flatten() for k in keys])
+    return torch.cat([(sd[k].double().cpu() - torch.from_numpy(g0[k])).flatten() for k in keys])
+
+
+def _groups(G, level):
     groups = {"trunk": [], "heads": []}
     for k, v in G.items():
         if v.dtype.is_floating_point and v.requires_grad:
+            if k.startswith("layer5") and level == "single-level":
+                continue  # receives no gradient in single-level (checked separately)
             groups["heads" if k.startswith("layer5") or k.startswith("layer6") else "trunk"].append(k)
-    for gname, keys in groups.items():
-        dref = torch.cat([(G[k].detach() - g_before[k]).flatten() for k in keys])
-        dgot = torch.cat([(sd[k].double().cpu() - g_before[k]).flatten() for k in keys])
-        f, c = frob(dgot, dref)
-        assert c > 0.99 and f < 0.1, (gname, f, c)
+    return groups
+
+
+def _run_hip(level, gan, cfg, data, iters, bn_train):
+    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+    xs, lab, xt = data
+    m, d1, d2 = build_g(), build_d(2001), build_d(2002)
+    m.train(bn_train)
+    tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2, StepConfig(**cfg))
+    batch_dev = [(xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))]
+    got = [tr.step(it, batch_dev).values() for it in range(iters)]
+    return m, d1, d2, got
+
+
+@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+def test_adversarial_step_eval_bn(data, level, gan):
+    """Six full iterations with eval-mode BN (well conditioned): every loss of every iteration
+    within 1e-4 rel of the fp64 oracle; generator/discriminator parameter updates within 2x
+    the fp32 oracle's own distance to fp64 (the fp32 parameter-rounding floor) + 1e-4."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    iters = 6
+    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
+    G, D1, D2, ref = _oracle_run(level, gan, cfg, data, torch.float64, iters, bn_train=False)
+    G32, D132, D232, _ = _oracle_run(level, gan, cfg, data, torch.float32, iters, bn_train=False)
+    m, d1, d2, got = _run_hip(level, gan, cfg, data, iters, bn_train=False)
+    for it in range(iters):
+        for k, v in ref[it].items():
+            print(f"eval-BN iter{it} {k}: hip={got[it][k]:.7f} fp64={v:.7f}")
+            assert abs(got[it][k] - v) <= 1e-4 * abs(v) + 1e-7, (it, k, got[it][k], v)
+    g0 = R.det_state(R.g_specs(), 1338)
+    sd = m.state_dict()
+    for gname, keys in _groups(G, level).items():
+        dref = _updates(G, keys, g0)
+        f, c = frob(_updates(None, keys, g0, sd), dref)
+        f32, _ = frob(_updates(G32, keys, g0), dref)
+        print(f"eval-BN {gname} update: rel-frob {f:.3e} (fp32 oracle {f32:.3e}) cos {c:.8f}")
+        assert f <= 2 * f32 + 1e-4, (gname, f, f32)
+    for dname, dm, DD, DD32, seed in (("D1", d1, D1, D132, 2001), ("D2", d2, D2, D232, 2002)):
+        if dname == "D1" and level == "single-level":
+            continue
+        d0 = R.det_state(R.d_specs(), seed)
+        dref = _updates(DD, list(DD), d0)
+        f, c = frob(_updates(None, list(DD), d0, dm.state_dict()), dref)
+        f32, _ = frob(_updates(DD32, list(DD), d0), dref)
+        print(f"eval-BN {dname} update: rel-frob {f:.3e} (fp32 oracle {f32:.3e}) cos {c:.8f}")
+        assert f <= 2 * f32 + 1e-3, (dname, f, f32)
+
+
+@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+def test_adversarial_step_train_bn(data, level, gan):
+    """Two iterations with train-mode BN (the training semantics).  Iteration-0 losses are
+    tight (1e-3 rel).  After one update the trajectory is chaotic at random init (SURVEY.md
+    §4: the reference's own fp32-vs-fp64 weight-grad spread is 4-5 %), so iteration-1 losses
+    are a sanity bound — within max(5x the fp32 oracle's error, 25 % rel) — and parameter
+    updates within 2x the fp32 oracle's distance to fp64.  test_adversarial_step_eval_bn is
+    the tight end-to-end check."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
+    G, D1, D2, ref = _oracle_run(level, gan, cfg, data, torch.float64, 2)
+    G32, _, _, ref32 = _oracle_run(level, gan, cfg, data, torch.float32, 2)
+    m, d1, d2, got = _run_hip(level, gan, cfg, data, 2, bn_train=True)
+    for it in range(2):
+        for k, v in ref[it].items():
+            err, err32 = abs(got[it][k] - v), abs(ref32[it][k] - v)
+            bound = 1e-3 * abs(v) + 1e-6 if it == 0 else max(5 * err32, 0.25 * abs(v)) + 1e-6
+            print(f"iter{it} {k}: hip={got[it][k]:.6f} fp64={v:.6f} fp32-oracle={ref32[it][k]:.6f}")
+            assert err <= bound, (it, k, got[it][k], v, ref32[it][k])
+    g0 = R.det_state(R.g_specs(), 1338)
+    sd = m.state_dict()
+    for gname, keys in _groups(G, level).items():
+        dref = _updates(G, keys, g0)
+        f, c = frob(_updates(None, keys, g0, sd), dref)
+        f32, c32 = frob(_updates(G32, keys, g0), dref)
+        print(f"{gname}: hip frob={f:.3e} cos={c:.6f} | fp32-oracle frob={f32:.3e} cos={c32:.6f}")
+        assert f <= max(2 * f32, 0.02) and c >= min(0.99, 1 - 2 * (1 - c32)), (gname, f, c, f32, c32)
     if level == "single-level":  # layer5 gets no gradient -> untouched, like torch's SGD
-        assert torch.equal(sd["layer5.conv2d_list.0.weight"].cpu().double(),
-                           g_before["layer5.conv2d_list.0.weight"].float().double())
-    d0 = R.det_state(R.d_specs(), 2002)
-    dsd = d2.state_dict()
-    dref = torch.cat([(D2[k].detach() - torch.from_numpy(d0[k])).flatten() for k in D2])
-    dgot = torch.cat([(dsd[k].double().cpu() - torch.from_numpy(d0[k]).float().double()).flatten() for k in D2])
-    f, c = frob(dgot, dref)
-    assert c > 0.99 and f < 0.1, ("D2", f, c)
+        assert torch.equal(sd["layer5.conv2d_list.0.weight"].cpu(),
+                           torch.from_numpy(g0["layer5.conv2d_list.0.weight"]).float())

@@ -51,6 +51,10 @@ CONV_CASES = [
     (2, 128, 6, 8, 1, 4, 2, (1,), (1,), True),            # D classifier (Cout 1)
     (2, 64, 7, 9, 19, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP, dil > spatial
     (1, 2048, 3, 5, 7, 1, 1, (0,), (1,), False),          # split-K path (M=15, K=2048)
+    (2, 32, 15, 17, 64, 3, 2, (1,), (1,), False),         # stride-2 3x3, odd sizes (parity classes)
+    (1, 64, 9, 11, 32, 4, 2, (1,), (1,), True),           # stride-2 4x4, odd sizes
+    (3, 64, 20, 24, 64, 3, 1, (1,), (1,), False),         # N = 64 tile (256x64)
+    (2, 96, 12, 10, 96, 1, 2, (0,), (1,), False),         # 1x1 stride 2, empty parity classes
 ]
 
 

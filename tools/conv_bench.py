@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Per-shape timing of every distinct conv product in one c2 adversarial step.
+
+    python tools/conv_bench.py [--batch 4] [--reps 5]
+
+Prints, for each (conv geometry, op) of DeeplabMulti + FCDiscriminator at 1024x512, the
+kernel selector, K-split, launches per step, average time and TFLOP/s, then the step total.
+Used to iterate on the igemm kernels without running the whole step.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from adaptsegnet_amd import kernels as K  # noqa: E402
+
+
+def shapes(batch, W=1024, H=512):
+    """(name, geom, n, h, w, ops, count/step, input strides or None)."""
+    out = collections.OrderedDict()
+
+    def add(name, g, n, h, w, ops, count, st=None):
+        key = (g, n, h, w, ops, st)
+        if key in out:
+            out[key][0] += count
+        else:
+            out[key] = [count, name]
+
+    # generator, 2 passes (source + target), single-level: layer5 fwd only
+    h, w = H, W
+    add("stem", K.ConvGeom(3, 64, 7, 7, 2, (3,), (1,)), batch, h, w, (0, 2), 2, (3 * h * w, h * w, w, 1))
+    h, w = 256, 512
+    h, w = 128, 256
+    cin = 64
+    for li, (planes, nblk, stride, dil) in enumerate(((64, 3, 1, 1), (128, 4, 2, 1), (256, 23, 1, 2), (512, 3, 1, 4)), 1):
+        if li == 4:
+            add("aspp5", K.ConvGeom(1024, 19, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24)), batch, h, w, (0,), 2)
+        for b in range(nblk):
+            s = stride if b == 0 else 1
+            bin_ = cin if b == 0 else planes * 4
+            g1 = K.ConvGeom(bin_, planes, 1, 1, s)
+            add(f"l{li}.conv1", g1, batch, h, w, (0, 1, 2), 2)
+            oh, ow = g1.out_hw(h, w)
+            add(f"l{li}.conv2", K.ConvGeom(planes, planes, 3, 3, 1, (dil,), (dil,)), batch, oh, ow, (0, 1, 2), 2)
+            add(f"l{li}.conv3", K.ConvGeom(planes, planes * 4, 1, 1), batch, oh, ow, (0, 1, 2), 2)
+            if b == 0:
+                add(f"l{li}.ds", K.ConvGeom(bin_, planes * 4, 1, 1, s), batch, h, w, (0, 1, 2), 2)
+            h, w = oh, ow
+        cin = planes * 4
+    add("aspp6", K.ConvGeom(2048, 19, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24)), batch, h, w, (0, 1, 2), 2)
+    # discriminator: fwd x3, dgrad x(1 + 2 for convs 2..5), wgrad x2
+    h, w = H, W
+    chans = (19, 64, 128, 256, 512, 1)
+    for i in range(5):
+        g = K.ConvGeom(chans[i], chans[i + 1], 4, 4, 2, (1,), (1,))
+        st = (19 * h * w, 1, w * 19, 19) if i == 0 else None
+        add(f"D.conv{i + 1}", g, batch, h, w, (0,), 3, st)
+        add(f"D.conv{i + 1}", g, batch, h, w, (1,), 1 if i == 0 else 3)
+        add(f"D.conv{i + 1}", g, batch, h, w, (2,), 2, st)
+        h, w = g.out_hw(h, w)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--filter", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    tot_ms, tot_fl = 0.0, 0.0
+    per_op = collections.defaultdict(lambda: [0.0, 0.0])
+    print(f"{'conv':<10} {'op':>3} {'n':>2} {'hxw':>9} {'cin':>5} {'cout':>5} {'k':>2} {'sel':>4} {'spl':>3} "
+          f"{'cnt':>4} {'avg us':>9} {'TF/s':>7}")
+    for (g, n, h, w, ops, st), (count, name) in shapes(args.batch).items():
+        if args.filter and args.filter not in name:
+            continue
+        oh, ow = g.out_hw(h, w)
+        if st is None:
+            x = torch.randn(n, h, w, g.cin, device=dev)
+        else:
+            x = torch.randn(n, g.cin, h, w, device=dev).permute(0, 2, 3, 1).contiguous() \
+                if st[1] == 1 else torch.randn(n, g.cin, h, w, device=dev)
+        ws = [torch.randn(g.cout, g.kh, g.kw, g.cin, device=dev) * 0.01 for _ in range(g.nseg)]
+        bs = [torch.randn(g.cout, device=dev) for _ in range(g.nseg)]
+        dy = torch.randn(n, oh, ow, g.cout, device=dev)
+        dws = [torch.zeros_like(t) for t in ws]
+        dbs = [torch.zeros_like(t) for t in bs]
+        for op in ops:
+            def run():
+                if op == 0:
+                    K.conv_fwd(g, x, n, h, w, ws, bs, strides=st)
+                elif op == 1:
+                    K.conv_dgrad(g, dy, n, h, w, ws)
+                else:
+                    K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=st)
+            run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            fl = g.flops(n, h, w)
+            sel, sp = K.conv_kernel_id(g, n, h, w, op, st)
+            c = count[op] if isinstance(count, dict) else count
+            tot_ms += ms * c
+            tot_fl += fl * c
+            per_op[op][0] += ms * c
+            per_op[op][1] += fl * c
+            print(f"{name:<10} {op:>3} {n:>2} {h:>4}x{w:<4} {g.cin:>5} {g.cout:>5} {g.kh:>2} {sel:>4} {sp:>3} "
+                  f"{c:>4} {ms * 1e3:9.1f} {fl / ms / 1e9:7.1f}", flush=True)
+    for op, (ms, fl) in sorted(per_op.items()):
+        print(f"op {op}: {ms:8.2f} ms/step  {fl / 1e12:6.3f} TFLOP  {fl / ms / 1e9:6.1f} TF/s")
+    print(f"TOTAL conv: {tot_ms:8.2f} ms/step, {tot_fl / 1e12:.3f} TFLOP, {tot_fl / tot_ms / 1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU round: parity tests -> smoke -> bench -> rocprofv3 kernel trace.  Each GPU step has
+# its own time limit; a crash/fault (rc > 1 for pytest) ends the round.
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+TAG=${1:-r}
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -s > gpurun_out/pytest_gpu_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu_$TAG.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit 3
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench_$TAG.log 2>&1 || exit 4
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || exit 5
