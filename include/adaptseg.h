@@ -206,9 +206,9 @@ int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream)
 /* implicit-GEMM conv kernel symbol is bracketed by hipEvents on its stream; the summed      */
 /* durations and summed algorithmic FLOPs (2*N*OH*OW*K*C*KH*KW*nseg per launch) are read    */
 /* back after a device synchronise.  selector = -1: every igemm launch; otherwise           */
-/* selector = 100*op + 10*tile_cfg + 2*vecA + vecB, which names ONE kernel symbol            */
-/* igemm_kernel<op, tile, vecA, vecB> (op: 0 fwd, 1 bwd-data, 2 bwd-weight;                  */
-/* tile_cfg: 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256).                               */
+/* selector = 100*op + 10*tile + variant names ONE kernel symbol: op 0 fwd, 1 bwd-data,     */
+/* 2 bwd-weight; tile 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256, 4 = 256x64;          */
+/* variant 0..3 = generic gather (2*vecA + vecB), 4 = FAST, 5 = FAST stride-2 parity path.   */
 /* ------------------------------------------------------------------------------------ */
 int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
