@@ -54,36 +54,126 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
   }
 }
 
-// Bias gradient: db[seg][co] (+)= sum_m dY[m][co].  One block per 64-channel strip x row split.
-__global__ void bias_grad_partial_kernel(const float *dy, int rows, int cout, int rows_per_split,
-                                         float *partial) {
-  // block: 256 threads = 64 channels x 4 row lanes
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  const int r0 = blockIdx.y * rows_per_split;
-  const int r1 = min(rows, r0 + rows_per_split);
-  float s = 0.f;
-  if (c < cout)
-    for (int r = r0 + rl; r < r1; r += 4) s += dy[(size_t)r * cout + c];
-  __shared__ float red[256];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (rl == 0 && c < cout) {
-    float t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
-    partial[(size_t)blockIdx.y * cout + c] = t;
+// Vectorised split-K reduction: 4 consecutive columns per thread (N % 4 == 0 and, for weight
+// gradients, segments of kseg % 4 == 0), 32-bit indexing, slabs summed in split order.
+__global__ void splitk_reduce4_kernel(const ConvParams p, const float *__restrict__ slab, int mode,
+                                      FastDiv fdn4) {
+  const uint32_t n4 = (uint32_t)p.N / 4;
+  const uint32_t total4 = (uint32_t)p.M * n4;
+  const float4 *s4 = reinterpret_cast<const float4 *>(slab);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+    for (int s = 0; s < p.splits; ++s) {
+      const float4 t = s4[(size_t)s * total4 + i];
+      v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+    }
+    const uint32_t row = fdiv(i, fdn4);
+    const int col = (int)(i - row * n4) * 4;
+    float *o;
+    if (mode == MODE_WGRAD) {
+      const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
+      float *dst = seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3];
+      o = dst + (size_t)row * p.kseg + (col - seg * p.kseg);
+      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
+        const float4 a = *reinterpret_cast<const float4 *>(o);
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+    } else {
+      const size_t idx = (size_t)row * p.N + col;
+      o = p.out + idx;
+      if (mode == MODE_FWD) {
+        for (int s = 0; s < p.nseg; ++s) {
+          const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
+          if (bp) {
+            const float4 b = *reinterpret_cast<const float4 *>(bp + col);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          }
+        }
+      }
+      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
+        const float4 a = *reinterpret_cast<const float4 *>(o);
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+      if (p.flags & ADAPTSEG_EPI_RESIDUAL) {
+        const float4 a = *reinterpret_cast<const float4 *>(p.res + idx);
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+      if (p.flags & ADAPTSEG_EPI_LEAKY) {
+        v.x = v.x > 0.f ? v.x : 0.2f * v.x; v.y = v.y > 0.f ? v.y : 0.2f * v.y;
+        v.z = v.z > 0.f ? v.z : 0.2f * v.z; v.w = v.w > 0.f ? v.w : 0.2f * v.w;
+      }
+      if (p.flags & ADAPTSEG_EPI_LEAKY_GRAD) {
+        const float4 a = *reinterpret_cast<const float4 *>(p.aux + idx);
+        v.x = a.x > 0.f ? v.x : 0.2f * v.x; v.y = a.y > 0.f ? v.y : 0.2f * v.y;
+        v.z = a.z > 0.f ? v.z : 0.2f * v.z; v.w = a.w > 0.f ? v.w : 0.2f * v.w;
+      }
+    }
+    *reinterpret_cast<float4 *>(o) = v;
   }
+}
+
+static bool aligned16(const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+// Bias gradient: db[seg][co] (+)= sum_m dY[m][co].  Each block sums a contiguous run of rows
+// of the NHWC gradient with flat coalesced reads: for cout <= 256 thread t owns column t % cout
+// and rows t / cout + j * (256 / cout) (so Cout = 19 uses 247 lanes, not 19 of 64); wider
+// rows loop over their columns.  Partials are [split][cout], reduced by one wave per channel.
+__global__ void __launch_bounds__(256) bias_grad_partial_kernel(const float *__restrict__ dy, int rows, int cout,
+                                                                int rows_per_split, float *partial) {
+  const int r0 = blockIdx.x * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  __shared__ float red[256];
+  if (cout <= 256) {
+    const int rstep = 256 / cout;
+    const int t = threadIdx.x;
+    float s = 0.f;
+    if (t < rstep * cout) {
+      const float *src = dy + (size_t)r0 * cout + t;
+      const int n = r1 - r0 - t / cout;  // rows left for this lane
+#pragma unroll 8
+      for (int j = 0; j < n; j += rstep) s += src[(size_t)j * cout];
+    }
+    red[t] = s;
+    __syncthreads();
+    if (t < cout) {
+      float a = 0.f;
+      for (int q = 0; q < rstep; ++q) a += red[t + q * cout];
+      partial[(size_t)blockIdx.x * cout + t] = a;
+    }
+  } else {
+    for (int col = threadIdx.x; col < cout; col += 256) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = r0; r < r1; ++r) s += dy[(size_t)r * cout + col];
+      partial[(size_t)blockIdx.x * cout + col] = s;
+    }
+  }
+}
+
+// ~16K floats per block, at most 2048 blocks; rows per block a multiple of 256 / cout.
+static void bias_grad_split(int rows, int cout, int *per, int *splits) {
+  const int64_t want = ceil_div((int64_t)rows * cout, 16384);
+  const int64_t s = std::max<int64_t>(1, std::min<int64_t>(want, 2048));
+  const int rstep = cout <= 256 ? 256 / cout : 1;
+  *per = (int)(ceil_div(ceil_div(rows, s), rstep) * rstep);
+  *splits = (int)ceil_div(rows, *per);
 }
 
 struct BiasOut {
   float *db[4];
 };
 
-__global__ void bias_grad_final_kernel(const float *partial, int splits, int cout, BiasOut o, int nseg,
-                                       int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave64 per channel: lanes stride over the splits (fp64), then a fixed shuffle tree.
+__global__ void __launch_bounds__(256) bias_grad_final_kernel(const float *partial, int splits, int cout, BiasOut o,
+                                                              int nseg, int accumulate) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= cout) return;
   double s = 0.0;
-  for (int i = 0; i < splits; ++i) s += partial[(size_t)i * cout + c];
+  for (int i = lane; i < splits; i += 64) s += partial[(size_t)i * cout + c];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane != 0) return;
   for (int g = 0; g < nseg; ++g) {
     float *d = o.db[g];
     if (!d) continue;
@@ -311,8 +401,23 @@ static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s
     ConvParams q = pl.p;
     q.out = final_out;
     size_t total = (size_t)q.M * q.N;
-    int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
-    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
+    bool vec = q.N % 4 == 0 && aligned16(slab);
+    if (mode == MODE_WGRAD) {
+      vec = vec && q.kseg % 4 == 0;
+      for (int g = 0; g < q.nseg; ++g) vec = vec && aligned16(q.dw[g]);
+    } else {
+      vec = vec && aligned16(q.out) && (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res)) &&
+            (!(q.flags & ADAPTSEG_EPI_LEAKY_GRAD) || aligned16(q.aux));
+      if (mode == MODE_FWD)
+        for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
+    }
+    if (vec) {
+      int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256), 8192);
+      splitk_reduce4_kernel<<<blocks, 256, 0, s>>>(q, slab, mode, make_fastdiv((uint32_t)q.N / 4));
+    } else {
+      int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
+      splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
+    }
     AS_CHECK_LAUNCH("splitk_reduce");
   }
   return ADAPTSEG_OK;
@@ -339,8 +444,8 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
   }
   if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
     // bias-gradient partials
-    int rows = d->n * d->oh * d->ow;
-    int splits = (int)std::min<int64_t>(ceil_div(rows, 2048), 256);
+    int per, splits;
+    bias_grad_split(d->n * d->oh * d->ow, d->k, &per, &splits);
     b = std::max(b, (size_t)splits * d->k * sizeof(float));
   }
   *bytes = b;
@@ -437,18 +542,17 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
     for (int g = 0; g < d->nseg; ++g) any |= db[g] != nullptr;
     if (any) {
       int rows = d->n * d->oh * d->ow;
-      int splits = (int)std::min<int64_t>(ceil_div(rows, 2048), 256);
-      int per = (int)ceil_div(rows, splits);
+      int per, splits;
+      bias_grad_split(rows, d->k, &per, &splits);
       size_t need = (size_t)splits * d->k * sizeof(float);
       if (!ws || ws_bytes < need) {
         set_error("conv bias grad: workspace too small");
         return ADAPTSEG_ERR_WORKSPACE;
       }
       float *partial = reinterpret_cast<float *>(ws);
-      dim3 g((unsigned)ceil_div(d->k, 64), splits);
-      bias_grad_partial_kernel<<<g, 256, 0, s>>>(dy, rows, d->k, per, partial);
+      bias_grad_partial_kernel<<<splits, 256, 0, s>>>(dy, rows, d->k, per, partial);
       AS_CHECK_LAUNCH("bias_grad_partial");
-      bias_grad_final_kernel<<<(unsigned)ceil_div(d->k, 256), 256, 0, s>>>(
+      bias_grad_final_kernel<<<(unsigned)ceil_div(d->k, 4), 256, 0, s>>>(
           partial, splits, d->k, o, d->nseg, (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
       AS_CHECK_LAUNCH("bias_grad_final");
     }

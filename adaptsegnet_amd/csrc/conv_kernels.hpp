@@ -821,8 +821,9 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int k = kbase + a_k[i] + e;
-            const int tap = (int)fdiv((uint32_t)min(k, K - 1), p.fd_k);
-            const int co = k - tap * p.k;
+            const int kc = min(k, K - 1);
+            const int tap = (int)fdiv((uint32_t)kc, p.fd_k);
+            const int co = kc - tap * p.k;
             int seg, t, dy, dx;
             seg_geom(p, tap, seg, t, dy, dx);
             const bool v = a_ok[i] && k < K && (unsigned)(a_y[i] - dy) < (unsigned)p.oh &&
@@ -837,8 +838,9 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
         for (int i = 0; i < NQB; ++i) {  // B row k = kbase + r: per-slot (seg, co, t)
           const int k = kbase + b_k[i];
           const bool rv = k < K;
-          const int tap = (int)fdiv((uint32_t)min(k, K - 1), p.fd_k);
-          const int co = k - tap * p.k;
+          const int kc = min(k, K - 1);  // rows past K still form an in-bounds address
+          const int tap = (int)fdiv((uint32_t)kc, p.fd_k);
+          const int co = kc - tap * p.k;
           int seg, t, dy, dx;
           seg_geom(p, tap, seg, t, dy, dx);
           const float *row = seg_ptr(p, seg) + (co * p.taps_per_seg + t) * p.c;

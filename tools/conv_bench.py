@@ -89,10 +89,12 @@ def main():
             x = torch.randn(n, g.cin, h, w, device=dev).permute(0, 2, 3, 1).contiguous() \
                 if st[1] == 1 else torch.randn(n, g.cin, h, w, device=dev)
         ws = [torch.randn(g.cout, g.kh, g.kw, g.cin, device=dev) * 0.01 for _ in range(g.nseg)]
-        bs = [torch.randn(g.cout, device=dev) for _ in range(g.nseg)]
+        # only the ASPP classifiers and the discriminator convs carry a bias
+        has_bias = name.startswith(("aspp", "D."))
+        bs = [torch.randn(g.cout, device=dev) for _ in range(g.nseg)] if has_bias else None
         dy = torch.randn(n, oh, ow, g.cout, device=dev)
         dws = [torch.zeros_like(t) for t in ws]
-        dbs = [torch.zeros_like(t) for t in bs]
+        dbs = [torch.zeros_like(t) for t in bs] if has_bias else None
         for op in ops:
             def run():
                 if op == 0:

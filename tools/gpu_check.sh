@@ -9,6 +9,8 @@ cd $R
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -s > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu_$TAG.log
 if [ $rc -gt 1 ]; then exit $rc; fi
+# a device fault surfaces as ordinary test failures: stop before touching the GPU again
+if grep -qiE "illegal memory access|memory access fault|hipErrorIllegalAddress" gpurun_out/pytest_gpu_$TAG.log; then exit 7; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit 3
 timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench_$TAG.log 2>&1 || exit 4
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || exit 5
