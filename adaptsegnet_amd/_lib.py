@@ -20,6 +20,8 @@ EPI_LEAKY = 1
 EPI_ACCUMULATE = 2
 EPI_LEAKY_GRAD = 4
 EPI_RESIDUAL = 8
+EPI_RELU = 16
+EPI_RELU_GRAD = 32
 CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT = 0, 1, 2
 
 
@@ -58,7 +60,7 @@ _SIGS = {
     "adaptseg_bn_workspace_size": [_L, _I, ctypes.POINTER(_SZ)],
     "adaptseg_bn_fwd_train": [_L, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_infer": [_L, _I, _P, _P, _P, _P, _P, _F, _P, _P, _I, _P],
-    "adaptseg_bn_bwd": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
+    "adaptseg_bn_bwd": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
     "adaptseg_maxpool2d_fwd": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "adaptseg_maxpool2d_bwd": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "adaptseg_upsample_workspace_size": [_I, _I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],

@@ -13,12 +13,26 @@
 
 namespace adaptseg {
 
+// ReLU mask without reading y: y > 0  <=>  (x - mean)*invstd*w + b > 0, evaluated with the
+// same expression bn_apply_kernel uses (valid for BNs without a residual input).
+__device__ __forceinline__ float bn_affine(float v, float m, float is, float w, float b) {
+  return (v - m) * is * w + b;
+}
+__device__ __forceinline__ float4 relu_mask_from_x(float4 g, float4 v, float4 m, float4 is, float4 w, float4 b) {
+  g.x = bn_affine(v.x, m.x, is.x, w.x, b.x) > 0.f ? g.x : 0.f;
+  g.y = bn_affine(v.y, m.y, is.y, w.y, b.y) > 0.f ? g.y : 0.f;
+  g.z = bn_affine(v.z, m.z, is.z, w.z, b.z) > 0.f ? g.z : 0.f;
+  g.w = bn_affine(v.w, m.w, is.w, w.w, b.w) > 0.f ? g.w : 0.f;
+  return g;
+}
+
 // Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
 // Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
 template <int MODE>  // 0: stats (shifted by pivot x[0][c]), 1: backward sums
 __global__ void __launch_bounds__(256)
 bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const float *__restrict__ dy,
-                 const float *__restrict__ y, const float *__restrict__ mean, int relu,
+                 const float *__restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
+                 const float *__restrict__ w, const float *__restrict__ b, int relu,
                  int64_t rows_per_split, float *__restrict__ partial) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc;   // channel quad within block
@@ -29,9 +43,15 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
   const int64_t r1 = min(rows, r0 + rows_per_split);
   float4 s1 = make_float4(0, 0, 0, 0), s2 = make_float4(0, 0, 0, 0);
   float4 piv = make_float4(0, 0, 0, 0);
+  float4 is = make_float4(0, 0, 0, 0), ww = is, bb = is;
   if (cok) {
     if (MODE == 0) piv = *reinterpret_cast<const float4 *>(x + c0);
     else piv = *reinterpret_cast<const float4 *>(mean + c0);
+    if (MODE == 1 && relu == 2) {
+      is = *reinterpret_cast<const float4 *>(invstd + c0);
+      ww = w ? *reinterpret_cast<const float4 *>(w + c0) : make_float4(1, 1, 1, 1);
+      bb = b ? *reinterpret_cast<const float4 *>(b + c0) : make_float4(0, 0, 0, 0);
+    }
     for (int64_t r = r0 + rl; r < r1; r += tr) {
       float4 v = *reinterpret_cast<const float4 *>(x + r * C + c0);
       float4 d = make_float4(v.x - piv.x, v.y - piv.y, v.z - piv.z, v.w - piv.w);
@@ -40,10 +60,12 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
         s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
       } else {
         float4 g = *reinterpret_cast<const float4 *>(dy + r * C + c0);
-        if (relu) {
+        if (relu == 1) {
           float4 o = *reinterpret_cast<const float4 *>(y + r * C + c0);
           g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
           g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
+        } else if (relu == 2) {
+          g = relu_mask_from_x(g, v, piv, is, ww, bb);
         }
         s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
         s2.x += g.x * d.x; s2.y += g.y * d.y; s2.z += g.z * d.z; s2.w += g.w * d.w;
@@ -135,10 +157,10 @@ __global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__
     float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
     float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
     float4 o;
-    o.x = (v.x - m.x) * is.x * ww.x + bb.x;
-    o.y = (v.y - m.y) * is.y * ww.y + bb.y;
-    o.z = (v.z - m.z) * is.z * ww.z + bb.z;
-    o.w = (v.w - m.w) * is.w * ww.w + bb.w;
+    o.x = bn_affine(v.x, m.x, is.x, ww.x, bb.x);
+    o.y = bn_affine(v.y, m.y, is.y, ww.y, bb.y);
+    o.z = bn_affine(v.z, m.z, is.z, ww.z, bb.z);
+    o.w = bn_affine(v.w, m.w, is.w, ww.w, bb.w);
     if (res) {
       float4 r = reinterpret_cast<const float4 *>(res)[i];
       o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
@@ -153,25 +175,32 @@ __global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__
 // dx / dres may alias dy (in-place gradient): each element is read before it is written.
 __global__ void bn_bwd_apply_kernel(int64_t total4, int C, const float *dy,
                                     const float *__restrict__ y, const float *__restrict__ x,
-                                    const float *__restrict__ w, const float *__restrict__ mean,
+                                    const float *__restrict__ w, const float *__restrict__ b,
+                                    const float *__restrict__ mean,
                                     const float *__restrict__ invstd, const float *__restrict__ coef,
                                     float *dx, float *dres, int relu, int train) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
     float4 g = reinterpret_cast<const float4 *>(dy)[i];
-    if (relu) {
+    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
+    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
+    float4 v = make_float4(0, 0, 0, 0), m = v;
+    if (train) {
+      v = reinterpret_cast<const float4 *>(x)[i];
+      m = *reinterpret_cast<const float4 *>(mean + c);
+    }
+    if (relu == 1) {
       float4 o = reinterpret_cast<const float4 *>(y)[i];
       g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
       g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
+    } else if (relu == 2) {
+      const float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
+      g = relu_mask_from_x(g, v, m, is, ww, bb);
     }
     if (dres) reinterpret_cast<float4 *>(dres)[i] = g;
-    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
-    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
     float4 o;
     if (train) {
-      float4 v = reinterpret_cast<const float4 *>(x)[i];
-      float4 m = *reinterpret_cast<const float4 *>(mean + c);
       float4 mg = *reinterpret_cast<const float4 *>(coef + c);
       float4 mgx = *reinterpret_cast<const float4 *>(coef + C + c);
       o.x = ww.x * is.x * (g.x - mg.x - (v.x - m.x) * is.x * mgx.x);
@@ -266,7 +295,7 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
   ReducePlan r = reduce_plan(rows, c);
   float *partial = reinterpret_cast<float *>(ws);
   bn_reduce_kernel<0><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
-                                                                0, r.per, partial);
+                                                                nullptr, nullptr, nullptr, 0, r.per, partial);
   AS_CHECK_LAUNCH("bn_reduce<stats>");
   bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
                                                                    save_invstd, running_mean, running_var,
@@ -293,10 +322,13 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
 }
 
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
-                    const float *save_mean, const float *save_invstd, float *dx, float *dres, int relu, int train,
-                    void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                    const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
+                    int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
-  AS_CHECK_ARG(dy && dx && save_invstd && (!relu || y) && (!train || (x && save_mean)), "bn_bwd: null pointer");
+  AS_CHECK_ARG(dy && dx && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
+  AS_CHECK_ARG(!relu || y || train, "bn_bwd: relu without y needs train mode (mask from x)");
+  // relu mode: 1 = mask from the saved output y, 2 = recomputed from x (y == NULL)
+  const int rmode = relu ? (y ? 1 : 2) : 0;
   hipStream_t s = as_stream(stream);
   float *coef = nullptr;
   if (train) {
@@ -308,16 +340,17 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
     ReducePlan r = reduce_plan(rows, c);
     float *partial = reinterpret_cast<float *>(ws);
     coef = partial + (size_t)r.splits * 2 * c;
-    bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean, relu,
-                                                                  r.per, partial);
+    bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
+                                                                  save_invstd, weight, bias, rmode, r.per,
+                                                                  partial);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
                                                                    coef);
     AS_CHECK_LAUNCH("bn_bwd_final");
   }
   int64_t total4 = rows * c / 4;
-  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, y, x, weight, save_mean, save_invstd, coef,
-                                                       dx, dres, relu, train);
+  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, y, x, weight, bias, save_mean, save_invstd,
+                                                       coef, dx, dres, rmode, train);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
 }

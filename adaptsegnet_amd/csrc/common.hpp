@@ -53,6 +53,21 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
 
 constexpr int kWave = 64;
 
+// Fused conv epilogue activations: LEAKY (slope 0.2, discriminator) or RELU (slope 0, VGG);
+// the *_GRAD forms scale a data gradient by the activation's derivative at aux (the
+// activation OUTPUT, whose sign equals the pre-activation's).
+__device__ __forceinline__ float epi_act(float v, int flags) {
+  if (flags & ADAPTSEG_EPI_LEAKY) v = v > 0.f ? v : 0.2f * v;
+  if (flags & ADAPTSEG_EPI_RELU) v = v > 0.f ? v : 0.f * v;
+  return v;
+}
+__device__ __forceinline__ float epi_act_grad(float v, float a, int flags) {
+  if (flags & ADAPTSEG_EPI_LEAKY_GRAD) v = a > 0.f ? v : 0.2f * v;
+  if (flags & ADAPTSEG_EPI_RELU_GRAD) v = a > 0.f ? v : 0.f;
+  return v;
+}
+constexpr int kEpiActGrad = ADAPTSEG_EPI_LEAKY_GRAD | ADAPTSEG_EPI_RELU_GRAD;
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace adaptseg

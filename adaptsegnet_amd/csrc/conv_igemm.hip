@@ -18,6 +18,7 @@
 // 32x32x2 MFMA with one ds_read_b32 per operand, which is conflict-free.  Small GEMM
 // grids are split along K into fp32 slabs that a deterministic reduce kernel sums.
 #include "conv_kernels.hpp"
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -47,27 +48,48 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
       }
       if (p.flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
       if (p.flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
-      if (p.flags & ADAPTSEG_EPI_LEAKY) v = v > 0.f ? v : 0.2f * v;
-      if (p.flags & ADAPTSEG_EPI_LEAKY_GRAD) v = p.aux[idx] > 0.f ? v : 0.2f * v;
+      v = epi_act(v, p.flags);
+      if (p.flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], p.flags);
       p.out[idx] = v;
     }
   }
 }
 
 // Vectorised split-K reduction: 4 consecutive columns per thread (N % 4 == 0 and, for weight
-// gradients, segments of kseg % 4 == 0), 32-bit indexing, slabs summed in split order.
-__global__ void splitk_reduce4_kernel(const ConvParams p, const float *__restrict__ slab, int mode,
-                                      FastDiv fdn4) {
+// gradients, segments of kseg % 4 == 0), 32-bit indexing.  G split-groups per block: thread
+// (g, lane) sums slabs g, g+G, ... of float4 `lane`, then the G partials are added in fixed
+// order through LDS — deterministic, and a 256-split reduce is 16 loads deep, not 256.
+template <int G>
+__global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p, const float *__restrict__ slab,
+                                                             int mode, FastDiv fdn4) {
+  constexpr int L = 256 / G;
   const uint32_t n4 = (uint32_t)p.N / 4;
   const uint32_t total4 = (uint32_t)p.M * n4;
   const float4 *s4 = reinterpret_cast<const float4 *>(slab);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x % L, g = threadIdx.x / L;
+  __shared__ float4 red[G > 1 ? 256 : 1];
+  for (uint32_t base = blockIdx.x * L; base < total4; base += gridDim.x * L) {  // block-uniform trip count
+    const uint32_t i = base + lane;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < total4) {
 #pragma unroll 8
-    for (int s = 0; s < p.splits; ++s) {
-      const float4 t = s4[(size_t)s * total4 + i];
-      v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+      for (int s = g; s < p.splits; s += G) {
+        const float4 t = s4[(size_t)s * total4 + i];
+        v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+      }
     }
+    if constexpr (G > 1) {
+      red[threadIdx.x] = v;
+      __syncthreads();
+      if (g == 0)
+        for (int q = 1; q < G; ++q) {
+          const float4 t = red[q * L + lane];
+          v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+        }
+      __syncthreads();
+      if (g != 0) continue;
+    }
+    if (i >= total4) continue;
     const uint32_t row = fdiv(i, fdn4);
     const int col = (int)(i - row * n4) * 4;
     float *o;
@@ -99,14 +121,12 @@ __global__ void splitk_reduce4_kernel(const ConvParams p, const float *__restric
         const float4 a = *reinterpret_cast<const float4 *>(p.res + idx);
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
-      if (p.flags & ADAPTSEG_EPI_LEAKY) {
-        v.x = v.x > 0.f ? v.x : 0.2f * v.x; v.y = v.y > 0.f ? v.y : 0.2f * v.y;
-        v.z = v.z > 0.f ? v.z : 0.2f * v.z; v.w = v.w > 0.f ? v.w : 0.2f * v.w;
-      }
-      if (p.flags & ADAPTSEG_EPI_LEAKY_GRAD) {
+      v.x = epi_act(v.x, p.flags); v.y = epi_act(v.y, p.flags);
+      v.z = epi_act(v.z, p.flags); v.w = epi_act(v.w, p.flags);
+      if (p.flags & kEpiActGrad) {
         const float4 a = *reinterpret_cast<const float4 *>(p.aux + idx);
-        v.x = a.x > 0.f ? v.x : 0.2f * v.x; v.y = a.y > 0.f ? v.y : 0.2f * v.y;
-        v.z = a.z > 0.f ? v.z : 0.2f * v.z; v.w = a.w > 0.f ? v.w : 0.2f * v.w;
+        v.x = epi_act_grad(v.x, a.x, p.flags); v.y = epi_act_grad(v.y, a.y, p.flags);
+        v.z = epi_act_grad(v.z, a.z, p.flags); v.w = epi_act_grad(v.w, a.w, p.flags);
       }
     }
     *reinterpret_cast<float4 *>(o) = v;
@@ -336,11 +356,13 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     p.kseg = p.taps_per_seg * d->c;
     pl.va = d->k % 4 == 0;
     pl.vb = nhwc_in && d->c % 4 == 0;
-    pl.cfg = p.M <= 32 ? 2 : (p.M <= 64 ? 3 : 0);
+    // M' = Cout rows, N' = taps*Cin columns: pick the tile that wastes the least MFMA work
+    pl.cfg = p.M <= 32 ? 2 : p.M <= 64 ? (p.N <= 64 ? 5 : 3) : (p.N <= 64 ? 4 : 0);
   } else {
     set_error("conv: bad op %d", op);
     return ADAPTSEG_ERR_ARG;
   }
+  if (pl.cfg == 0 && getenv("ADAPTSEG_EXP_CFG6")) pl.cfg = 6;  // A/B experiment knob
   p.fd_nseg_k = make_fastdiv(p.kseg);
   pl.flops = conv_flops(d);
   // FAST path eligibility (alignment re-checked at launch).  Vector operands need tile-
@@ -407,13 +429,17 @@ static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s
       for (int g = 0; g < q.nseg; ++g) vec = vec && aligned16(q.dw[g]);
     } else {
       vec = vec && aligned16(q.out) && (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res)) &&
-            (!(q.flags & ADAPTSEG_EPI_LEAKY_GRAD) || aligned16(q.aux));
+            (!(q.flags & kEpiActGrad) || aligned16(q.aux));
       if (mode == MODE_FWD)
         for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
     }
     if (vec) {
-      int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256), 8192);
-      splitk_reduce4_kernel<<<blocks, 256, 0, s>>>(q, slab, mode, make_fastdiv((uint32_t)q.N / 4));
+      const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
+      const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
+      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
+      if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
+      else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
+      else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
     } else {
       int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
       splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
@@ -470,7 +496,8 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
   AS_CHECK_ARG(x && w && y, "conv fwd: null pointer");
-  AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY_GRAD)), "conv fwd: LEAKY_GRAD not valid");
+  AS_CHECK_ARG(!(flags & kEpiActGrad), "conv fwd: *_GRAD flags not valid");
+  AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv fwd: residual flag without res");
   ConvParams &p = pl.p;
   p.x = x;
@@ -495,9 +522,10 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
   AS_CHECK_ARG(dy && w && dx, "conv bwd_data: null pointer");
-  AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_LEAKY), "conv bwd_data: LEAKY not valid");
+  AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY | ADAPTSEG_EPI_RELU)), "conv bwd_data: LEAKY/RELU not valid");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv bwd_data: residual flag without res");
-  AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_LEAKY_GRAD) || aux, "conv bwd_data: LEAKY_GRAD without aux");
+  AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
+  AS_CHECK_ARG((flags & kEpiActGrad) != kEpiActGrad, "conv bwd_data: LEAKY_GRAD and RELU_GRAD");
   ConvParams &p = pl.p;
   p.dy = dy;
   for (int s = 0; s < d->nseg; ++s) {

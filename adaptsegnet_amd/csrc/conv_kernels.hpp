@@ -446,18 +446,28 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
       if (more) load_tile(kt + 1);
       const float *As = lds + cur * STAGE + wm * WTM + l32;
       const float *Bs = lds + cur * STAGE + BK * SA + wn * WTN + l32;
+      // LDS operands are read one k-pair ahead of the MFMAs that consume them, so the
+      // ds_read latency hides behind the previous pair's MFMAs instead of stalling issue.
+      float a[2][TM], b[2][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[0][i] = As[hh * SA + i * 32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[0][j] = Bs[hh * SB + j * 32];
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
-        float a[TM], b[TN];
+        const int cb = (kk >> 1) & 1;
+        if (kk + 2 < BK) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[(kk + hh) * SA + i * 32];
+          for (int i = 0; i < TM; ++i) a[cb ^ 1][i] = As[(kk + 2 + hh) * SA + i * 32];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[(kk + hh) * SB + j * 32];
+          for (int j = 0; j < TN; ++j) b[cb ^ 1][j] = Bs[(kk + 2 + hh) * SB + j * 32];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this pair's MFMAs
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
       }
       if (more) store_tile(cur ^ 1);
       __syncthreads();
@@ -527,8 +537,8 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
           float v = acc[i][j][r] + bsum;
           if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
           if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
-          if (flags & ADAPTSEG_EPI_LEAKY) v = v > 0.f ? v : 0.2f * v;
-          if (flags & ADAPTSEG_EPI_LEAKY_GRAD) v = p.aux[idx] > 0.f ? v : 0.2f * v;
+          v = epi_act(v, flags);
+          if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           p.out[idx] = v;
         }
     }
@@ -971,18 +981,28 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
       if (more) load_tile(kt + 1);
       const float *As = lds + cur * STAGE + wm * WTM + l32;
       const float *Bs = lds + cur * STAGE + BK * SA + wn * WTN + l32;
+      // LDS operands are read one k-pair ahead of the MFMAs that consume them, so the
+      // ds_read latency hides behind the previous pair's MFMAs instead of stalling issue.
+      float a[2][TM], b[2][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[0][i] = As[hh * SA + i * 32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[0][j] = Bs[hh * SB + j * 32];
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
-        float a[TM], b[TN];
+        const int cb = (kk >> 1) & 1;
+        if (kk + 2 < BK) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[(kk + hh) * SA + i * 32];
+          for (int i = 0; i < TM; ++i) a[cb ^ 1][i] = As[(kk + 2 + hh) * SA + i * 32];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[(kk + hh) * SB + j * 32];
+          for (int j = 0; j < TN; ++j) b[cb ^ 1][j] = Bs[(kk + 2 + hh) * SB + j * 32];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this pair's MFMAs
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
       }
       if (more) store_tile(cur ^ 1);
       __syncthreads();
@@ -1060,8 +1080,8 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
           float v = acc[i][j][r] + bsum;
           if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
           if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
-          if (flags & ADAPTSEG_EPI_LEAKY) v = v > 0.f ? v : 0.2f * v;
-          if (flags & ADAPTSEG_EPI_LEAKY_GRAD) v = p.aux[idx] > 0.f ? v : 0.2f * v;
+          v = epi_act(v, flags);
+          if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           p.out[idx] = v;
         }
     }
@@ -1071,7 +1091,7 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
 
 struct Plan {
   ConvParams p;
-  int cfg;        // 0: 128x128 (2x2), 1: 256x32 (4x1), 2: 32x256 (1x4), 3: 64x256 (1x4)
+  int cfg;        // index into kCfgBM / kCfgBN
   bool va, vb;
   bool fast;
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
@@ -1084,11 +1104,12 @@ struct Plan {
 };
 
 // tile configs: 0 = 128x128 (2x2 waves), 1 = 256x32 (4x1), 2 = 32x256 (1x4), 3 = 64x256 (1x4),
-// 4 = 256x64 (4x1).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
-static const int kCfgBM[5] = {128, 256, 32, 64, 256};
-static const int kCfgBN[5] = {128, 32, 256, 256, 64};
+// 4 = 256x64 (4x1), 5 = 64x64 (2x2, small weight gradients), 6 = 128x128 with BK 16
+// (33 KB of LDS: three blocks per CU).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
+static const int kCfgBM[7] = {128, 256, 32, 64, 256, 64, 128};
+static const int kCfgBN[7] = {128, 32, 256, 256, 64, 64, 128};
 // K step of the FAST kernel per config (LDS: 2 stages x BK x (BM+BN+pad) floats)
-static int fast_bk(int cfg) { return cfg == 4 ? 16 : 32; }
+static int fast_bk(int cfg) { return (cfg == 4 || cfg == 6) ? 16 : 32; }
 
 
 hipError_t launch_fwd(const Plan &pl, hipStream_t s);

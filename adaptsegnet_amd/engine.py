@@ -16,6 +16,7 @@ Reference semantics followed (file:line in /root/reference):
   Classifier_Module.forward (ASPP sum)   model/deeplab_multi.py:117-121
   ResNetMulti.forward                    model/deeplab_multi.py:174-194
   FCDiscriminator.forward                model/discriminator.py:21-34
+  DeeplabVGG.forward (+ 2-branch ASPP)   model/deeplab_vgg.py:17-21, 46-49
 """
 from __future__ import annotations
 
@@ -38,11 +39,16 @@ def bn_forward(bn, x, res, relu, training):
     return y, (bn.running_mean, None, False)
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False):
+    """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
+    mode instead of reading the saved output y (one activation read less per pass)."""
     mean, invstd, train = st
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
-    return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train)
+    elif mask_from_x and relu:
+        y = None
+    return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train,
+                    bias=bn.bias)
 
 
 # ---------------------------------------------------------------------------------------
@@ -90,12 +96,12 @@ def block_backward(blk, rec, gout, need_w):
     if need_w and blk.conv3.weight.grad is not None:
         K.conv_wgrad(g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
     del dc3
-    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2)
+    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True)
     dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
     if need_w and blk.conv2.weight.grad is not None:
         K.conv_wgrad(g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
     del dy2
-    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1)
+    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True)
     if need_w and blk.conv1.weight.grad is not None:
         K.conv_wgrad(g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
     if blk.downsample is not None:
@@ -233,7 +239,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
         ctx.stem = None
         dy0 = K.maxpool_bwd(g, am, h0, w0)
         del g
-        bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0)
+        bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0, mask_from_x=True)
         gs = model.conv1.geom()
         if need_w and model.conv1.weight.grad is not None:
             K.conv_wgrad(gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
@@ -325,3 +331,107 @@ def discriminator_forward(model, x):
     need_w = any(p.requires_grad for p in model._arena.params)
     grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
     return _FCDiscriminatorFn.apply(model._anchors[need_w], x, model, grad)
+
+
+# ---------------------------------------------------------------------------------------
+# DeeplabVGG (model/deeplab_vgg.py:24-51): conv+bias+ReLU stack with 2x2 pools, then the
+# two-branch ASPP sum.  ReLU is fused into each conv epilogue; its derivative is applied in
+# the next data-gradient epilogue (EPI_RELU_GRAD on the saved post-ReLU activation, which is
+# also the pooled value a 2x2 max-pool routes back to).
+# ---------------------------------------------------------------------------------------
+
+
+class _DeeplabVGGFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, model, save):
+        ctx.set_materialize_grads(False)
+        n, c, h, w = x.shape
+        prog = model.conv_program()
+        acts = []  # (conv input, h, w, strides, pool record or None)
+        cur, ch, cw, cs = x, h, w, _input_strides(x)
+        for conv, pool in prog:
+            g = conv.geom()
+            out = K.conv_fwd(g, cur, n, ch, cw, [conv.weight], [conv.bias], strides=cs,
+                             flags=K.EPI_RELU)
+            rec = [cur, ch, cw, cs, None]
+            ch, cw = g.out_hw(ch, cw)
+            if pool:
+                ph, pw = ch, cw
+                cur, am = K.maxpool_fwd(out, k=2, s=2, p=0)
+                rec[4] = (am, ph, pw)
+                ch, cw = cur.shape[1], cur.shape[2]
+                del out
+            else:
+                cur = out
+            cs = K.nhwc_strides(n, ch, cw, cur.shape[3])
+            acts.append(rec)
+        branches = model.classifier_branches()
+        gc = _branches_geom(branches)
+        y = K.conv_fwd(gc, cur, n, ch, cw, [b.weight for b in branches], [b.bias for b in branches])
+        if save:
+            ctx.model, ctx.acts, ctx.n = model, acts, n
+            ctx.cls_in = (cur, ch, cw)
+            ctx.need_w = anchor.requires_grad
+        return K.as_nchw(y)
+
+    @staticmethod
+    def backward(ctx, gout):
+        if gout is None:
+            return None, None, None, None
+        model, acts, n = ctx.model, ctx.acts, ctx.n
+        need_w = ctx.need_w
+        if need_w:
+            model._arena.claim(model._pidx["used"])
+        g = K.nhwc_view(gout)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        branches = model.classifier_branches()
+        gc = _branches_geom(branches)
+        a, ch, cw = ctx.cls_in
+        ctx.cls_in = None
+        if need_w and branches[0].weight.grad is not None:
+            K.conv_wgrad(gc, g, a, n, ch, cw, [b.weight.grad for b in branches],
+                         [b.bias.grad for b in branches])
+        # grad of fc7's pre-activation: dgrad * relu'(a)
+        g = K.conv_dgrad(gc, g, n, ch, cw, [b.weight for b in branches], aux=a,
+                         flags=K.EPI_RELU_GRAD)
+        del a
+        prog = model.conv_program()
+        dx = None
+        for i in reversed(range(len(prog))):
+            conv, _ = prog[i]
+            geo = conv.geom()
+            xin, ih, iw, cs, _ = acts[i]
+            if need_w and conv.weight.grad is not None:
+                K.conv_wgrad(geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
+            if i > 0:
+                # grad of the previous conv's pre-activation.  xin is its post-ReLU output,
+                # or the 2x2 max of it: relu' at the routed (argmax) position = [max > 0].
+                g = K.conv_dgrad(geo, g, n, ih, iw, [conv.weight], aux=xin, flags=K.EPI_RELU_GRAD)
+                prev_pool = acts[i - 1][4]
+                if prev_pool is not None:
+                    am, ph, pw = prev_pool
+                    g = K.maxpool_bwd(g, am, ph, pw, k=2, s=2, p=0)
+            elif ctx.needs_input_grad[1]:
+                dx = K.as_nchw(K.conv_dgrad(geo, g, n, ih, iw, [conv.weight]))
+            acts[i] = None
+        return None, dx, None, None
+
+
+def _branches_geom(branches):
+    c0 = branches[0]
+    return K.ConvGeom(c0.in_channels, c0.out_channels, 3, 3, 1,
+                      tuple(b.padding for b in branches), tuple(b.dilation for b in branches))
+
+
+def deeplab_vgg_forward(model, x):
+    """DeeplabVGG.forward(x) (model/deeplab_vgg.py:46-49) on the HIP engine."""
+    if not x.is_cuda:
+        raise RuntimeError("adaptsegnet_amd DeeplabVGG runs on the HIP engine only; "
+                           f"got input on {x.device}")
+    if x.dtype != torch.float32:
+        raise RuntimeError(f"expected float32 input, got {x.dtype}")
+    model._ensure_arena(x.device)
+    need_w = any(p.requires_grad for p in model._arena.params)
+    grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
+    return _DeeplabVGGFn.apply(model._anchors[need_w], x, model, grad)

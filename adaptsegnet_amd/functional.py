@@ -7,6 +7,8 @@ Tensors at this boundary are NCHW-shaped, as in the reference; internally they a
   nn.CrossEntropyLoss(ignore_index=255)         train_gta2cityscapes_multi.py:359,546,599-600
   CrossEntropy2d                                utils/loss.py:14-36
   BCEWithLogitsLoss / MSELoss vs const target   train_gta2cityscapes_multi.py:542-545,620-624
+  nn.Upsample(bilinear, align_corners=True)     train_gta2cityscapes_multi.py:237-238 (interp),
+                                                model/deeplab_multi.py:188-189
 """
 from __future__ import annotations
 
@@ -109,3 +111,22 @@ def bce_with_logits_const(d_out, target: float):
 
 def mse_const(d_out, target: float):
     return adv_loss(d_out, target, MSE)
+
+
+class _Interp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        xv = K.nhwc_view(x)
+        ctx.hw = (xv.shape[1], xv.shape[2])
+        return K.as_nchw(K.upsample_fwd(xv, oh, ow))
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.hw
+        return K.as_nchw(K.upsample_bwd(K.nhwc_view(g), h, w)), None, None
+
+
+def interp(x: torch.Tensor, size) -> torch.Tensor:
+    """``nn.Upsample(size=(H, W), mode='bilinear', align_corners=True)(x)`` for [N, C, h, w]."""
+    _check(x, "interp")
+    return _Interp.apply(x, int(size[0]), int(size[1]))

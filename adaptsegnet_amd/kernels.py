@@ -15,13 +15,13 @@ import torch
 
 from . import _lib
 from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
-                   EPI_LEAKY_GRAD, EPI_RESIDUAL, ConvDesc, check)
+                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, ConvDesc, check)
 
 __all__ = [
     "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_fwd_train", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
-    "axpy", "add_i64", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RESIDUAL",
+    "axpy", "add_i64", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
 ]
 
 
@@ -133,7 +133,7 @@ def _ptrs(ts):
 
 def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, biases=None,
              strides=None, out=None, res=None, flags: int = 0) -> torch.Tensor:
-    """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (leaky if EPI_LEAKY)."""
+    """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (EPI_LEAKY / EPI_RELU)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
     d, ws, oh, ow = _desc(g, n, h, w, tuple(strides))
     if out is None:
@@ -149,13 +149,13 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, bias
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
                res=None, aux=None, flags: int = 0) -> torch.Tensor:
-    """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux))."""
+    """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD)."""
     d, ws, oh, ow = _desc(g, n, h, w, nhwc_strides(n, h, w, g.cin))
     if out is None:
         out = torch.empty((n, h, w, g.cin), device=dy.device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
-    if aux is not None:
+    if aux is not None and not flags & EPI_RELU_GRAD:
         flags |= EPI_LEAKY_GRAD
     wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
     check(_lib.lib().adaptseg_conv2d_bwd_data(
@@ -214,15 +214,16 @@ def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu
     return y
 
 
-def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True):
-    """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy."""
+def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None):
+    """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy.
+    y=None with relu (train mode): the mask is recomputed from x, weight and bias."""
     rows, c = dy.numel() // dy.shape[-1], dy.shape[-1]
     if dx is None:
         dx = torch.empty_like(dy)
     wp, wsz = _ws_args(_bn_ws(rows, c) if train else 0, dy.device)
     check(_lib.lib().adaptseg_bn_bwd(
-        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(mean), _p(invstd), _p(dx), _p(dres),
-        1 if relu else 0, 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx),
+        _p(dres), 1 if relu else 0, 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
     return dx
 
 

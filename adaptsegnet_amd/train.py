@@ -73,6 +73,8 @@ class AdaptSegTrainer:
         self.model, self.D1, self.D2, self.cfg = model, model_D1, model_D2, cfg
         if cfg.level == "multi-level" and model_D1 is None:
             raise ValueError("multi-level needs model_D1")
+        if cfg.level == "multi-level" and getattr(model, "single_output", False):
+            raise ValueError("multi-level needs a two-head generator (DeeplabMulti)")
         self.opt = SGD(model, cfg.learning_rate, cfg.momentum, cfg.weight_decay)
         self.opt_D1 = Adam(model_D1, cfg.learning_rate_D, betas=(0.9, 0.99)) if model_D1 is not None else None
         self.opt_D2 = Adam(model_D2, cfg.learning_rate_D, betas=(0.9, 0.99))
@@ -148,16 +150,23 @@ class AdaptSegTrainer:
         self.opt_D2.step(grad_scale=gs)
         return L
 
+    def _pred_single(self, images, size):
+        """The single-level prediction at ``size`` = (W, H): DeeplabMulti's second head, or a
+        single-map model (DeeplabVGG, config c4) followed by the caller-side ``interp``."""
+        if getattr(self.model, "single_output", False):
+            return F.interp(self.model(images), (size[1], size[0]))
+        return self.model(images, size)[1]
+
     def _sub_single(self, images, labels, images_t, inv, tsize, L):
         """train_gta2cityscapes_multi.py:385-461."""
         c, D2 = self.cfg, self.D2
         self._set_requires_grad(D2, False)
-        _, pred2 = self.model(images, c.input_size)
+        pred2 = self._pred_single(images, c.input_size)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         self._backward([loss_seg2], [inv])
         L.add("loss_seg2", loss_seg2, inv)
 
-        _, pred_target2 = self.model(images_t, tsize)
+        pred_target2 = self._pred_single(images_t, tsize)
         d_out2 = D2(F.softmax2d(pred_target2))
         loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
         self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: AdaptSegNet adversarial-train images/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
 One "step" = one full adversarial iteration of train_gta2cityscapes_multi.py on the HIP
@@ -36,9 +36,10 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X: 256 CU x 2.4 GHz x 256 FLOP/clk/CU (MI
 METRIC = "adversarial-train images/sec at 1024×512, DeeplabMulti+D, 1/2/4/8 MI355X"
 
 CONFIGS = {
-    # name: (level, gan, batch/GPU, source (W,H), target (W,H))
-    "c2": ("single-level", "Vanilla", 4, (1024, 512), (1024, 512)),
-    "c3": ("multi-level", "Vanilla", 2, (1280, 720), (1024, 512)),
+    # name: (level, gan, batch/GPU, source (W,H), target (W,H), generator)
+    "c2": ("single-level", "Vanilla", 4, (1024, 512), (1024, 512), "DeeplabMulti"),
+    "c3": ("multi-level", "Vanilla", 2, (1280, 720), (1024, 512), "DeeplabMulti"),
+    "c4": ("single-level", "Vanilla", 8, (1024, 512), (1024, 512), "DeeplabVGG"),
 }
 
 
@@ -52,7 +53,26 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize):
         kid, _ = K.conv_kernel_id(geom, n, h, w, op, strides)
         inv[kid] = inv.get(kid, 0.0) + count * geom.flops(n, h, w)
 
+    def vgg_pass(wh):
+        w, h = wh
+        st = (3 * h * w, h * w, w, 1)
+        for i, (conv, pool) in enumerate(model.conv_program()):
+            g = conv.geom()
+            add(g, batch, h, w, 0, st)
+            if i > 0:
+                add(g, batch, h, w, 1)
+            add(g, batch, h, w, 2, st)
+            h, w = g.out_hw(h, w)
+            if pool:
+                h, w = h // 2, w // 2
+            st = None
+        gc = engine._branches_geom(model.classifier_branches())
+        for op in (0, 1, 2):
+            add(gc, batch, h, w, op)
+
     def g_pass(wh, backward, heads_bwd):
+        if getattr(model, "single_output", False):
+            return vgg_pass(wh)
         w, h = wh
         gs = model.conv1.geom()
         add(gs, batch, h, w, 0, (3 * h * w, h * w, w, 1))
@@ -132,7 +152,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="c2 (default, BASELINE metric at N=1), c3 multi-level, c4 DeeplabVGG")
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -147,14 +168,14 @@ def main():
     dev = torch.device("cuda", local)
 
     from adaptsegnet_amd import kernels as K
-    from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
+    from adaptsegnet_amd.model import DeeplabMulti, DeeplabVGG, FCDiscriminator
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
 
-    level, gan, batch, src_wh, tgt_wh = CONFIGS[args.config]
+    level, gan, batch, src_wh, tgt_wh, gen = CONFIGS[args.config]
     if args.batch:
         batch = args.batch
     torch.manual_seed(1338 + rank)
-    model = DeeplabMulti(num_classes=19).to(dev)
+    model = (DeeplabMulti if gen == "DeeplabMulti" else DeeplabVGG)(num_classes=19).to(dev)
     D1 = FCDiscriminator(num_classes=19).to(dev) if level == "multi-level" else None
     D2 = FCDiscriminator(num_classes=19).to(dev)
     if world > 1:  # identical initial weights on every rank (DDP's initial broadcast)
@@ -214,7 +235,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (U[-122.7,151] BGR-mean-subtracted pixels, uniform labels, 10% ignore=255)",
-        "config": {"workload": f"{args.config}: {level} {gan}, batch/GPU {batch}, source "
+        "config": {"workload": f"{args.config}: {gen} {level} {gan}, batch/GPU {batch}, source "
                                f"{src_wh[0]}x{src_wh[1]}, target {tgt_wh[0]}x{tgt_wh[1]}",
                    "global_batch": batch * world, "parallelism": f"dp{world}",
                    "step_conv_tflop": step_flops / 1e12,

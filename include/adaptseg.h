@@ -64,7 +64,9 @@ enum adaptseg_conv_flags {
   ADAPTSEG_EPI_LEAKY = 1,      /* fwd: y = leaky_relu(y, 0.2)  (discriminator.py:21-29)    */
   ADAPTSEG_EPI_ACCUMULATE = 2, /* out += result instead of out = result                    */
   ADAPTSEG_EPI_LEAKY_GRAD = 4, /* bwd_data: dx *= (aux > 0 ? 1 : 0.2)                      */
-  ADAPTSEG_EPI_RESIDUAL = 8    /* out = result + res (same NHWC shape as out)              */
+  ADAPTSEG_EPI_RESIDUAL = 8,   /* out = result + res (same NHWC shape as out)              */
+  ADAPTSEG_EPI_RELU = 16,      /* fwd: y = relu(y)  (deeplab_vgg.py:34-43 conv + ReLU)     */
+  ADAPTSEG_EPI_RELU_GRAD = 32  /* bwd_data: dx *= (aux > 0 ? 1 : 0)                        */
 };
 
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
@@ -76,7 +78,7 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
                         const float *const *bias, const float *res, float *y, int flags,
                         void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
-/* dx[n,h,w,c] = conv_transpose(dy, w)  (NHWC, contiguous).  aux: LEAKY_GRAD source. */
+/* dx[n,h,w,c] = conv_transpose(dy, w)  (NHWC, contiguous).  aux: LEAKY_/RELU_GRAD source. */
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream);
@@ -110,11 +112,13 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
 
 /* Backward of bn_fwd_train.  g = dy * (relu ? (y > 0) : 1).
    dx = weight*invstd*(g - mean(g) - xhat*mean(g*xhat)); dres = g if dres != NULL.
+   y == NULL with relu (train mode, BN without residual): the mask is recomputed from x as
+   (x-mean)*invstd*weight + bias > 0 — one tensor read less in both passes.
    If train == 0 the eval-mode backward dx = g*weight*invstd is computed. */
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x,
-                    const float *weight, const float *save_mean, const float *save_invstd,
-                    float *dx, float *dres, int relu, int train, void *ws, size_t ws_bytes,
-                    adaptseg_stream_t stream);
+                    const float *weight, const float *bias, const float *save_mean,
+                    const float *save_invstd, float *dx, float *dres, int relu, int train,
+                    void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* MaxPool2d (model/deeplab_multi.py:135: kernel 3, stride 2, pad 1, floor mode), NHWC.  */

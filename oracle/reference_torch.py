@@ -12,6 +12,7 @@ Restated reference code (file:line in /root/reference):
   ResNetMulti.forward (+ bilinear upsample)    model/deeplab_multi.py:174-194
   get_1x_lr_params_NOscale multiplicity        model/deeplab_multi.py:196-222
   FCDiscriminator.forward                      model/discriminator.py:21-34
+  DeeplabVGG layout / forward (c4)             model/deeplab_vgg.py:7-21, 24-49
   CrossEntropy2d.forward                       utils/loss.py:14-36
   step bodies, losses, optimisers, poly LR     train_gta2cityscapes_multi.py:162-177,
                                                355-359, 379-464, 532-546, 570-683
@@ -72,6 +73,39 @@ def g_specs(num_classes=19, layout=RESNET101):
     return out
 
 
+# DeeplabVGG (deeplab_vgg.py:24-43): VGG16 cfg "D" convs with pool4/pool5 removed, conv5
+# dilated 2, fc6/fc7 3x3 d4.  (features index, cin, cout, dilation, 2x2 max-pool after ReLU)
+VGG_CONVS = ((0, 3, 64, 1, False), (2, 64, 64, 1, True), (5, 64, 128, 1, False),
+             (7, 128, 128, 1, True), (10, 128, 256, 1, False), (12, 256, 256, 1, False),
+             (14, 256, 256, 1, True), (17, 256, 512, 1, False), (19, 512, 512, 1, False),
+             (21, 512, 512, 1, False), (23, 512, 512, 2, False), (25, 512, 512, 2, False),
+             (27, 512, 512, 2, False), (29, 512, 1024, 4, False), (31, 1024, 1024, 4, False))
+
+
+def vgg_specs(num_classes=19):
+    """[(key, shape, kind)] of DeeplabVGG in registration order."""
+    out = []
+    for idx, ci, co, _d, _p in VGG_CONVS:
+        out.append((f"features.{idx}.weight", (co, ci, 3, 3), "vconv"))
+        out.append((f"features.{idx}.bias", (co,), "vbias"))
+    for r in range(4):
+        out.append((f"classifier.conv2d_list.{r}.weight", (num_classes, 1024, 3, 3), "conv"))
+        out.append((f"classifier.conv2d_list.{r}.bias", (num_classes,), "bias"))
+    return out
+
+
+def vgg_forward(P, x):
+    """DeeplabVGG.forward: features (conv+ReLU, 2x2 pools), then Classifier_Module, whose
+    ``return`` inside the loop (deeplab_vgg.py:19-21) sums only branches 0 (d6) and 1 (d12)."""
+    for idx, _ci, _co, d, pool in VGG_CONVS:
+        x = F.relu(F.conv2d(x, P[f"features.{idx}.weight"], P[f"features.{idx}.bias"], 1, d, d))
+        if pool:
+            x = F.max_pool2d(x, 2, 2)
+    out = F.conv2d(x, P["classifier.conv2d_list.0.weight"], P["classifier.conv2d_list.0.bias"], 1, 6, 6)
+    return out + F.conv2d(x, P["classifier.conv2d_list.1.weight"], P["classifier.conv2d_list.1.bias"],
+                          1, 12, 12)
+
+
 def d_specs(num_classes=19, ndf=64):
     chans = (num_classes, ndf, ndf * 2, ndf * 4, ndf * 8, 1)
     names = ("conv1", "conv2", "conv3", "conv4", "classifier")
@@ -91,6 +125,10 @@ def det_state(specs, seed, conv_std=0.01, bn_random=True):
             v = rng.normal(0.0, conv_std, shape)
         elif kind == "bias":
             fan_in = None
+            v = rng.uniform(-0.05, 0.05, shape)
+        elif kind == "vconv":  # torchvision VGG: kaiming_normal_(fan_out, relu)
+            v = rng.normal(0.0, np.sqrt(2.0 / (shape[0] * shape[2] * shape[3])), shape)
+        elif kind == "vbias":
             v = rng.uniform(-0.05, 0.05, shape)
         elif kind in ("dconv", "dbias"):
             wshape = [s for k2, s, kd in specs if k2 == key.rsplit(".", 1)[0] + ".weight"][0]

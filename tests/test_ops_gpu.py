@@ -55,6 +55,10 @@ CONV_CASES = [
     (1, 64, 9, 11, 32, 4, 2, (1,), (1,), True),           # stride-2 4x4, odd sizes
     (3, 64, 20, 24, 64, 3, 1, (1,), (1,), False),         # N = 64 tile (256x64)
     (2, 96, 12, 10, 96, 1, 2, (0,), (1,), False),         # 1x1 stride 2, empty parity classes
+    (2, 64, 40, 48, 64, 1, 1, (0,), (1,), True),          # wgrad 64x64 tile, bias Cout 64
+    (2, 64, 30, 34, 256, 1, 1, (0,), (1,), False),        # wgrad 256x64 tile (M'=256, N'=64)
+    (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),          # wgrad ~192 K-splits (16-group reduce)
+    (1, 32, 8, 10, 320, 1, 1, (0,), (1,), True),          # bias grad with Cout > 256
 ]
 
 
