@@ -134,6 +134,12 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
 }
 
 static bool aligned16(const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+template <typename T>
+static bool segs_aligned(T *const *w, int nseg) {
+  for (int s = 0; s < nseg; ++s)
+    if (!aligned16(w[s])) return false;
+  return true;
+}
 
 // Bias gradient: db[seg][co] (+)= sum_m dY[m][co].  Each block sums a contiguous run of rows
 // of the NHWC gradient with flat coalesced reads: for cout <= 256 thread t owns column t % cout
@@ -290,13 +296,13 @@ static void fill_common(ConvParams &p, const adaptseg_conv_desc *d) {
   p.fd_hw = make_fastdiv(d->h);
 }
 
-static double conv_flops(const adaptseg_conv_desc *d) {
+double conv_flops(const adaptseg_conv_desc *d) {
   return 2.0 * d->n * d->oh * d->ow * (double)d->k * d->c * d->kh * d->kw * d->nseg;
 }
 
 // Grid decomposition: tiles, then split K until the grid has ~2 blocks per CU while keeping
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
-static void set_splits(Plan &pl) {
+void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
   const int bm = kCfgBM[pl.cfg], bn = kCfgBN[pl.cfg];
   pl.bk = pl.fast ? fast_bk(pl.cfg) : BK;
@@ -326,7 +332,7 @@ static void set_splits(Plan &pl) {
   pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
 }
 
-static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
+int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   int st = validate(d);
   if (st) return st;
   ConvParams &p = pl.p;
@@ -362,7 +368,7 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     set_error("conv: bad op %d", op);
     return ADAPTSEG_ERR_ARG;
   }
-  if (pl.cfg == 0 && getenv("ADAPTSEG_EXP_CFG6")) pl.cfg = 6;  // A/B experiment knob
+  if (pl.cfg == 0 && getenv("ADAPTSEG_EXP_CFG")) pl.cfg = atoi(getenv("ADAPTSEG_EXP_CFG"));  // A/B knob
   p.fd_nseg_k = make_fastdiv(p.kseg);
   pl.flops = conv_flops(d);
   // FAST path eligibility (alignment re-checked at launch).  Vector operands need tile-
@@ -392,13 +398,13 @@ static int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   return ADAPTSEG_OK;
 }
 
-static int kernel_id(const Plan &pl, int mode) {
+int kernel_id(const Plan &pl, int mode) {
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)
   if (pl.fast) return 100 * mode + 10 * pl.cfg + 4 + (pl.s2 ? 4 : 0) + (pl.ae ? 2 : 0) + (pl.be ? 1 : 0);
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
 }
 
-static int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
+int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
   if (pl.p.splits > 1) {
     if (!ws || ws_bytes < pl.slab_bytes) {
@@ -468,6 +474,7 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
     set_splits(g);
     b = std::max(b, g.slab_bytes);
   }
+  if (tapgemm_eligible(d)) b = std::max(b, tapgemm_workspace(d, op));
   if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
     // bias-gradient partials
     int per, splits;
@@ -484,6 +491,7 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
   int st = make_plan(d, op, pl);
   if (st) return st;
   // alignment-dependent downgrades are not known here; report the aligned choice
+  if (tapgemm_eligible(d)) return tapgemm_kernel_id(d, op, kernel_id, splits);
   *kernel_id = ::adaptseg::kernel_id(pl, op);
   *splits = pl.p.splits;
   return ADAPTSEG_OK;
@@ -499,6 +507,9 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
   AS_CHECK_ARG(!(flags & kEpiActGrad), "conv fwd: *_GRAD flags not valid");
   AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv fwd: residual flag without res");
+  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd: null weight %d", s);
+  if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg))
+    return tapgemm_fwd(d, x, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
   ConvParams &p = pl.p;
   p.x = x;
   for (int s = 0; s < d->nseg; ++s) {
@@ -526,6 +537,10 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv bwd_data: residual flag without res");
   AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
   AS_CHECK_ARG((flags & kEpiActGrad) != kEpiActGrad, "conv bwd_data: LEAKY_GRAD and RELU_GRAD");
+  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data: null weight %d", s);
+  if (tapgemm_eligible(d) && aligned16(dy) && aligned16(dx) && segs_aligned(w, d->nseg) &&
+      (!res || aligned16(res)) && (!aux || aligned16(aux)))
+    return tapgemm_bwd_data(d, dy, w, res, aux, dx, flags, ws, ws_bytes, as_stream(stream));
   ConvParams &p = pl.p;
   p.dy = dy;
   for (int s = 0; s < d->nseg; ++s) {
@@ -549,19 +564,21 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
   int st = make_plan(d, ADAPTSEG_CONV_BWD_WEIGHT, pl);
   if (st) return st;
   AS_CHECK_ARG(dy && x && dw, "conv bwd_weight: null pointer");
-  ConvParams &p = pl.p;
-  p.dy = dy;
-  p.x = x;
-  for (int s = 0; s < d->nseg; ++s) {
-    AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
-    p.dw[s] = dw[s];
-  }
-  if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
-  if (reinterpret_cast<uintptr_t>(x) & 15) pl.vb = pl.fast = false;
-  set_splits(pl);
-  p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
+  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
   hipStream_t s = as_stream(stream);
-  st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
+  if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(dw, d->nseg)) {
+    st = tapgemm_bwd_weight(d, dy, x, dw, flags, ws, ws_bytes, s);
+  } else {
+    ConvParams &p = pl.p;
+    p.dy = dy;
+    p.x = x;
+    for (int g = 0; g < d->nseg; ++g) p.dw[g] = dw[g];
+    if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
+    if (reinterpret_cast<uintptr_t>(x) & 15) pl.vb = pl.fast = false;
+    set_splits(pl);
+    p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
+    st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
+  }
   if (st) return st;
   if (db) {
     bool any = false;

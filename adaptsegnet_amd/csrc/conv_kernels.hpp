@@ -282,10 +282,11 @@ __device__ __forceinline__ float wgrad_b_elem(const ConvParams &p, const PixInfo
 // Kernel
 // ------------------------------------------------------------------------------------
 template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool VA, bool VB>
-__global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_kernel(const ConvParams p) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
   static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
   constexpr bool A_KC = MODE != MODE_WGRAD;  // A stored k-contiguous in global memory
   constexpr bool B_KC = MODE == MODE_FWD;
@@ -294,7 +295,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
   constexpr int STAGE = BK * SA + BK * SB;
   // float4 staging slots per thread
   constexpr int QA = BM * BK / 4, QB = BN * BK / 4;
-  constexpr int NQA = (QA + 255) / 256, NQB = (QB + 255) / 256;
+  constexpr int NQA = (QA + NT - 1) / NT, NQB = (QB + NT - 1) / NT;
 
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   __shared__ short s_tdy[kMaxTaps], s_tdx[kMaxTaps];
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
   bool aact[NQA];
 #pragma unroll
   for (int i = 0; i < NQA; ++i) {
-    int q = tid + 256 * i;
+    int q = tid + NT * i;
     aact[i] = q < QA;
     if constexpr (A_KC) {
       acol[i] = q >> 2;          // row m within tile
@@ -340,7 +341,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
   ColInfo bci[NQB][VB ? 1 : 4];
 #pragma unroll
   for (int i = 0; i < NQB; ++i) {
-    int q = tid + 256 * i;
+    int q = tid + NT * i;
     bact[i] = q < QB;
     if constexpr (B_KC) {
       bcol[i] = q >> 2;
@@ -563,6 +564,16 @@ __global__ void __launch_bounds__(256) igemm_kernel(const ConvParams p) {
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// XCD-aware tile order.  The dispatcher places workgroup b on XCD b % 8 (8 XCDs, each with
+// its own 4 MB L2); renumber so every XCD walks a CONTIGUOUS run of tiles (row-tile major):
+// the column tiles of one row-tile and the tap halos of neighbouring row-tiles then hit the
+// same L2 instead of being fetched once per XCD.
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+  const int x = b & 7, j = b >> 3;
+  const int q = nb >> 3, r = nb & 7;
+  return x * q + min(x, r) + j;
+}
+
 __device__ __forceinline__ float4 mask4(int m, float4 v) {
   return make_float4((m & 1) ? v.x : 0.f, (m & 2) ? v.y : 0.f, (m & 4) ? v.z : 0.f, (m & 8) ? v.w : 0.f);
 }
@@ -579,10 +590,11 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, int tap, int &seg,
 }
 
 template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool S2, bool AE, bool BE>
-__global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(const ConvParams p) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;  // threads per block (4 or 8 waves)
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
   static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
   constexpr bool A_KC = MODE != MODE_WGRAD;
   constexpr bool B_KC = MODE == MODE_FWD;
@@ -590,15 +602,16 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
   constexpr int SB = B_KC ? BN + 2 : BN + 4;
   constexpr int STAGE = BK * SA + BK * SB;
   constexpr int QA = BM * BK / 4, QB = BN * BK / 4;
-  constexpr int NQA = QA / 256, NQB = QB / 256;
+  constexpr int NQA = QA / NT, NQB = QB / NT;
   constexpr int KQ = BK / 4;  // float4 per k-contiguous row
-  static_assert(QA % 256 == 0 && QB % 256 == 0, "every thread stages whole float4 slots");
+  static_assert(QA % NT == 0 && QB % NT == 0, "every thread stages whole float4 slots");
 
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
 
   const int tid = threadIdx.x;
   const int ntn = (p.N + BN - 1) / BN;
-  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
   const int bm = tm * BM, bn = tn * BN;
   const int split = blockIdx.y;
 
@@ -629,7 +642,7 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
   bool a_ok[NQA];
 #pragma unroll
   for (int i = 0; i < NQA; ++i) {
-    const int q = tid + 256 * i;
+    const int q = tid + NT * i;
     if constexpr (A_KC) {
       const int row = q / KQ;
       a_col[i] = row;
@@ -674,7 +687,7 @@ __global__ void __launch_bounds__(256) igemm_fast_kernel(const ConvParams p) {
   bool b_ok[NQB];
 #pragma unroll
   for (int i = 0; i < NQB; ++i) {
-    const int q = tid + 256 * i;
+    const int q = tid + NT * i;
     if constexpr (B_KC) {  // FWD B: rows n, k contiguous
       const int row = q / KQ;
       b_col[i] = row;
@@ -1105,12 +1118,31 @@ struct Plan {
 
 // tile configs: 0 = 128x128 (2x2 waves), 1 = 256x32 (4x1), 2 = 32x256 (1x4), 3 = 64x256 (1x4),
 // 4 = 256x64 (4x1), 5 = 64x64 (2x2, small weight gradients), 6 = 128x128 with BK 16
-// (33 KB of LDS: three blocks per CU).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
-static const int kCfgBM[7] = {128, 256, 32, 64, 256, 64, 128};
-static const int kCfgBN[7] = {128, 32, 256, 256, 64, 64, 128};
+// (33 KB of LDS: three blocks per CU), 7 = 256x128 with 8 waves (4x2, 512 threads).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
+static const int kCfgBM[8] = {128, 256, 32, 64, 256, 64, 128, 256};
+static const int kCfgBN[8] = {128, 32, 256, 256, 64, 64, 128, 128};
+static const int kCfgThreads[8] = {256, 256, 256, 256, 256, 256, 256, 512};
 // K step of the FAST kernel per config (LDS: 2 stages x BK x (BM+BN+pad) floats)
 static int fast_bk(int cfg) { return (cfg == 4 || cfg == 6) ? 16 : 32; }
 
+
+// Planning and execution (conv_igemm.hip), shared with the tap-GEMM path (conv_tapgemm.hip).
+double conv_flops(const adaptseg_conv_desc *d);
+void set_splits(Plan &pl);
+int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl);
+int kernel_id(const Plan &pl, int mode);
+int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s);
+
+// Tap-GEMM path for stride-1 'same' convs with Cout <= 32 (ASPP): conv_tapgemm.hip.
+bool tapgemm_eligible(const adaptseg_conv_desc *d);
+size_t tapgemm_workspace(const adaptseg_conv_desc *d, int op);
+int tapgemm_kernel_id(const adaptseg_conv_desc *d, int op, int *kid, int *splits);
+int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w, const float *const *bias,
+                const float *res, float *y, int flags, void *ws, size_t ws_bytes, hipStream_t s);
+int tapgemm_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w, const float *res,
+                     const float *aux, float *dx, int flags, void *ws, size_t ws_bytes, hipStream_t s);
+int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x, float *const *dw,
+                       int flags, void *ws, size_t ws_bytes, hipStream_t s);
 
 hipError_t launch_fwd(const Plan &pl, hipStream_t s);
 hipError_t launch_dgrad(const Plan &pl, hipStream_t s);

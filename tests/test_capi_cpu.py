@@ -32,4 +32,10 @@ def test_workspace_and_kernel_selection_on_host():
     assert kid // 100 == 2 and splits > 1     # weight grad splits K = N*OH*OW
     aspp = K.ConvGeom(2048, 19, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24))
     kid, _ = K.conv_kernel_id(aspp, 4, 64, 128, 0)
-    assert (kid // 10) % 10 == 1              # skinny-N tile (256x32) for the 19-class head
+    assert kid == 4                           # tap-GEMM: the 19-class head runs as a dense
+    #                                           1x1 GEMM with N = 36 taps x 19 (pad 704)
+    dgrad, _ = K.conv_kernel_id(aspp, 4, 64, 128, 1)
+    assert dgrad == 104                       # dX = G * W', K = 704: vector data-grad
+    d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))  # D classifier: stride 2 keeps the direct GEMM
+    kid, _ = K.conv_kernel_id(d5, 4, 32, 64, 0)
+    assert (kid // 10) % 10 == 1              # skinny-N tile (256x32)

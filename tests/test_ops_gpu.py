@@ -139,6 +139,45 @@ def test_conv_epilogues():
     assert rel(nchw(dxl), xr.grad * torch.where(res > 0, 1.0, 0.2)) < 2e-5
 
 
+@pytest.mark.parametrize("rates", [(6, 12, 18, 24), (6, 12)])
+def test_aspp_tap_gemm_epilogues(rates):
+    """ASPP-shaped convs (stride 1, Cout 19, Cin % 32 == 0) take the tap-GEMM path: check the
+    epilogue flags through it — fwd residual / accumulate / ReLU, dgrad accumulate (the
+    engine's layer5 + layer6 gradient sum) and ReLU-grad, wgrad accumulate — and that the
+    selector reports the inner 1x1 GEMM."""
+    k = K()
+    g = torch.Generator().manual_seed(19)
+    n, cin, h, w, cout = 2, 64, 11, 13, 19
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    ws = [torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.1 for _ in rates]
+    bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in rates]
+    geom = k.ConvGeom(cin, cout, 3, 3, 1, rates, rates)
+    sel, _ = k.conv_kernel_id(geom, n, h, w, 0)
+    assert sel % 100 // 10 == 0, sel  # 128x128 tile of the dense 1x1 GEMM, not the 256x32 tile
+    ref = _ref_conv(x, ws, bs, 1, rates, rates)
+    res = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    wd, bd = [w_cl(t) for t in ws], [t.float().to(DEV) for t in bs]
+    y = k.conv_fwd(geom, nhwc(x), n, h, w, wd, bd, res=nhwc(res))
+    assert rel(nchw(y), ref + res) < 2e-5
+    y2 = nhwc(res)
+    k.conv_fwd(geom, nhwc(x), n, h, w, wd, bd, out=y2, flags=k.EPI_ACCUMULATE | k.EPI_RELU)
+    assert rel(nchw(y2), F.relu(ref + res)) < 2e-5
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    wr = [t.clone().requires_grad_(True) for t in ws]
+    _ref_conv(xr, wr, None, 1, rates, rates).backward(gy)
+    prev = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    dx = nhwc(prev)
+    k.conv_dgrad(geom, nhwc(gy), n, h, w, wd, out=dx, flags=k.EPI_ACCUMULATE)
+    assert rel(nchw(dx), xr.grad + prev) < 2e-5
+    dxr = k.conv_dgrad(geom, nhwc(gy), n, h, w, wd, aux=nhwc(prev), flags=k.EPI_RELU_GRAD)
+    assert rel(nchw(dxr), xr.grad * (prev > 0)) < 2e-5
+    dws = [torch.ones_like(t) for t in wd]
+    k.conv_wgrad(geom, nhwc(gy), nhwc(x), n, h, w, dws, accumulate=True)
+    for i in range(len(rates)):
+        assert rel(dws[i].permute(0, 3, 1, 2).cpu() - 1.0, wr[i].grad) < 2e-5
+
+
 @pytest.mark.parametrize("relu,with_res", [(True, False), (False, False), (True, True)])
 def test_batchnorm_train(relu, with_res):
     k = K()
@@ -169,6 +208,11 @@ def test_batchnorm_train(relu, with_res):
     assert rel(nchw(dx), xr.grad) < 1e-5
     if with_res:
         assert rel(nchw(dres), gy * (y > 0)) < 1e-6
+    if relu and not with_res:
+        # ReLU mask recomputed from x (y not read): identical to the y-masked backward
+        dx2 = k.bn_bwd(gyd, None, xd, wt.float().to(DEV), mean, invstd, relu=True,
+                       bias=b.float().to(DEV))
+        assert torch.equal(dx2, dx)
 
 
 def test_batchnorm_eval_and_inplace_bwd():
