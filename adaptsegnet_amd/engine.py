@@ -25,6 +25,47 @@ import torch
 from . import kernels as K
 
 # ---------------------------------------------------------------------------------------
+# Weight gradients on a side stream
+# ---------------------------------------------------------------------------------------
+
+
+class WgradStream:
+    """Runs weight-gradient GEMMs on a second HIP stream of the same device.
+
+    A weight gradient only depends on its layer's saved input and the data gradient just
+    produced on the main stream, and nothing on the main stream depends on it until the
+    optimiser; so it overlaps the main stream's chain of data-gradient GEMMs and the
+    HBM-bound BN-backward passes.  ``launch`` orders the side stream after everything
+    issued so far on the main stream and marks the tensors it reads as used on the side
+    stream (the caching allocator then delays their reuse); ``join`` makes the main stream
+    wait for every weight gradient before the backward returns.
+    """
+
+    _streams: dict = {}
+
+    def __init__(self, device):
+        self.main = torch.cuda.current_stream(device)
+        side = WgradStream._streams.get(device.index)
+        if side is None:
+            side = WgradStream._streams[device.index] = torch.cuda.Stream(device)
+        self.side = side
+        self.used = False
+
+    def launch(self, fn, *tensors):
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn()
+        for t in tensors:
+            t.record_stream(self.side)
+        self.used = True
+
+    def join(self):
+        if self.used:
+            self.main.wait_stream(self.side)
+            self.used = False
+
+
+# ---------------------------------------------------------------------------------------
 # BatchNorm (train: batch statistics; eval: running statistics)
 # ---------------------------------------------------------------------------------------
 
@@ -86,7 +127,17 @@ def block_forward(blk, x, n, h, w, training, save):
     return out, rec
 
 
-def block_backward(blk, rec, gout, need_w):
+def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
+    """Weight gradient of one conv: on the side stream when ``ws`` is given."""
+    def run():
+        K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides)
+    if ws is None:
+        run()
+    else:
+        ws.launch(run, dy, x)
+
+
+def block_backward(blk, rec, gout, need_w, ws=None):
     """gout: grad of the block output (owned, modified in place).  Returns grad of the input."""
     n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
@@ -94,22 +145,22 @@ def block_backward(blk, rec, gout, need_w):
     dc3 = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout)
     dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight])
     if need_w and blk.conv3.weight.grad is not None:
-        K.conv_wgrad(g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
+        _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
     del dc3
     bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True)
     dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
     if need_w and blk.conv2.weight.grad is not None:
-        K.conv_wgrad(g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
+        _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
     del dy2
     bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True)
     if need_w and blk.conv1.weight.grad is not None:
-        K.conv_wgrad(g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
+        _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
         bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout)
         if need_w and dconv.weight.grad is not None:
-            K.conv_wgrad(gd, gout, rec.x, n, h, w, [dconv.weight.grad])
+            _wgrad(ws, gd, gout, rec.x, n, h, w, [dconv.weight.grad])
         dx = K.conv_dgrad(gd, gout, n, h, w, [dconv.weight])
         K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE)
     else:
@@ -135,11 +186,11 @@ def aspp_forward(cls, x, n, h, w):
                       [c.bias for c in cls.conv2d_list])
 
 
-def aspp_backward(cls, gy, x, n, h, w, need_w, gx_out=None):
+def aspp_backward(cls, gy, x, n, h, w, need_w, gx_out=None, ws=None):
     g = aspp_geom(cls)
     if need_w and cls.conv2d_list[0].weight.grad is not None:
-        K.conv_wgrad(g, gy, x, n, h, w, [c.weight.grad for c in cls.conv2d_list],
-                     [c.bias.grad for c in cls.conv2d_list])
+        _wgrad(ws, g, gy, x, n, h, w, [c.weight.grad for c in cls.conv2d_list],
+               [c.bias.grad for c in cls.conv2d_list])
     if gx_out is None:
         return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list])
     return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list], out=gx_out,
@@ -213,27 +264,30 @@ class _DeeplabMultiFn(torch.autograd.Function):
             if g1_up is not None:
                 idx += model._pidx["layer5"]
             model._arena.claim(idx)
+        ws = WgradStream(ctx.x.device) if need_w else None
         gp3 = None
         if g2_up is not None:
             gx2 = K.upsample_bwd(K.nhwc_view(g2_up), h3, w3)
-            gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w)
+            gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w, ws=ws)
             del gx2
             ctx.q = None
             for i in reversed(range(len(model.layer4))):
-                gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w)
+                gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w, ws)
                 ctx.recs4[i] = None
             gp3 = gq
         if g1_up is not None:
             gx1 = K.upsample_bwd(K.nhwc_view(g1_up), h3, w3)
-            gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3)
+            gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3, ws=ws)
             del gx1
         ctx.p3 = None
         if gp3 is None:
+            if ws is not None:
+                ws.join()
             return None, None, None, None, None, None
         blocks = [b for layer in (model.layer1, model.layer2, model.layer3) for b in layer]
         g = gp3
         for i in reversed(range(len(blocks))):
-            g = block_backward(blocks[i], ctx.recs[i], g, need_w)
+            g = block_backward(blocks[i], ctx.recs[i], g, need_w, ws)
             ctx.recs[i] = None
         c0, y0, s0, am = ctx.stem
         ctx.stem = None
@@ -242,11 +296,13 @@ class _DeeplabMultiFn(torch.autograd.Function):
         bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0, mask_from_x=True)
         gs = model.conv1.geom()
         if need_w and model.conv1.weight.grad is not None:
-            K.conv_wgrad(gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
+            _wgrad(ws, gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
         dx = None
         if ctx.needs_input_grad[1]:
             dx = K.as_nchw(K.conv_dgrad(gs, dy0, n, h, w, [model.conv1.weight]))
         ctx.x = None
+        if ws is not None:
+            ws.join()
         return None, dx, None, None, None, None
 
 
@@ -306,20 +362,23 @@ class _FCDiscriminatorFn(torch.autograd.Function):
         g = K.nhwc_view(gout)
         if not g.is_contiguous():
             g = g.contiguous()
+        ws = WgradStream(g.device) if need_w else None
         dx = None
         for i in reversed(range(len(convs))):
             conv = convs[i]
             geo = conv.geom()
             ch, cw, cs = dims[i]
             if need_w and conv.weight.grad is not None:
-                K.conv_wgrad(geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
-                             strides=cs)
+                _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
+                       strides=cs)
             if i > 0:
                 # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
                 g = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i])
             elif ctx.needs_input_grad[1]:
                 dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight]))
             acts[i] = None
+        if ws is not None:
+            ws.join()
         return None, dx, None, None
 
 
@@ -389,9 +448,10 @@ class _DeeplabVGGFn(torch.autograd.Function):
         gc = _branches_geom(branches)
         a, ch, cw = ctx.cls_in
         ctx.cls_in = None
+        ws = WgradStream(g.device) if need_w else None
         if need_w and branches[0].weight.grad is not None:
-            K.conv_wgrad(gc, g, a, n, ch, cw, [b.weight.grad for b in branches],
-                         [b.bias.grad for b in branches])
+            _wgrad(ws, gc, g, a, n, ch, cw, [b.weight.grad for b in branches],
+                   [b.bias.grad for b in branches])
         # grad of fc7's pre-activation: dgrad * relu'(a)
         g = K.conv_dgrad(gc, g, n, ch, cw, [b.weight for b in branches], aux=a,
                          flags=K.EPI_RELU_GRAD)
@@ -403,7 +463,7 @@ class _DeeplabVGGFn(torch.autograd.Function):
             geo = conv.geom()
             xin, ih, iw, cs, _ = acts[i]
             if need_w and conv.weight.grad is not None:
-                K.conv_wgrad(geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
+                _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
             if i > 0:
                 # grad of the previous conv's pre-activation.  xin is its post-ReLU output,
                 # or the 2x2 max of it: relu' at the routed (argmax) position = [max > 0].
@@ -415,6 +475,8 @@ class _DeeplabVGGFn(torch.autograd.Function):
             elif ctx.needs_input_grad[1]:
                 dx = K.as_nchw(K.conv_dgrad(geo, g, n, ih, iw, [conv.weight]))
             acts[i] = None
+        if ws is not None:
+            ws.join()
         return None, dx, None, None
 
 
