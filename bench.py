@@ -128,6 +128,35 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize):
     return inv
 
 
+# kernel selector (adaptseg_conv2d_kernel_id) -> the kernel template rocprofv3 reports
+_CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32), 3: (64, 256, 1, 4, 32),
+        4: (256, 64, 4, 1, 16), 5: (64, 64, 2, 2, 32), 6: (128, 128, 2, 2, 16), 7: (256, 128, 4, 2, 32)}
+
+
+def selector_symbol(sel):
+    op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
+    bm, bn, wm, wn, bk = _CFG[cfg]
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    if var >= 4:
+        v = var - 4
+        return (f"igemm_fast_kernel<{op}, {bm}, {bn}, {wm}, {wn}, {bk}, {b(v & 4)}, {b(v & 2)}, "
+                f"{b(v & 1)}>")
+    return f"igemm_kernel<{op}, {bm}, {bn}, {wm}, {wn}, {b(var & 2)}, {b(var & 1)}>"
+
+
+def pmc_traffic(config, sel):
+    """Per-launch HBM-side bytes of the dominant kernel from the committed PMC passes
+    (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command)."""
+    path = os.path.join(REPO, "profiles", "r1", "pmc", f"traffic_{config}.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("kernel") != selector_symbol(sel) or not d.get("traffic_bytes_per_launch"):
+        return None, None
+    return float(d["traffic_bytes_per_launch"]), os.path.relpath(path, REPO)
+
+
 def cpu_baseline(threads):
     """The oracle's single-level step at batch 1, 1024x512, fp32 on `threads` host cores."""
     from oracle import reference_torch as R
@@ -157,14 +186,22 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path with several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     from adaptsegnet_amd import kernels as K
@@ -245,9 +282,14 @@ def main():
     if not args.no_roofline and k_launches:
         avg_ms = k_ms / k_launches
         ach = k_flops / (k_ms / 1e3) / 1e12
+        traffic, tsrc = pmc_traffic(args.config, dom)
         out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": FP32_MFMA_PEAK_TFLOPS,
-                           "unit": "TFLOP/s", "frac": ach / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                           "kernel": f"igemm_kernel selector {dom}", "launches_per_step": k_launches / args.steps,
+                           "unit": "TFLOP/s", "frac": ach / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                           "traffic_unit": "bytes/launch (L2 memory-side FETCH_SIZE x2 + WRITE_SIZE)",
+                           "traffic_source": tsrc,
+                           "algorithmic_flop_per_launch": k_flops / k_launches,
+                           "kernel": selector_symbol(dom), "selector": dom,
+                           "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,
                            "flop_share_of_step": inv[dom] / step_flops}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -16,3 +16,6 @@ timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench_$TAG.l
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || exit 5
 cd $R && timeout -k 10 600 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c3_$TAG.log 2>&1 || exit 6
 timeout -k 10 600 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c4_$TAG.log 2>&1 || exit 8
+# multi-rank rehearsal on one GPU (gloo): the N>1 code path of bench.py (broadcast, per-rank
+# shards, gradient all-reduce, barrier + max-over-ranks timing)
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 2 --warmup 1 --backend gloo --batch 1 > gpurun_out/bench_dp2_gloo_$TAG.log 2>&1 || exit 9
