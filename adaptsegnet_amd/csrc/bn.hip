@@ -131,6 +131,54 @@ __global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const flo
   }
 }
 
+// Finalise forward statistics from row-tile (count, mean, M2) triples (conv epilogue):
+// lanes merge their tiles sequentially, then a fixed shuffle tree — Chan et al.'s pairwise
+// update in fp64, deterministic.
+__device__ __forceinline__ void chan_merge(double &n, double &m, double &q, double nb, double mb, double qb) {
+  const double nn = n + nb;
+  if (nb == 0.0) return;
+  if (n == 0.0) {
+    n = nb; m = mb; q = qb;
+    return;
+  }
+  const double d = mb - m;
+  m += d * nb / nn;
+  q += qb + d * d * n * nb / nn;
+  n = nn;
+}
+
+__global__ void bn_tiles_final_kernel(int C, int ntiles, const float *__restrict__ stats, float *mean_out,
+                                      float *invstd_out, float *running_mean, float *running_var,
+                                      float momentum, float eps) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const float *cnt = stats, *mu = stats + ntiles + (size_t)c * ntiles;
+  const float *m2 = stats + ntiles + ((size_t)C + c) * ntiles;
+  double n = 0, m = 0, q = 0;
+  for (int t = lane; t < ntiles; t += 64) chan_merge(n, m, q, cnt[t], mu[t], m2[t]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double nb = __shfl_xor(n, o), mb = __shfl_xor(m, o), qb = __shfl_xor(q, o);
+    if (lane & o) {  // the upper lane merges into a copy of the lower one's order: keep the
+      double n2 = nb, m2v = mb, q2 = qb;  // same (lower, upper) operand order on both lanes
+      chan_merge(n2, m2v, q2, n, m, q);
+      n = n2; m = m2v; q = q2;
+    } else {
+      chan_merge(n, m, q, nb, mb, qb);
+    }
+  }
+  if (lane != 0) return;
+  const double var = n > 0 ? q / n : 0.0;
+  mean_out[c] = (float)m;
+  invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * m);
+  if (running_var) {
+    const double unb = n > 1 ? q / (n - 1.0) : var;
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+  }
+}
+
 // Finalise backward sums: store mean(g) and mean(g*xhat) per channel.
 __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ partial,
                                     const float *__restrict__ invstd, float *coef) {
@@ -301,6 +349,23 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
                                                                    save_invstd, running_mean, running_var,
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
+  int64_t total4 = rows * c / 4;
+  bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
+                                                   relu);
+  AS_CHECK_LAUNCH("bn_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                const float *weight, const float *bias, float *running_mean, float *running_var,
+                                float momentum, float eps, float *save_mean, float *save_invstd, const float *res,
+                                float *y, int relu, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
+  AS_CHECK_ARG(stats && ntiles > 0 && x && y && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
+  hipStream_t s = as_stream(stream);
+  bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
+                                                                   running_mean, running_var, momentum, eps);
+  AS_CHECK_LAUNCH("bn_tiles_final");
   int64_t total4 = rows * c / 4;
   bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
                                                    relu);

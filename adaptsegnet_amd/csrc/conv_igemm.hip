@@ -526,6 +526,50 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
   return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
 }
 
+int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
+  AS_CHECK_ARG(bytes, "conv2d_bnstats_size: null");
+  int st = validate(d);
+  if (st) return st;
+  // the smallest row tile any forward config uses (128) bounds the tile count
+  const int64_t m = (int64_t)d->n * d->oh * d->ow;
+  const int64_t nt = ceil_div(m, 128);
+  *bytes = (size_t)(nt + 2 * (int64_t)d->k * nt) * sizeof(float);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w, float *y,
+                                float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                adaptseg_stream_t stream) {
+  AS_CHECK_ARG(ntiles && stats, "conv fwd_bnstats: null stats / ntiles");
+  *ntiles = 0;
+  Plan pl;
+  int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
+  if (st) return st;
+  AS_CHECK_ARG(x && w && y, "conv fwd_bnstats: null pointer");
+  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
+  if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
+    return adaptseg_conv2d_fwd(d, x, w, nullptr, nullptr, y, 0, ws, ws_bytes, stream);
+  ConvParams &p = pl.p;
+  p.x = x;
+  for (int s = 0; s < d->nseg; ++s) {
+    p.wt[s] = w[s];
+    if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
+  }
+  if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
+  set_splits(pl);
+  p.out = y;
+  p.flags = 0;
+  if (pl.fast && p.splits == 1) {
+    const int nt = (int)ceil_div(p.M, kCfgBM[pl.cfg]);
+    if ((size_t)(nt + 2 * (int64_t)p.N * nt) * sizeof(float) <= stats_bytes) {
+      p.stats = stats;
+      p.stats_ntiles = nt;
+      *ntiles = nt;
+    }
+  }
+  return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
+}
+
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream) {

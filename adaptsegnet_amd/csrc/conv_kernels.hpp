@@ -54,6 +54,8 @@ struct ConvParams {
   int kw_, kh_;                // kernel width / height (tap -> kh, kw)
   int pad_[4], dil_[4];        // per-segment padding / dilation
   FastDiv fd_taps, fd_kw;
+  float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
+  int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
 
@@ -1097,6 +1099,69 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           p.out[idx] = v;
         }
+    }
+    if constexpr (MODE == MODE_FWD && !S2) {
+      // BatchNorm statistics of this row tile, straight from the accumulators (the BN that
+      // consumes this conv then skips its statistics pass over y): per column the tile's
+      // mean and sum of squared deviations (two passes over registers, Chan-mergeable in fp64
+      // by bn_fwd_train_tiles).  Only with flags == 0 and no bias: y == acc.
+      if (p.stats) {
+        __syncthreads();  // the LDS stages are free (the main loop ended on a barrier)
+        float *red = lds;  // [WAVES_M][BN]
+        const int nvalid = min(BM, M - bm);
+        float mean[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              s += rl < nvalid ? acc[i][j][r] : 0.f;
+            }
+          s += __shfl_xor(s, 32);
+          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < WAVES_M; ++q) s += red[q * BN + wn * WTN + j * 32 + l32];
+          mean[j] = s / (float)nvalid;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              const float dv = acc[i][j][r] - mean[j];
+              s += rl < nvalid ? dv * dv : 0.f;
+            }
+          s += __shfl_xor(s, 32);
+          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
+        }
+        __syncthreads();
+        const int nt = p.stats_ntiles;
+        if (wm == 0 && hh == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = bn + wn * WTN + j * 32 + l32;
+            if (col >= p.N) continue;
+            float m2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < WAVES_M; ++q) m2 += red[q * BN + wn * WTN + j * 32 + l32];
+            p.stats[nt + (size_t)col * nt + tm] = mean[j];
+            p.stats[nt + ((size_t)p.N + col) * nt + tm] = m2;
+          }
+        }
+        if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
+      }
     }
   }
 }

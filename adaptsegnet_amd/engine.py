@@ -70,10 +70,17 @@ class WgradStream:
 # ---------------------------------------------------------------------------------------
 
 
-def bn_forward(bn, x, res, relu, training):
+def bn_forward(bn, x, res, relu, training, tiles=None):
+    """tiles: row-tile statistics of x from the producing conv (conv_fwd_bnstats), which
+    replace the BN's own statistics pass in train mode."""
     if training:
-        y, mean, invstd = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                         bn.momentum, bn.eps, res=res, relu=relu)
+        if tiles is not None:
+            y, mean, invstd = K.bn_fwd_train_tiles(x, tiles, bn.weight, bn.bias, bn.running_mean,
+                                                   bn.running_var, bn.momentum, bn.eps, res=res,
+                                                   relu=relu)
+        else:
+            y, mean, invstd = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                             bn.momentum, bn.eps, res=res, relu=relu)
         return y, (mean, invstd, True)
     y = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
                        relu=relu)
@@ -102,22 +109,32 @@ class BlockRec:
                  "n", "h", "w", "oh", "ow")
 
 
+def _conv_bn(g, x, n, h, w, weight, strides=None):
+    """Conv feeding a train-mode BN: also returns the BN's row-tile statistics (or None)."""
+    return K.conv_fwd_bnstats(g, x, n, h, w, [weight], strides=strides)
+
+
+def _conv_plain(g, x, n, h, w, weight, strides=None):
+    return K.conv_fwd(g, x, n, h, w, [weight], strides=strides), None
+
+
 def block_forward(blk, x, n, h, w, training, save):
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     oh, ow = g1.out_hw(h, w)
-    c1 = K.conv_fwd(g1, x, n, h, w, [blk.conv1.weight])
-    y1, s1 = bn_forward(blk.bn1, c1, None, True, training)
-    c2 = K.conv_fwd(g2, y1, n, oh, ow, [blk.conv2.weight])
-    y2, s2 = bn_forward(blk.bn2, c2, None, True, training)
-    c3 = K.conv_fwd(g3, y2, n, oh, ow, [blk.conv3.weight])
+    conv = _conv_bn if training else _conv_plain
+    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight)
+    y1, s1 = bn_forward(blk.bn1, c1, None, True, training, t1)
+    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight)
+    y2, s2 = bn_forward(blk.bn2, c2, None, True, training, t2)
+    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight)
     cd = sd = None
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
-        cd = K.conv_fwd(dconv.geom(), x, n, h, w, [dconv.weight])
-        r, sd = bn_forward(dbn, cd, None, False, training)
+        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight)
+        r, sd = bn_forward(dbn, cd, None, False, training, td)
     else:
         r = x
-    out, s3 = bn_forward(blk.bn3, c3, r, True, training)
+    out, s3 = bn_forward(blk.bn3, c3, r, True, training, t3)
     rec = None
     if save:
         rec = BlockRec()
@@ -219,8 +236,8 @@ class _DeeplabMultiFn(torch.autograd.Function):
         # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
         gs = model.conv1.geom()
         h0, w0 = gs.out_hw(h, w)
-        c0 = K.conv_fwd(gs, x, n, h, w, [model.conv1.weight], strides=xs)
-        y0, s0 = bn_forward(model.bn1, c0, None, True, training)
+        c0, t0 = (_conv_bn if training else _conv_plain)(gs, x, n, h, w, model.conv1.weight, xs)
+        y0, s0 = bn_forward(model.bn1, c0, None, True, training, t0)
         p, am = K.maxpool_fwd(y0)
         ph, pw = p.shape[1], p.shape[2]
         recs = []

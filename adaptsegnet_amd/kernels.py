@@ -18,7 +18,8 @@ from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI
                    EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_fwd_train", "bn_fwd_infer", "bn_bwd",
+    "ConvGeom", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
     "axpy", "add_i64", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
@@ -147,6 +148,23 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, bias
     return out
 
 
+def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, strides=None):
+    """y = conv(x, w) plus the per-row-tile BatchNorm statistics of y when the kernel can
+    produce them: returns (y, (stats, ntiles)) or (y, None)."""
+    strides = strides or nhwc_strides(n, h, w, g.cin)
+    d, ws, oh, ow = _desc(g, n, h, w, tuple(strides))
+    out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
+    sb = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_conv2d_bnstats_size(ctypes.byref(d), ctypes.byref(sb)), "conv2d_bnstats_size")
+    stats = torch.empty(sb.value // 4, device=x.device, dtype=torch.float32)
+    nt = ctypes.c_int(0)
+    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    check(_lib.lib().adaptseg_conv2d_fwd_bnstats(
+        ctypes.byref(d), _p(x), _ptrs(weights), _p(out), _p(stats), sb, ctypes.byref(nt), wp, wsz,
+        _stream()), "conv2d_fwd_bnstats")
+    return out, ((stats, nt.value) if nt.value > 0 else None)
+
+
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
                res=None, aux=None, flags: int = 0) -> torch.Tensor:
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD)."""
@@ -202,6 +220,21 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=
         rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
         float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), 1 if relu else 0,
         wp, wsz, _stream()), "bn_fwd_train")
+    return y, mean, invstd
+
+
+def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, momentum, eps, res=None,
+                       relu=True, out=None):
+    """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles."""
+    stats, ntiles = tiles
+    rows, c = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    mean = torch.empty(c, device=x.device, dtype=torch.float32)
+    invstd = torch.empty(c, device=x.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_bn_fwd_train_tiles(
+        rows, c, _p(stats), int(ntiles), _p(x), _p(weight), _p(bias), _p(running_mean),
+        _p(running_var), float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y),
+        1 if relu else 0, _stream()), "bn_fwd_train_tiles")
     return y, mean, invstd
 
 

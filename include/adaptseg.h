@@ -78,6 +78,18 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
                         const float *const *bias, const float *res, float *y, int flags,
                         void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
+/* Forward conv (no bias / epilogue flags) that also emits the per-row-tile BatchNorm
+   statistics of y for adaptseg_bn_fwd_train_tiles: stats = [ntiles] row counts, then
+   [k][ntiles] tile means, then [k][ntiles] tile sums of squared deviations.  *ntiles = 0
+   when the chosen kernel cannot produce them (split-K, unaligned operands, tap-GEMM path):
+   y is still computed and the caller runs adaptseg_bn_fwd_train.  The BN statistics pass
+   over y is skipped otherwise (model/deeplab_multi.py:83-103: every Bottleneck conv feeds a
+   BatchNorm). */
+int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes);
+int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w,
+                                float *y, float *stats, size_t stats_bytes, int *ntiles, void *ws,
+                                size_t ws_bytes, adaptseg_stream_t stream);
+
 /* dx[n,h,w,c] = conv_transpose(dy, w)  (NHWC, contiguous).  aux: LEAKY_/RELU_GRAD source. */
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
@@ -103,6 +115,14 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
                           float momentum, float eps, float *save_mean, float *save_invstd,
                           const float *res, float *y, int relu, void *ws, size_t ws_bytes,
                           adaptseg_stream_t stream);
+
+/* bn_fwd_train from row-tile statistics (adaptseg_conv2d_fwd_bnstats): a Chan merge of the
+   tiles' (count, mean, M2) in fp64 replaces the statistics pass over x; then the same apply. */
+int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                const float *weight, const float *bias, float *running_mean,
+                                float *running_var, float momentum, float eps, float *save_mean,
+                                float *save_invstd, const float *res, float *y, int relu,
+                                adaptseg_stream_t stream);
 
 /* Eval-mode BN (running statistics): y = (x-rm)/sqrt(rv+eps)*w + b (+res), ReLU if relu. */
 int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight,

@@ -215,6 +215,36 @@ def test_batchnorm_train(relu, with_res):
         assert torch.equal(dx2, dx)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 17, 23, 256, 1), (2, 64, 256, 256, 64, 1), (3, 128, 40, 44, 512, 1),
+                                   (1, 32, 9, 11, 64, 3)])
+def test_conv_fused_bn_statistics(shape):
+    """conv_fwd_bnstats + bn_fwd_train_tiles (row-tile statistics from the conv epilogue,
+    Chan-merged in fp64) == conv_fwd + bn_fwd_train, incl. partial row tiles."""
+    k = K()
+    n, cin, h, w, cout, ks = shape
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64) + 0.5
+    wt = torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.1
+    geom = k.ConvGeom(cin, cout, ks, ks, 1, ((ks - 1) // 2,), (1,))
+    bw = (1 + 0.1 * torch.randn(cout, generator=g, dtype=torch.float64)).float().to(DEV)
+    bb = (0.1 * torch.randn(cout, generator=g, dtype=torch.float64)).float().to(DEV)
+    y, tiles = k.conv_fwd_bnstats(geom, nhwc(x), n, h, w, [w_cl(wt)])
+    c = F.conv2d(x, wt, None, 1, (ks - 1) // 2)
+    assert rel(nchw(y), c) < 2e-5
+    if n * h * w < 1000:  # tiny grid -> split-K: no fused statistics, plain output
+        assert tiles is None
+        return
+    assert tiles is not None
+    rm1, rv1 = torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV)
+    rm2, rv2 = torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV)
+    z1, m1, i1 = k.bn_fwd_train_tiles(y, tiles, bw, bb, rm1, rv1, 0.1, 1e-5)
+    z2, m2, i2 = k.bn_fwd_train(y, bw, bb, rm2, rv2, 0.1, 1e-5)
+    ref = F.relu(F.batch_norm(c, None, None, bw.double().cpu(), bb.double().cpu(), True, 0.1, 1e-5))
+    assert rel(nchw(z1), ref) < 1e-5
+    assert rel(m1, m2) < 1e-5 and rel(i1, i2) < 1e-5
+    assert rel(rm1, rm2) < 1e-5 and rel(rv1, rv2) < 1e-5
+
+
 def test_batchnorm_eval_and_inplace_bwd():
     k = K()
     g = torch.Generator().manual_seed(8)
