@@ -318,9 +318,12 @@ void set_splits(Plan &pl) {
   const int nkt = (int)ceil_div(p.K, pl.bk);
   // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~4.
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
+  // fwd / data-grad split only grids below one block per CU (slab + reduce traffic costs more
+  // than the partial second wave it would fill); weight-grad grids are almost always tiny.
   const int target = pl.mode == MODE_WGRAD ? 1024 : 512;
+  const int split_below = pl.mode == MODE_WGRAD ? target : 256;
   int splits = 1;
-  if (pl.tiles < target && !pl.s2) {
+  if (pl.tiles < split_below && !pl.s2) {
     splits = (int)ceil_div(target, pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);

@@ -22,6 +22,7 @@ from adaptsegnet_amd import kernels as K  # noqa: E402
 
 
 def shapes(batch, W=1024, H=512):
+    """(conv geometry, op set) -> [count, name] for one domain's G pass and D passes."""
     """(name, geom, n, h, w, ops, count/step, input strides or None)."""
     out = collections.OrderedDict()
 
@@ -35,8 +36,8 @@ def shapes(batch, W=1024, H=512):
     # generator, 2 passes (source + target), single-level: layer5 fwd only
     h, w = H, W
     add("stem", K.ConvGeom(3, 64, 7, 7, 2, (3,), (1,)), batch, h, w, (0, 2), 2, (3 * h * w, h * w, w, 1))
-    h, w = 256, 512
-    h, w = 128, 256
+    h, w = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1       # stem 7x7/2 p3
+    h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1       # maxpool 3x3/2 p1
     cin = 64
     for li, (planes, nblk, stride, dil) in enumerate(((64, 3, 1, 1), (128, 4, 2, 1), (256, 23, 1, 2), (512, 3, 1, 4)), 1):
         if li == 4:
@@ -72,6 +73,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--filter", default="")
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=512)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -79,7 +82,7 @@ def main():
     per_op = collections.defaultdict(lambda: [0.0, 0.0])
     print(f"{'conv':<10} {'op':>3} {'n':>2} {'hxw':>9} {'cin':>5} {'cout':>5} {'k':>2} {'sel':>4} {'spl':>3} "
           f"{'cnt':>4} {'avg us':>9} {'TF/s':>7}")
-    for (g, n, h, w, ops, st), (count, name) in shapes(args.batch).items():
+    for (g, n, h, w, ops, st), (count, name) in shapes(args.batch, args.width, args.height).items():
         if args.filter and args.filter not in name:
             continue
         oh, ow = g.out_hw(h, w)
