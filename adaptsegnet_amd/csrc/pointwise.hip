@@ -575,11 +575,92 @@ __global__ void axpy_kernel(int64_t n, float a, const float *__restrict__ src, f
     dst[i] = accumulate ? dst[i] + a * src[i] : a * src[i];
 }
 
+// ------------------------------------------------------------------------------------
+// Evaluation (evaluate_cityscapes.py:153-169, compute_iou.py:15-28).
+// ------------------------------------------------------------------------------------
+// interp(logits) to OHxOW (align_corners=True) fused with the class argmax: one thread per
+// output pixel interpolates its C class scores from the 4 source rows (L2-resident: the
+// low-res map is ~2.5 MB) and writes one byte.  First maximal class wins; a NaN score wins
+// over numbers (torch.argmax / np.argmax semantics).
+__global__ void upsample_argmax_kernel(int n, int C, int h, int w, int OH, int OW, const float *__restrict__ x,
+                                       uint8_t *__restrict__ out) {
+  const float sh = ac_scale(h, OH), sw = ac_scale(w, OW);
+  const int64_t total = (int64_t)n * OH * OW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int X = (int)(i % OW);
+    const int64_t t = i / OW;
+    const int Y = (int)(t % OH), b = (int)(t / OH);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    ac_src(sh, Y, h, y0, y1, ly);
+    ac_src(sw, X, w, x0, x1, lx);
+    const float *base = x + (int64_t)b * h * w * C;
+    const float *r00 = base + ((int64_t)y0 * w + x0) * C, *r01 = base + ((int64_t)y0 * w + x1) * C;
+    const float *r10 = base + ((int64_t)y1 * w + x0) * C, *r11 = base + ((int64_t)y1 * w + x1) * C;
+    float best = 0.f;
+    int arg = 0;
+    for (int c = 0; c < C; ++c) {
+      const float v = (1.f - ly) * ((1.f - lx) * r00[c] + lx * r01[c]) + ly * ((1.f - lx) * r10[c] + lx * r11[c]);
+      if (c == 0 || (!isnan(best) && (v > best || isnan(v)))) {
+        best = v;
+        arg = c;
+      }
+    }
+    out[i] = (uint8_t)arg;
+  }
+}
+
+// hist[gt][pred] += 1 over pixels whose (LUT-mapped) label is in [0, n): compute_iou's
+// label_mapping + fast_hist.  Per-block LDS bins, then one 64-bit atomic per non-zero bin
+// (integer adds: the result is exact and order-independent).
+__global__ void __launch_bounds__(256) confusion_hist_kernel(int64_t npix, const uint8_t *__restrict__ gt,
+                                                             const int *__restrict__ lut,
+                                                             const uint8_t *__restrict__ pred, int n,
+                                                             unsigned long long *hist) {
+  extern __shared__ unsigned int bins[];
+  const int nb = n * n;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) bins[j] = 0u;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int a = lut ? lut[gt[i]] : (int)gt[i];
+    const int b = pred[i];
+    if (a >= 0 && a < n && b < n) atomicAdd(&bins[a * n + b], 1u);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nb; j += blockDim.x)
+    if (bins[j]) atomicAdd(&hist[j], (unsigned long long)bins[j]);
+}
+
 }  // namespace adaptseg
 
 using namespace adaptseg;
 
 extern "C" {
+
+int adaptseg_upsample_argmax(int n, int c, int h, int w, int oh, int ow, const float *x, uint8_t *out,
+                             adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && c <= 256 && h > 0 && w > 0 && oh > 0 && ow > 0 && x && out,
+               "upsample_argmax: bad args");
+  const int64_t total = (int64_t)n * oh * ow;
+  upsample_argmax_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, x, out);
+  AS_CHECK_LAUNCH("upsample_argmax");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_confusion_hist(int64_t npix, const uint8_t *gt, const int32_t *lut, const uint8_t *pred, int ncls,
+                            int64_t *hist, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(npix >= 0 && ncls > 0 && ncls <= 128 && hist && (npix == 0 || (gt && pred)),
+               "confusion_hist: bad args");
+  if (npix == 0) return ADAPTSEG_OK;
+  const int blocks = grid1d(npix, 256 * 16, 1024);
+  confusion_hist_kernel<<<blocks, 256, (size_t)ncls * ncls * sizeof(unsigned int), as_stream(stream)>>>(
+      npix, gt, lut, pred, ncls, reinterpret_cast<unsigned long long *>(hist));
+  AS_CHECK_LAUNCH("confusion_hist");
+  return ADAPTSEG_OK;
+}
+
 
 const char *adaptseg_last_error(void) { return g_err; }
 const char *adaptseg_version(void) { return "adaptseg 0.1 gfx950 fp32-mfma"; }

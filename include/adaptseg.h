@@ -141,6 +141,18 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
+/* Evaluation: evaluate_cityscapes.py:153-169 (interp to 1024x2048 + argmax) and          */
+/* compute_iou.py:15-28 (label_mapping + fast_hist).                                      */
+/* ------------------------------------------------------------------------------------ */
+/* out[n][oh][ow] = argmax_c bilinear_align_corners(x)[n][oh][ow][c]; x NHWC [n][h][w][c]. */
+int adaptseg_upsample_argmax(int n, int c, int h, int w, int oh, int ow, const float *x,
+                             uint8_t *out, adaptseg_stream_t stream);
+/* hist[a][b] += #pixels with a = lut[gt] (or gt if lut == NULL) in [0, ncls), b = pred;
+   hist is int64 [ncls][ncls] (accumulated, never cleared). */
+int adaptseg_confusion_hist(int64_t npix, const uint8_t *gt, const int32_t *lut,
+                            const uint8_t *pred, int ncls, int64_t *hist, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
 /* MaxPool2d (model/deeplab_multi.py:135: kernel 3, stride 2, pad 1, floor mode), NHWC.  */
 /* ------------------------------------------------------------------------------------ */
 int adaptseg_maxpool2d_fwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,

@@ -19,3 +19,4 @@ timeout -k 10 600 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-base
 # multi-rank rehearsal on one GPU (gloo): the N>1 code path of bench.py (broadcast, per-rank
 # shards, gradient all-reduce, barrier + max-over-ranks timing)
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 2 --warmup 1 --backend gloo --batch 1 > gpurun_out/bench_dp2_gloo_$TAG.log 2>&1 || exit 9
+timeout -k 10 600 python tools/bench_eval.py > gpurun_out/bench_eval_$TAG.log 2>&1 || exit 10
