@@ -580,13 +580,45 @@ __device__ __forceinline__ float4 mask4(int m, float4 v) {
   return make_float4((m & 1) ? v.x : 0.f, (m & 2) ? v.y : 0.f, (m & 4) ? v.z : 0.f, (m & 8) ? v.w : 0.f);
 }
 
-__device__ __forceinline__ void seg_geom(const ConvParams &p, int tap, int &seg, int &t, int &dy, int &dx) {
+// Per-segment dilation / padding / weight pointer held in SGPRs for the whole kernel.  A
+// select chain over p.dil_[seg] directly compiles to an indexed kernarg s_load inside the
+// K loop, whose lgkmcnt(0) wait then stalls every K tile; readfirstlane'd copies cannot be
+// rematerialised as loads.
+struct SegRegs {
+  int dilpack, padpack;          // byte s = dilation / padding of segment s (<= 255)
+  uint32_t wlo, whi;             // lane s (s < 4) holds the weight pointer of segment s
+};
+
+__device__ __forceinline__ SegRegs seg_regs(const ConvParams &p) {
+  SegRegs r;
+  r.dilpack = __builtin_amdgcn_readfirstlane(p.dil_[0] | (p.dil_[1] << 8) | (p.dil_[2] << 16) | (p.dil_[3] << 24));
+  r.padpack = __builtin_amdgcn_readfirstlane(p.pad_[0] | (p.pad_[1] << 8) | (p.pad_[2] << 16) | (p.pad_[3] << 24));
+  const uint64_t w = (uint64_t)p.wt[threadIdx.x & 3];
+  r.wlo = (uint32_t)w;
+  r.whi = (uint32_t)(w >> 32);
+  return r;
+}
+
+// Uniform segment -> weight pointer with two v_readlane_b32 (no memory access in the K loop:
+// a select chain over p.wt[] compiles to an indexed kernarg / LDS table load whose
+// lgkmcnt(0) wait stalls every K tile).  The pointer is rebuilt through an explicit global
+// (addrspace 1) pointer so its loads stay global_load: a flat load would also count against
+// lgkmcnt and serialise the LDS waits of the MFMA loop.
+__device__ __forceinline__ const float *seg_ptr(const SegRegs &r, int seg) {
+  typedef const float __attribute__((address_space(1))) gfloat;
+  const uint32_t lo = __builtin_amdgcn_readlane(r.wlo, seg);
+  const uint32_t hi = __builtin_amdgcn_readlane(r.whi, seg);
+  return (const float *)(gfloat *)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr, int tap, int &seg, int &t,
+                                         int &dy, int &dx) {
   seg = (int)fdiv((uint32_t)tap, p.fd_taps);
   t = tap - seg * p.taps_per_seg;
   const int kh = (int)fdiv((uint32_t)t, p.fd_kw);
   const int kw = t - kh * p.kw_;
-  const int dil = seg == 0 ? p.dil_[0] : seg == 1 ? p.dil_[1] : seg == 2 ? p.dil_[2] : p.dil_[3];
-  const int pad = seg == 0 ? p.pad_[0] : seg == 1 ? p.pad_[1] : seg == 2 ? p.pad_[2] : p.pad_[3];
+  const int dil = (sr.dilpack >> (8 * seg)) & 255;
+  const int pad = (sr.padpack >> (8 * seg)) & 255;
   dy = kh * dil - pad;
   dx = kw * dil - pad;
 }
@@ -616,6 +648,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
   const int tm = tile / ntn, tn = tile - tm * ntn;
   const int bm = tm * BM, bn = tn * BN;
   const int split = blockIdx.y;
+  const SegRegs sr = seg_regs(p);
 
   // Stride-2 data gradient: blockIdx.z = output-pixel parity class (py, px).  The class's
   // pixels (2i+py, 2j+px) form a dense (Hc x Wc) grid that only the taps kh = kh0 + 2u,
@@ -709,7 +742,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
         const int tap = (int)fdiv((uint32_t)nn, p.fd_c);
         const int ci = nn - tap * p.c;
         int seg, t;
-        seg_geom(p, tap, seg, t, b_dy[i], b_dx[i]);
+        seg_geom(p, sr, tap, seg, t, b_dy[i], b_dx[i]);
         b_off[i] = ci;
       } else {  // WGRAD B' per element: pack (dy, dx) and the channel offset per column
 #pragma unroll
@@ -718,7 +751,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           const int tap = (int)fdiv((uint32_t)min(ne, p.N - 1), p.fd_c);
           const int ci = min(ne, p.N - 1) - tap * p.c;
           int seg, t, dy, dx;
-          seg_geom(p, tap, seg, t, dy, dx);
+          seg_geom(p, sr, tap, seg, t, dy, dx);
           b_pk[i][e] = (dy + 32768) | ((dx + 32768) << 16);
           b_ci[i][e] = ne < p.N ? ci * p.sxc : -1;
         }
@@ -735,7 +768,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
       if constexpr (!AE) {
         const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
         int seg, t, dy, dx;
-        seg_geom(p, tap, seg, t, dy, dx);
+        seg_geom(p, sr, tap, seg, t, dy, dx);
         dy = uni(dy);
         dx = uni(dx);
         const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
@@ -770,7 +803,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
       }
       if constexpr (!BE) {
         const int seg = uni((int)fdiv((uint32_t)kbase, p.fd_nseg_k));
-        const float *wp = seg_ptr(p, seg) + (kbase - seg * p.kseg);
+        const float *wp = seg_ptr(sr, seg) + (kbase - seg * p.kseg);
 #pragma unroll
         for (int i = 0; i < NQB; ++i) {
           mb[i] = b_ok[i] ? 15 : 0;
@@ -785,7 +818,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           for (int e = 0; e < 4; ++e) {
             const bool v = b_ok[i] && kbase + b_k[i] + e < K;
             msk |= v ? (1 << e) : 0;
-            vv[e] = p.wt[0][v ? b_off[i] + kbase + e : 0];
+            vv[e] = seg_ptr(sr, 0)[v ? b_off[i] + kbase + e : 0];
           }
           mb[i] = msk;
           rb[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -804,7 +837,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           dy = uni(-((py + p.pad_[0] - kh) >> 1));  // dY row = i - dy
           dx = uni(-((px + p.pad_[0] - kw) >> 1));
         } else {
-          seg_geom(p, tap, seg, t, dy, dx);
+          seg_geom(p, sr, tap, seg, t, dy, dx);
           seg = uni(seg);
           t = uni(t);
           dy = uni(dy);
@@ -818,7 +851,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           ma[i] = v ? 15 : 0;
           ra[i] = ld4(p.dy + (v ? a_pix[i] + soff : 0));
         }
-        const float *wp = seg_ptr(p, seg) + (co0 * p.taps_per_seg + t) * p.c;
+        const float *wp = seg_ptr(sr, seg) + (co0 * p.taps_per_seg + t) * p.c;
 #pragma unroll
         for (int i = 0; i < NQB; ++i) {
           if constexpr (!BE) {
@@ -850,7 +883,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
             const int tap = (int)fdiv((uint32_t)kc, p.fd_k);
             const int co = kc - tap * p.k;
             int seg, t, dy, dx;
-            seg_geom(p, tap, seg, t, dy, dx);
+            seg_geom(p, sr, tap, seg, t, dy, dx);
             const bool v = a_ok[i] && k < K && (unsigned)(a_y[i] - dy) < (unsigned)p.oh &&
                            (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
             msk |= v ? (1 << e) : 0;
@@ -867,7 +900,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
           const int tap = (int)fdiv((uint32_t)kc, p.fd_k);
           const int co = kc - tap * p.k;
           int seg, t, dy, dx;
-          seg_geom(p, tap, seg, t, dy, dx);
+          seg_geom(p, sr, tap, seg, t, dy, dx);
           const float *row = seg_ptr(p, seg) + (co * p.taps_per_seg + t) * p.c;
           const int n = bn + b_col[i];
           if constexpr (!BE) {

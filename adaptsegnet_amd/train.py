@@ -82,6 +82,7 @@ class AdaptSegTrainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self._consts = {}
+        self._pending = []
 
     # -- helpers -------------------------------------------------------------------------
     def _c(self, v: float, device):
@@ -118,16 +119,36 @@ class AdaptSegTrainer:
         return c.input_size if mode == "source" else c.input_size_target
 
     def sync_gradients(self):
-        """SUM all-reduce of each parameter arena's gradients (RCCL on ROCm)."""
+        """SUM all-reduce of each parameter arena's gradients (RCCL on ROCm), blocking."""
+        self._start_sync((self.model, self.D1, self.D2))
+        self._finish_sync()
+
+    def _start_sync(self, models):
+        """Launch the arena all-reduces of ``models`` asynchronously.  RCCL orders them after
+        the work already queued on the current stream (the gradients they read) and runs them
+        on its own stream, so they overlap whatever the step launches next."""
         if self.world == 1:
             return
-        for m in (self.model, self.D1, self.D2):
+        pending = self.__dict__.setdefault("_pending", [])
+        for m in models:
             if m is not None and m.arena is not None:
-                dist.all_reduce(m.arena.grad, op=dist.ReduceOp.SUM, group=self.pg)
+                pending.append(dist.all_reduce(m.arena.grad, op=dist.ReduceOp.SUM,
+                                                     group=self.pg, async_op=True))
+
+    def _finish_sync(self):
+        """Make the current stream wait for every launched all-reduce (no host sync)."""
+        for w in self.__dict__.get("_pending", ()):
+            w.wait()
+        self._pending = []
 
     # -- the step --------------------------------------------------------------------------
     def step(self, i_iter, batches):
-        """batches: iterable of ``iter_size`` tuples (images, labels, images_target)."""
+        """batches: iterable of ``iter_size`` tuples (images, labels, images_target).
+
+        Multi-GPU: the generator's gradients are final after its adversarial backward of the
+        last sub-iteration, so their all-reduce (the 178 MB arena) is launched right there and
+        overlaps the discriminator forward/backward passes; the discriminators' (11 MB each)
+        follow their last backward.  The optimisers wait for both."""
         c = self.cfg
         L = StepLosses()
         self.opt.zero_grad()
@@ -137,12 +158,18 @@ class AdaptSegTrainer:
         self.adjust_learning_rate(i_iter)
         inv = 1.0 / c.iter_size
         tsize = self._target_size()
-        for images, labels, images_t in batches:
+        batches = list(batches)
+        self._pending = []
+        for idx, (images, labels, images_t) in enumerate(batches):
+            g_done = (lambda: self._start_sync((self.model,))) if idx == len(batches) - 1 else None
             if c.level == "single-level":
-                self._sub_single(images, labels, images_t, inv, tsize, L)
+                self._sub_single(images, labels, images_t, inv, tsize, L, g_done)
             else:
-                self._sub_multi(images, labels, images_t, inv, tsize, L)
-        self.sync_gradients()
+                self._sub_multi(images, labels, images_t, inv, tsize, L, g_done)
+        if not batches:
+            self._start_sync((self.model,))
+        self._start_sync((self.D1, self.D2))
+        self._finish_sync()
         gs = 1.0 / self.world
         self.opt.step(grad_scale=gs)
         if self.opt_D1 is not None:
@@ -157,7 +184,7 @@ class AdaptSegTrainer:
             return F.interp(self.model(images), (size[1], size[0]))
         return self.model(images, size)[1]
 
-    def _sub_single(self, images, labels, images_t, inv, tsize, L):
+    def _sub_single(self, images, labels, images_t, inv, tsize, L, g_done=None):
         """train_gta2cityscapes_multi.py:385-461."""
         c, D2 = self.cfg, self.D2
         self._set_requires_grad(D2, False)
@@ -171,6 +198,8 @@ class AdaptSegTrainer:
         loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
         self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])
         L.add("loss_adv_target2", loss_adv_target2, inv)
+        if g_done is not None:
+            g_done()
 
         self._set_requires_grad(D2, True)
         pred2 = pred2.detach()
@@ -182,7 +211,7 @@ class AdaptSegTrainer:
         self._backward([loss_d2], [inv / 2])
         L.add("loss_D2", loss_d2, inv / 2)
 
-    def _sub_multi(self, images, labels, images_t, inv, tsize, L):
+    def _sub_multi(self, images, labels, images_t, inv, tsize, L, g_done=None):
         """train_gta2cityscapes_multi.py:578-679."""
         c, D1, D2 = self.cfg, self.D1, self.D2
         self._set_requires_grad(D1, False)
@@ -203,6 +232,8 @@ class AdaptSegTrainer:
                        [c.lambda_adv_target1 * inv, c.lambda_adv_target2 * inv])
         L.add("loss_adv_target1", loss_adv1, inv)
         L.add("loss_adv_target2", loss_adv2, inv)
+        if g_done is not None:
+            g_done()
 
         self._set_requires_grad(D1, True)
         self._set_requires_grad(D2, True)

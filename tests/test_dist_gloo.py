@@ -60,6 +60,43 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
+def _overlap_worker(rank, world, port, out):
+    """The step's overlapped order: G's all-reduce launched asynchronously, more work (the
+    D passes) queued while it runs, then the D arenas, then one wait for all of them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from adaptsegnet_amd.train import AdaptSegTrainer
+        g = _shard_grads(rank, None).clone()
+        d1 = torch.full((1000,), float(rank + 1), dtype=torch.float64)
+        d2 = torch.arange(7, dtype=torch.float64) * (rank + 1)
+        tr = AdaptSegTrainer.__new__(AdaptSegTrainer)
+        tr.model, tr.D1, tr.D2, tr.pg = _FakeModel(g), _FakeModel(d1), _FakeModel(d2), None
+        tr.world = dist.get_world_size()
+        tr._start_sync((tr.model,))
+        busy = _shard_grads(1 - rank, None)          # the D passes of the step
+        tr._start_sync((tr.D1, tr.D2))
+        tr._finish_sync()
+        out[rank] = (g.clone(), d1.clone(), d2.clone(), float(busy.sum()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_sync_matches_blocking_sync():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_overlap_worker, args=(world, port, out), nprocs=world, join=True)
+    g_sum = _shard_grads(0, None) + _shard_grads(1, None)
+    for r in range(world):
+        g, d1, d2, _ = out[r]
+        assert torch.allclose(g, g_sum, rtol=1e-12, atol=1e-15)
+        assert torch.equal(d1, torch.full((1000,), 3.0, dtype=torch.float64))
+        assert torch.equal(d2, torch.arange(7, dtype=torch.float64) * 3)
+    assert torch.equal(out[0][0], out[1][0])
+
+
 def test_gradient_sync_matches_dataparallel_mean():
     world = 2
     port = _free_port()
