@@ -23,6 +23,7 @@ EPI_RESIDUAL = 8
 EPI_RELU = 16
 EPI_RELU_GRAD = 32
 CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT = 0, 1, 2
+MATH_F32, MATH_BF16 = 0, 1
 
 
 class AdaptSegLibraryError(RuntimeError):
@@ -85,6 +86,8 @@ _SIGS = {
     "adaptseg_to_nhwc": [_I, _I, _I, _I, ctypes.POINTER(_L), _P, _P, _P],
     "adaptseg_axpy": [_L, _F, _P, _P, _I, _P],
     "adaptseg_add_i64": [_P, _L, _L, _P],
+    "adaptseg_conv_set_math": [_I],
+    "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(_L)],

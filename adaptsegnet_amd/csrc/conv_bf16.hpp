@@ -1,0 +1,335 @@
+// Implicit-GEMM convolution on bf16 MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulate) for
+// gfx950 — the "bf16" conv math of BASELINE config c5 (adaptseg_conv_set_math).
+//
+// Same three products, gathers, tile order, split-K and epilogue as igemm_fast_kernel
+// (conv_kernels.hpp); what changes is the operand path:
+//   * activations stay fp32 in HBM; each K tile is gathered as fp32 and rounded to bf16
+//     (round-to-nearest-even, v_cvt_pk_bf16_f32) on its way into LDS;
+//   * weights are packed once per call into bf16 K-contiguous rows (FWD: Wf[co][seg,tap,ci],
+//     DGRAD: Wd[ci][seg,tap,co]) by conv_wpack_*_kernel, so the B operand of FWD and DGRAD is a
+//     plain 16-byte load straight into LDS;
+//   * LDS images: a K-contiguous operand is [row][64 k] (128-B rows, 16-B chunk ch of row r at
+//     (ch ^ (r>>1 & 7)) — conflict-free for the ds_read_b128 fragment reads and the
+//     ds_write_b128 stores); an M/N-contiguous operand (both WGRAD operands: k = output pixel)
+//     is [64 k][128 m] (256-B rows, chunk ch at ch ^ ((r&3)<<2 | (r>>2)&3)) read with the
+//     ds_read_b64_tr_b16 transpose, so neither operand is transposed through registers.
+// Block tile 128x128x64, 4 waves (2x2), each wave 64x64 = 2x2 MFMA tiles of 32x32x16.
+#pragma once
+#include "conv_kernels.hpp"
+
+namespace adaptseg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int kB16BK = 64;
+
+// 128-B row (64 bf16 along k), 16-B chunk ch (8 k) of row r
+__device__ __forceinline__ int kc_off(int r, int ch) { return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4); }
+// 256-B row (128 bf16 along m/n), 16-B chunk ch (8 m) of k-row r
+__device__ __forceinline__ int mc_off(int r, int ch) {
+  return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4);
+}
+
+__device__ __forceinline__ uint2 cvt4_bf16(float4 v) {
+  floatx4v f = {v.x, v.y, v.z, v.w};
+  bf16x4 h = __builtin_convertvector(f, bf16x4);
+  return __builtin_bit_cast(uint2, h);
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// Transposed fragment of an M/N-contiguous image: lane l gets column c0 + (l&31), k rows
+// 16*ks + 8*(l>>5) + 0..7 (the MFMA operand map), in two ds_read_b64_tr_b16.
+__device__ __forceinline__ bf16x8 mc_frag(const char *img, int c0, int ks, int lane) {
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+  const int cb = c0 + 16 * (g & 1);
+  const int kb = 16 * ks + 8 * (g >> 1);
+  const int ch = (cb >> 3) + (pp >> 1);
+  const int o0 = mc_off(kb + q, ch) + 8 * (pp & 1);
+  const int o1 = mc_off(kb + 4 + q, ch) + 8 * (pp & 1);
+  const uint32_t base = (uint32_t)(uintptr_t)img;
+  bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(base + o0));
+  bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(base + o1));
+  return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// K-contiguous fragment: lane l gets row r0 + (l&31), k 16*ks + 8*(l>>5) + 0..7.
+__device__ __forceinline__ bf16x8 kc_frag(const char *img, int r0, int ks, int lane) {
+  return as_bf16x8(*reinterpret_cast<const uint4 *>(img + kc_off(r0 + (lane & 31), 2 * ks + (lane >> 5))));
+}
+
+template <int MODE, bool S2>
+__global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  constexpr int BM = 128, BN = 128, BK = kB16BK, NT = 256;
+  constexpr int WAVES_M = 2, WAVES_N = 2, TM = 2, TN = 2;
+  constexpr bool MC = MODE == MODE_WGRAD;      // both operands M/N-contiguous
+  constexpr int IMG = 16384;                   // bytes per operand image (128 x 64 bf16)
+  constexpr int STAGE = 2 * IMG;
+  constexpr int NQ = MC ? BM * BK / 4 / NT : BM * BK / 8 / NT;  // slots per thread per operand: 8 / 4
+  static_assert(NQ * NT * (MC ? 4 : 8) == BM * BK, "slots cover the tile");
+
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int bm = tm * BM, bn = tn * BN;
+  const int split = blockIdx.y;
+  const SegRegs sr = seg_regs(p);
+
+  int M = p.M, K = p.K, Hc = p.h, Wc = p.w, py = 0, px = 0, kh0 = 0, kw0 = 0, nkw = p.kw_;
+  if constexpr (S2) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (p.h - py + 1) >> 1;
+    Wc = (p.w - px + 1) >> 1;
+    kh0 = (py + p.pad_[0]) & 1;
+    kw0 = (px + p.pad_[0]) & 1;
+    const int nkh = (p.kh_ - kh0 + 1) >> 1;
+    nkw = (p.kw_ - kw0 + 1) >> 1;
+    M = p.n * Hc * Wc;
+    K = nkh * nkw * p.k;
+    if (bm >= M) return;
+  }
+  const int nkt = (K + BK - 1) / BK;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
+  const int ktot = p.ntaps * (MODE == MODE_FWD ? p.c : p.k);  // packed weight row length
+
+  // ---- per-slot constants ----
+  // K-contiguous slot q: row q>>3, chunk q&7 (8 k).  M/N-contiguous slot q: k-row q>>5,
+  // columns 4*(q&31) .. +3.
+  int a_pix[NQ], a_y[NQ], a_x[NQ];
+  bool a_ok[NQ];
+  int b_off[NQ], b_dy[NQ], b_dx[NQ];
+  bool b_ok[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = tid + NT * i;
+    if constexpr (!MC) {
+      const int row = q >> 3, ch = q & 7;
+      const int m = bm + row;
+      a_ok[i] = m < M;
+      const int mm = min(m, M - 1);
+      if constexpr (S2) {
+        const int j = mm % Wc, t2 = mm / Wc;
+        const int ii = t2 % Hc, b = t2 / Hc;
+        a_y[i] = ii;
+        a_x[i] = j;
+        a_pix[i] = ((b * p.oh + ii) * p.ow + j) * p.k + 8 * ch;
+      } else if constexpr (MODE == MODE_FWD) {
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        a_y[i] = oh * p.stride;
+        a_x[i] = ow * p.stride;
+        a_pix[i] = (int)b * p.sxn + a_y[i] * p.sxh + a_x[i] * p.sxw + 8 * ch;
+      } else {
+        uint32_t t = fdiv((uint32_t)mm, p.fd_w);
+        const int iw = mm - (int)t * p.w;
+        uint32_t b = fdiv(t, p.fd_hw);
+        const int ih = (int)t - (int)b * p.h;
+        a_y[i] = ih;
+        a_x[i] = iw;
+        a_pix[i] = (((int)b * p.oh + ih) * p.ow + iw) * p.k + 8 * ch;
+      }
+      const int n = bn + row;
+      b_ok[i] = n < p.N;
+      b_off[i] = min(n, p.N - 1) * ktot + 8 * ch;
+    } else {
+      const int col = 4 * (q & 31);
+      a_ok[i] = bm + col < p.M;                    // Cout % 4 == 0
+      a_pix[i] = a_ok[i] ? bm + col : 0;
+      const int n = bn + col;
+      b_ok[i] = n < p.N;
+      const int nn = b_ok[i] ? n : 0;
+      const int tap = (int)fdiv((uint32_t)nn, p.fd_c);
+      int seg, t;
+      seg_geom(p, sr, tap, seg, t, b_dy[i], b_dx[i]);
+      b_off[i] = nn - tap * p.c;                   // input channel of the column
+    }
+  }
+
+  float4 ra[MC ? NQ : 2 * NQ];
+  float4 rbf[MC ? NQ : 1];
+  uint4 rbh[MC ? 1 : NQ];
+  bool ma[NQ], mb[NQ];
+
+  auto load_tile = [&](int kt) {
+    const int kbase = kt * BK;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
+      int seg, t, dy, dx;
+      seg_geom(p, sr, tap, seg, t, dy, dx);
+      dy = uni(dy);
+      dx = uni(dx);
+      const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const bool v = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h && (unsigned)(a_x[i] + dx) < (unsigned)p.w;
+        ma[i] = v;
+        const float *src = p.x + (v ? a_pix[i] + soff : 0);
+        ra[2 * i] = ld4(src);
+        ra[2 * i + 1] = ld4(src + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        mb[i] = b_ok[i];
+        rbh[i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + kbase);
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
+      const int co0 = kbase - tap * p.k;
+      int dy, dx, wk;
+      if constexpr (S2) {
+        const int u = tap / nkw, v = tap - u * nkw;
+        const int kh = kh0 + 2 * u, kw = kw0 + 2 * v;
+        dy = uni(-((py + p.pad_[0] - kh) >> 1));
+        dx = uni(-((px + p.pad_[0] - kw) >> 1));
+        wk = uni((kh * p.kw_ + kw) * p.k + co0);   // packed row offset of (tap, co0)
+      } else {
+        int seg, t;
+        seg_geom(p, sr, tap, seg, t, dy, dx);
+        dy = uni(dy);
+        dx = uni(dx);
+        wk = kbase;
+      }
+      const int soff = uni(co0 - (dy * p.ow + dx) * p.k);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const bool v = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh && (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
+        ma[i] = v;
+        const float *src = p.dy + (v ? a_pix[i] + soff : 0);
+        ra[2 * i] = ld4(src);
+        ra[2 * i + 1] = ld4(src + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        mb[i] = b_ok[i];
+        rbh[i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + wk);
+      }
+    } else {  // WGRAD: k = output pixel
+      const int krow0 = tid >> 5;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int m = kbase + krow0 + (NT / 32) * i;
+        const bool rv = m < K;
+        ma[i] = rv && a_ok[i];
+        ra[i] = ld4(p.dy + (size_t)(rv ? m : 0) * p.k + a_pix[i]);
+        const int mm = min(m, K - 1);
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        const int iy = oh * p.stride + b_dy[i], ix = ow * p.stride + b_dx[i];
+        const bool v = b_ok[i] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+        mb[i] = v;
+        rbf[i] = ld4(p.x + (v ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char *As = lds + buf * STAGE;
+    char *Bs = As + IMG;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = tid + NT * i;
+      if constexpr (!MC) {
+        const int row = q >> 3, ch = q & 7;
+        const uint2 lo = cvt4_bf16(ra[2 * i]), hi = cvt4_bf16(ra[2 * i + 1]);
+        const uint4 av = ma[i] ? make_uint4(lo.x, lo.y, hi.x, hi.y) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4 *>(As + kc_off(row, ch)) = av;
+        *reinterpret_cast<uint4 *>(Bs + kc_off(row, ch)) = mb[i] ? rbh[i] : make_uint4(0, 0, 0, 0);
+      } else {
+        const int kr = q >> 5, col = 4 * (q & 31);
+        const int o = mc_off(kr, col >> 3) + 8 * ((col >> 2) & 1);
+        const uint2 av = cvt4_bf16(ra[i]), bv = cvt4_bf16(rbf[i]);
+        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? av : make_uint2(0, 0);
+        *reinterpret_cast<uint2 *>(Bs + o) = mb[i] ? bv : make_uint2(0, 0);
+      }
+    }
+  };
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      const char *As = lds + cur * STAGE;
+      const char *Bs = As + IMG;
+      bf16x8 a[2][TM], b[2][TN];
+      auto read_frags = [&](int ks, int slot) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[slot][i] = MC ? mc_frag(As, wm * 64 + i * 32, ks, lane) : kc_frag(As, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[slot][j] = MC ? mc_frag(Bs, wn * 64 + j * 32, ks, lane) : kc_frag(Bs, wn * 64 + j * 32, ks, lane);
+      };
+      read_frags(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int cb = ks & 1;
+        if (ks + 1 < BK / 16) read_frags(ks + 1, cb ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
+      }
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+                                                      reinterpret_cast<float *>(lds));
+}
+
+// bf16 weight packing (once per conv call; weights are small next to the activations).
+// FWD: out[co][seg*kseg + tk] = W_seg[co][tk], tk = tap*Cin + ci  (K-contiguous rows).
+__global__ void conv_wpack_fwd_kernel(const ConvParams p, __bf16 *out) {
+  const int ktot = p.nseg * p.kseg;
+  const int64_t n = (int64_t)p.k * ktot;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i / ktot), kk = (int)(i - (int64_t)co * ktot);
+    const int seg = kk / p.kseg, tk = kk - seg * p.kseg;
+    out[i] = (__bf16)seg_ptr(p, seg)[(size_t)co * p.kseg + tk];
+  }
+}
+
+// DGRAD: out[ci][tap*Cout + co] = W_seg(tap)[co][t][ci]  (tap over all segments).
+__global__ void conv_wpack_dgrad_kernel(const ConvParams p, __bf16 *out) {
+  const int ktot = p.ntaps * p.k;
+  const int64_t n = (int64_t)p.c * ktot;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i / ktot), kk = (int)(i - (int64_t)ci * ktot);
+    const int tap = kk / p.k, co = kk - tap * p.k;
+    const int seg = tap / p.taps_per_seg, t = tap - seg * p.taps_per_seg;
+    out[i] = (__bf16)seg_ptr(p, seg)[((size_t)co * p.taps_per_seg + t) * p.c + ci];
+  }
+}
+
+}  // namespace adaptseg

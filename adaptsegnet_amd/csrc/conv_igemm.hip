@@ -17,6 +17,7 @@
 // MFMA pipe).  LDS holds both operands k-major ([16][BM+pad]); each lane feeds the
 // 32x32x2 MFMA with one ds_read_b32 per operand, which is conflict-free.  Small GEMM
 // grids are split along K into fp32 slabs that a deterministic reduce kernel sums.
+#include <atomic>
 #include "conv_kernels.hpp"
 #include <cstdlib>
 #include <mutex>
@@ -220,6 +221,11 @@ struct TimingState {
 };
 static TimingState g_timing;
 
+// Process-wide conv math (adaptseg_conv_set_math): 0 = fp32 MFMA, 1 = bf16 MFMA.  Global, not
+// thread-local: autograd runs backward on its own worker thread.
+static std::atomic<int> g_conv_math{0};
+int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
+
 static void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
   *slot = -1;
   if (!g_timing.enabled) return;
@@ -304,9 +310,9 @@ double conv_flops(const adaptseg_conv_desc *d) {
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  const int bm = kCfgBM[pl.cfg], bn = kCfgBN[pl.cfg];
-  pl.bk = pl.fast ? fast_bk(pl.cfg) : BK;
-  if (!pl.fast) pl.s2 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = false;
+  const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg], bn = pl.bf16 ? 128 : kCfgBN[pl.cfg];
+  pl.bk = pl.bf16 ? 64 : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
     p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
@@ -333,6 +339,7 @@ void set_splits(Plan &pl) {
   p.splits = splits;
   p.ktiles_per_split = per;
   pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
+  if (pl.bf16) pl.slab_bytes += (bf16_wpack_bytes(pl) + 255) / 256 * 256;
 }
 
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
@@ -397,11 +404,20 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     pl.ae = d->k % 4 != 0;
     pl.be = !(nhwc_in && d->c % 4 == 0);
   }
+  // bf16 conv math: the vector FAST cases whose K tiles of 64 stay inside one tap
+  pl.bf16 = false;
+  if (conv_math() == 1 && pl.fast && !pl.ae && !pl.be) {
+    if (op == ADAPTSEG_CONV_FWD) pl.bf16 = d->c % 64 == 0;
+    else if (op == ADAPTSEG_CONV_BWD_DATA) pl.bf16 = d->k % 64 == 0;
+    else pl.bf16 = true;
+  }
+  if (pl.bf16) pl.cfg = 0;
   set_splits(pl);
   return ADAPTSEG_OK;
 }
 
 int kernel_id(const Plan &pl, int mode) {
+  if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0);
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)
   if (pl.fast) return 100 * mode + 10 * pl.cfg + 4 + (pl.s2 ? 4 : 0) + (pl.ae ? 2 : 0) + (pl.be ? 1 : 0);
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
@@ -409,7 +425,7 @@ int kernel_id(const Plan &pl, int mode) {
 
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
-  if (pl.p.splits > 1) {
+  if (pl.p.splits > 1 && !pl.bf16) {
     if (!ws || ws_bytes < pl.slab_bytes) {
       set_error("conv: workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
@@ -418,11 +434,24 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   }
   hipError_t e;
   int slot;
+  if (pl.bf16) {  // [bf16 weight pack][slabs]
+    const size_t wb = (bf16_wpack_bytes(pl) + 255) / 256 * 256;
+    if (!ws || ws_bytes < pl.slab_bytes) {
+      set_error("conv (bf16): workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
+      return ADAPTSEG_ERR_WORKSPACE;
+    }
+    if (pl.p.splits > 1) pl.p.out = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + wb);
+    timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
+    e = launch_bf16(pl, ws, s);
+    timing_end(slot, s);
+    ws = reinterpret_cast<char *>(ws) + wb;  // the reduce below reads the slabs
+  } else {
   timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
   if (mode == MODE_FWD) e = launch_fwd(pl, s);
   else if (mode == MODE_DGRAD) e = launch_dgrad(pl, s);
   else e = launch_wgrad(pl, s);
   timing_end(slot, s);
+  }
   if (e != hipSuccess) {
     set_error("igemm launch: %s", hipGetErrorString(e));
     return ADAPTSEG_ERR_HIP;
@@ -649,6 +678,18 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
       AS_CHECK_LAUNCH("bias_grad_final");
     }
   }
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv_set_math(int math) {
+  AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16, "conv_set_math: bad math %d", math);
+  g_conv_math.store(math);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv_get_math(int *math) {
+  AS_CHECK_ARG(math, "conv_get_math: null");
+  *math = g_conv_math.load();
   return ADAPTSEG_OK;
 }
 

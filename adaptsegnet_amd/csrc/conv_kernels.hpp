@@ -623,6 +623,162 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
   dx = kw * dil - pad;
 }
 
+// Epilogue shared by the fp32 (igemm_fast_kernel) and bf16 (igemm_bf16_kernel) MFMA paths:
+// both accumulate 32x32 tiles whose C layout is row = (r&3) + 8*(r>>2) + 4*(lane>>5),
+// col = lane&31 (dtype-independent on gfx950).  Split-K slabs, the weight-gradient store
+// (per segment, optional accumulate) and the fwd / data-grad epilogue (bias, accumulate,
+// residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
+// `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2>
+__device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
+                                               int bm, int bn, int tm, int tn, int split, int M, int Hc,
+                                               int Wc, int py, int px, float *lds) {
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const bool full = (bm + BM <= M) && (bn + BN <= p.N);
+  // output row of GEMM row `row` (S2: scatter the parity class back into the NHWC image)
+  auto out_row = [&](int row) -> size_t {
+    if constexpr (S2) {
+      const int j = row % Wc, t2 = row / Wc;
+      const int ii = t2 % Hc, b = t2 / Hc;
+      return ((size_t)(b * p.h + 2 * ii + py) * p.w + 2 * j + px);
+    } else {
+      return (size_t)row;
+    }
+  };
+  if (p.splits > 1) {
+    float *slab = p.out + (size_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = bn + wn * WTN + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (full || (row < p.M && col < p.N)) slab[(size_t)row * p.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == MODE_WGRAD) {
+    const bool accum = p.flags & ADAPTSEG_EPI_ACCUMULATE;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = bn + wn * WTN + j * 32 + l32;
+      if (!full && col >= p.N) continue;
+      const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
+      const int cc = col - seg * p.kseg;
+      float *dst = (seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3]) + cc;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!full && row >= p.M) continue;
+          float *o = dst + (size_t)row * p.kseg;
+          const float v = acc[i][j][r];
+          *o = accum ? *o + v : v;
+        }
+    }
+  } else {
+    const int flags = p.flags;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = bn + wn * WTN + j * 32 + l32;
+      if (!full && col >= p.N) continue;
+      float bsum = 0.f;
+      if constexpr (MODE == MODE_FWD) {
+        for (int s = 0; s < p.nseg; ++s) {
+          const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
+          if (bp) bsum += bp[col];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (!full && row >= M) continue;
+          const size_t idx = out_row(row) * p.N + col;
+          float v = acc[i][j][r] + bsum;
+          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
+          if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
+          v = epi_act(v, flags);
+          if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
+          p.out[idx] = v;
+        }
+    }
+    if constexpr (MODE == MODE_FWD && !S2) {
+      // BatchNorm statistics of this row tile, straight from the accumulators (the BN that
+      // consumes this conv then skips its statistics pass over y): per column the tile's
+      // mean and sum of squared deviations (two passes over registers, Chan-mergeable in fp64
+      // by bn_fwd_train_tiles).  Only with flags == 0 and no bias: y == acc.
+      if (p.stats) {
+        __syncthreads();  // the LDS stages are free (the main loop ended on a barrier)
+        float *red = lds;  // [WAVES_M][BN]
+        const int nvalid = min(BM, M - bm);
+        float mean[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              s += rl < nvalid ? acc[i][j][r] : 0.f;
+            }
+          s += __shfl_xor(s, 32);
+          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < WAVES_M; ++q) s += red[q * BN + wn * WTN + j * 32 + l32];
+          mean[j] = s / (float)nvalid;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              const float dv = acc[i][j][r] - mean[j];
+              s += rl < nvalid ? dv * dv : 0.f;
+            }
+          s += __shfl_xor(s, 32);
+          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
+        }
+        __syncthreads();
+        const int nt = p.stats_ntiles;
+        if (wm == 0 && hh == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = bn + wn * WTN + j * 32 + l32;
+            if (col >= p.N) continue;
+            float m2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < WAVES_M; ++q) m2 += red[q * BN + wn * WTN + j * 32 + l32];
+            p.stats[nt + (size_t)col * nt + tm] = mean[j];
+            p.stats[nt + ((size_t)p.N + col) * nt + tm] = m2;
+          }
+        }
+        if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
+      }
+    }
+  }
+}
+
 template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool S2, bool AE, bool BE>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(const ConvParams p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;  // threads per block (4 or 8 waves)
@@ -1059,144 +1215,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(cons
   }
 
   // ---- epilogue ----
-  const bool full = (bm + BM <= M) && (bn + BN <= p.N);
-  // output row of GEMM row `row` (S2: scatter the parity class back into the NHWC image)
-  auto out_row = [&](int row) -> size_t {
-    if constexpr (S2) {
-      const int j = row % Wc, t2 = row / Wc;
-      const int ii = t2 % Hc, b = t2 / Hc;
-      return ((size_t)(b * p.h + 2 * ii + py) * p.w + 2 * j + px);
-    } else {
-      return (size_t)row;
-    }
-  };
-  if (p.splits > 1) {
-    float *slab = p.out + (size_t)split * p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = bn + wn * WTN + j * 32 + l32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (full || (row < p.M && col < p.N)) slab[(size_t)row * p.N + col] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  if constexpr (MODE == MODE_WGRAD) {
-    const bool accum = p.flags & ADAPTSEG_EPI_ACCUMULATE;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = bn + wn * WTN + j * 32 + l32;
-      if (!full && col >= p.N) continue;
-      const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
-      const int cc = col - seg * p.kseg;
-      float *dst = (seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3]) + cc;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (!full && row >= p.M) continue;
-          float *o = dst + (size_t)row * p.kseg;
-          const float v = acc[i][j][r];
-          *o = accum ? *o + v : v;
-        }
-    }
-  } else {
-    const int flags = p.flags;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = bn + wn * WTN + j * 32 + l32;
-      if (!full && col >= p.N) continue;
-      float bsum = 0.f;
-      if constexpr (MODE == MODE_FWD) {
-        for (int s = 0; s < p.nseg; ++s) {
-          const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
-          if (bp) bsum += bp[col];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (!full && row >= M) continue;
-          const size_t idx = out_row(row) * p.N + col;
-          float v = acc[i][j][r] + bsum;
-          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
-          if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
-          v = epi_act(v, flags);
-          if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
-          p.out[idx] = v;
-        }
-    }
-    if constexpr (MODE == MODE_FWD && !S2) {
-      // BatchNorm statistics of this row tile, straight from the accumulators (the BN that
-      // consumes this conv then skips its statistics pass over y): per column the tile's
-      // mean and sum of squared deviations (two passes over registers, Chan-mergeable in fp64
-      // by bn_fwd_train_tiles).  Only with flags == 0 and no bias: y == acc.
-      if (p.stats) {
-        __syncthreads();  // the LDS stages are free (the main loop ended on a barrier)
-        float *red = lds;  // [WAVES_M][BN]
-        const int nvalid = min(BM, M - bm);
-        float mean[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float s = 0.f;
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              s += rl < nvalid ? acc[i][j][r] : 0.f;
-            }
-          s += __shfl_xor(s, 32);
-          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float s = 0.f;
-#pragma unroll
-          for (int q = 0; q < WAVES_M; ++q) s += red[q * BN + wn * WTN + j * 32 + l32];
-          mean[j] = s / (float)nvalid;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float s = 0.f;
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              const float dv = acc[i][j][r] - mean[j];
-              s += rl < nvalid ? dv * dv : 0.f;
-            }
-          s += __shfl_xor(s, 32);
-          if (hh == 0) red[wm * BN + wn * WTN + j * 32 + l32] = s;
-        }
-        __syncthreads();
-        const int nt = p.stats_ntiles;
-        if (wm == 0 && hh == 0) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = bn + wn * WTN + j * 32 + l32;
-            if (col >= p.N) continue;
-            float m2 = 0.f;
-#pragma unroll
-            for (int q = 0; q < WAVES_M; ++q) m2 += red[q * BN + wn * WTN + j * 32 + l32];
-            p.stats[nt + (size_t)col * nt + tm] = mean[j];
-            p.stats[nt + ((size_t)p.N + col) * nt + tm] = m2;
-          }
-        }
-        if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
-      }
-    }
-  }
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
 }
 
 
@@ -1206,11 +1225,12 @@ struct Plan {
   bool va, vb;
   bool fast;
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
+  bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x128x64 tiles, packed bf16 weights
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
   int mode;
   int tiles;
-  size_t slab_bytes;
+  size_t slab_bytes;  // workspace need: [bf16 weight pack, 256-B aligned] + split-K slabs
   double flops;  // algorithmic FLOPs of the conv product this plan computes
 };
 
@@ -1243,6 +1263,10 @@ int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float
                        int flags, void *ws, size_t ws_bytes, hipStream_t s);
 
 hipError_t launch_fwd(const Plan &pl, hipStream_t s);
+// bf16 conv math (adaptseg_conv_set_math): weight-pack bytes and launcher (conv_launch_bf16.hip)
+int conv_math();
+size_t bf16_wpack_bytes(const Plan &pl);
+hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s);
 hipError_t launch_dgrad(const Plan &pl, hipStream_t s);
 hipError_t launch_wgrad(const Plan &pl, hipStream_t s);
 

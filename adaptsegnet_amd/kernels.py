@@ -15,10 +15,11 @@ import torch
 
 from . import _lib
 from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
-                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, ConvDesc, check)
+                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_F32,
+                   ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
@@ -96,10 +97,25 @@ class ConvGeom:
 
 
 _DESC_CACHE: dict = {}
+_CONV_MATH = [MATH_F32]
+
+
+def set_conv_math(math: int) -> None:
+    """Process-wide conv arithmetic: MATH_F32 (fp32 MFMA, default) or MATH_BF16 (operands
+    rounded to bf16, fp32 accumulate: BASELINE config c5).  Workspace sizes depend on it,
+    so the descriptor cache is keyed on it."""
+    check(_lib.lib().adaptseg_conv_set_math(int(math)), "conv_set_math")
+    _CONV_MATH[0] = int(math)
+
+
+def get_conv_math() -> int:
+    m = ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv_get_math(ctypes.byref(m)), "conv_get_math")
+    return m.value
 
 
 def _desc(g: ConvGeom, n, h, w, strides):
-    key = (g, n, h, w, strides)
+    key = (g, n, h, w, strides, _CONV_MATH[0])
     d = _DESC_CACHE.get(key)
     if d is None:
         oh, ow = g.out_hw(h, w)

@@ -69,6 +69,17 @@ enum adaptseg_conv_flags {
   ADAPTSEG_EPI_RELU_GRAD = 32  /* bwd_data: dx *= (aux > 0 ? 1 : 0)                        */
 };
 
+/* Conv arithmetic, process-wide (set before sizing workspaces; every conv entry point and
+   *_workspace_size() reads it).  F32: fp32 MFMA, exact fp32 products (default).  BF16: the
+   operands of each product are rounded to bf16 (RNE) as they are staged into LDS and
+   multiplied on v_mfma_f32_32x32x16_bf16 with fp32 accumulation — torch.autocast(bfloat16)
+   conv semantics; activations, gradients and epilogues stay fp32 (BASELINE config c5).
+   Products the bf16 kernel does not cover (Cin or Cout not a multiple of 64 for the forward /
+   data-gradient, per-element operands) stay on the fp32 path. */
+enum adaptseg_conv_math { ADAPTSEG_MATH_F32 = 0, ADAPTSEG_MATH_BF16 = 1 };
+int adaptseg_conv_set_math(int math);
+int adaptseg_conv_get_math(int *math);
+
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
 /* Kernel selector (see adaptseg_timing_enable) and K-split count the library would use. */
 int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_id, int *splits);
@@ -244,7 +255,8 @@ int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream)
 /* back after a device synchronise.  selector = -1: every igemm launch; otherwise           */
 /* selector = 100*op + 10*tile + variant names ONE kernel symbol: op 0 fwd, 1 bwd-data,     */
 /* 2 bwd-weight; tile 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256, 4 = 256x64;          */
-/* variant 0..3 = generic gather (2*vecA + vecB), 4 = FAST, 5 = FAST stride-2 parity path.   */
+/* variant 0..3 = generic gather (2*vecA + vecB), 4 = FAST, 5 = FAST stride-2 parity path;    */
+/* tile 9 = the bf16-MFMA kernel (128x128x64), variant 0 / 1 (stride-2 parity path).         */
 /* ------------------------------------------------------------------------------------ */
 int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);

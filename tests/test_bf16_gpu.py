@@ -1,0 +1,145 @@
+"""GPU parity of the bf16-MFMA conv path (adaptseg_conv_set_math(BF16), BASELINE config c5).
+
+Semantics (torch.autocast(bfloat16) conv): each product's two operands are rounded to bf16
+(round-to-nearest-even), multiplied exactly and accumulated in fp32.  The oracle therefore
+rounds the same operands to bf16 on the host and convolves them in fp64, so the only
+remaining difference is fp32 accumulation order: max|err| <= 2e-5 * max|ref| (as the fp32
+path).  Against the UNROUNDED fp64 conv the error is the bf16 input rounding itself
+(~2^-9 relative per operand), checked loosely (<= 2e-2) to show the result is a conv at all.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+# (n, cin, h, w, cout, k, stride, pads, dils, bias) — shapes the bf16 kernel covers
+BF16_CASES = [
+    (2, 64, 17, 23, 256, 1, 1, (0,), (1,), False),       # 1x1, M and N tails
+    (2, 256, 17, 23, 128, 1, 2, (0,), (1,), False),      # stride-2 1x1 (dgrad parity classes)
+    (2, 64, 15, 21, 64, 3, 1, (1,), (1,), False),        # 3x3, N = 64 < tile
+    (2, 128, 13, 11, 128, 3, 1, (2,), (2,), False),      # atrous d2
+    (1, 256, 9, 12, 256, 3, 1, (4,), (4,), False),       # atrous d4
+    (2, 64, 16, 20, 128, 4, 2, (1,), (1,), True),        # D conv2 (4x4/2, bias)
+    (2, 128, 7, 9, 64, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP segments
+    (1, 2048, 3, 5, 64, 1, 1, (0,), (1,), False),        # split-K (M = 15, K = 2048)
+    (2, 64, 31, 33, 192, 3, 2, (1,), (1,), False),       # stride-2 3x3, odd sizes
+    (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),         # wgrad, many K splits
+]
+
+
+def K():
+    from adaptsegnet_amd import kernels
+    return kernels
+
+
+@pytest.fixture
+def bf16_math():
+    k = K()
+    k.set_conv_math(k.MATH_BF16)
+    yield k
+    k.set_conv_math(k.MATH_F32)
+
+
+def bf(t):
+    return t.to(torch.bfloat16).double()
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).double().cpu()
+
+
+def _ref(x, ws, bs, stride, pads, dils):
+    out = None
+    for i, (p, d) in enumerate(zip(pads, dils)):
+        y = F.conv2d(x, ws[i], bs[i] if bs is not None else None, stride, p, d)
+        out = y if out is None else out + y
+    return out
+
+
+@pytest.mark.parametrize("case", BF16_CASES, ids=[f"b{i}" for i in range(len(BF16_CASES))])
+def test_bf16_conv_products(case, bf16_math):
+    k = bf16_math
+    n, cin, h, w, cout, ks, stride, pads, dils, bias = case
+    g = torch.Generator().manual_seed(1000 + BF16_CASES.index(case))
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    nseg = len(pads)
+    ws = [torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.1 for _ in range(nseg)]
+    bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in range(nseg)] if bias else None
+    geom = k.ConvGeom(cin, cout, ks, ks, stride, pads, dils)
+    oh, ow = geom.out_hw(h, w)
+    gy = torch.randn(n, cout, oh, ow, generator=g, dtype=torch.float64)
+
+    # the bf16 kernel must be the one selected (kernel id 100*op + 90 + s2)
+    for op in (0, 1, 2):
+        kid, _ = k.conv_kernel_id(geom, n, h, w, op)
+        assert kid // 10 % 10 == 9, (op, kid)
+
+    xd, gyd = nhwc(x), nhwc(gy)
+    wd = [t.permute(0, 2, 3, 1).contiguous().float().to(DEV) for t in ws]
+    bd = [t.float().to(DEV) for t in bs] if bias else None
+
+    # forward: bf16(x) * bf16(w)
+    y = nchw(k.conv_fwd(geom, xd, n, h, w, wd, bd))
+    ref = _ref(bf(x), [bf(t) for t in ws], bs, stride, pads, dils)
+    assert rel(y, ref) < 2e-5
+    assert rel(y, _ref(x, ws, bs, stride, pads, dils)) < 2e-2
+
+    # data gradient: bf16(dy) * bf16(w)
+    xr = bf(x).requires_grad_(True)
+    _ref(xr, [bf(t) for t in ws], None, stride, pads, dils).backward(bf(gy))
+    dx = nchw(k.conv_dgrad(geom, gyd, n, h, w, wd))
+    assert rel(dx, xr.grad) < 2e-5
+
+    # weight gradient: bf16(dy) * bf16(x); bias gradient stays an fp32 sum of dy
+    wr = [bf(t).requires_grad_(True) for t in ws]
+    _ref(bf(x), wr, None, stride, pads, dils).backward(bf(gy))
+    dws = [torch.zeros_like(t) for t in wd]
+    dbs = [torch.zeros(cout, device=DEV) for _ in range(nseg)] if bias else None
+    k.conv_wgrad(geom, gyd, xd, n, h, w, dws, dbs, accumulate=False)
+    for i in range(nseg):
+        assert rel(dws[i].permute(0, 3, 1, 2).cpu(), wr[i].grad) < 2e-5
+        if bias:
+            assert rel(dbs[i].cpu(), gy.sum((0, 2, 3))) < 1e-5
+
+
+def test_bf16_fused_bn_statistics(bf16_math):
+    """The bf16 forward also emits the per-row-tile BN statistics of its output."""
+    k = bf16_math
+    n, cin, h, w, cout = 4, 128, 64, 72, 256   # 288 tiles: no K split, so statistics are fused
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.1
+    geom = k.ConvGeom(cin, cout, 3, 3, 1, (1,), (1,))
+    y, st = k.conv_fwd_bnstats(geom, nhwc(x), n, h, w, [wt.permute(0, 2, 3, 1).contiguous().float().to(DEV)])
+    assert st is not None
+    ref = F.conv2d(bf(x), bf(wt), None, 1, 1)
+    assert rel(nchw(y), ref) < 2e-5
+    stats, nt = st
+    s = stats.double().cpu()
+    cnt = s[:nt]
+    means = s[nt:nt + cout * nt].view(cout, nt)
+    mean = (means * cnt).sum(1) / cnt.sum()
+    assert rel(mean, ref.mean((0, 2, 3))) < 1e-4
+
+
+def test_bf16_math_is_process_wide_and_default_off():
+    k = K()
+    assert k.get_conv_math() == k.MATH_F32
+    geom = k.ConvGeom(64, 64, 3, 3, 1, (1,), (1,))
+    kid, _ = k.conv_kernel_id(geom, 2, 16, 16, 0)
+    assert kid // 10 % 10 != 9
+    with pytest.raises(RuntimeError):
+        k.set_conv_math(7)
