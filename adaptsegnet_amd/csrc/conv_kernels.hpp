@@ -593,7 +593,10 @@ __device__ __forceinline__ SegRegs seg_regs(const ConvParams &p) {
   SegRegs r;
   r.dilpack = __builtin_amdgcn_readfirstlane(p.dil_[0] | (p.dil_[1] << 8) | (p.dil_[2] << 16) | (p.dil_[3] << 24));
   r.padpack = __builtin_amdgcn_readfirstlane(p.pad_[0] | (p.pad_[1] << 8) | (p.pad_[2] << 16) | (p.pad_[3] << 24));
-  const uint64_t w = (uint64_t)p.wt[threadIdx.x & 3];
+  // lane s < 4 <- p.wt[s] through a select: a per-lane dynamic index into the kernarg struct
+  // makes the compiler copy the whole ConvParams to scratch and turn every load flat
+  const int l3 = threadIdx.x & 3;
+  const uint64_t w = (uint64_t)(l3 == 0 ? p.wt[0] : l3 == 1 ? p.wt[1] : l3 == 2 ? p.wt[2] : p.wt[3]);
   r.wlo = (uint32_t)w;
   r.whi = (uint32_t)(w >> 32);
   return r;

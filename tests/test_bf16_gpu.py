@@ -143,3 +143,31 @@ def test_bf16_math_is_process_wide_and_default_off():
     assert kid // 10 % 10 != 9
     with pytest.raises(RuntimeError):
         k.set_conv_math(7)
+
+
+def test_c5_multilevel_ls_step_bf16(bf16_math):
+    """Config c5's step (multi-level, LS-GAN) with bf16 conv math, eval-mode BN (well
+    conditioned) against the fp64 oracle: every loss of 3 iterations within 2e-2 relative
+    (bf16 operand rounding, ~2^-9 per operand, through ~100 layers), and the generator's
+    parameter update within cosine 0.99 of the fp64 update.  The per-product semantics are
+    pinned tightly by test_bf16_conv_products; this checks the whole program runs on them."""
+    import os
+    from test_model_gpu import _oracle_run, _run_hip, _groups, _updates, frob, R
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    xs = torch.from_numpy(R.det_images((2, 3, 41, 57), 11))
+    lab = torch.from_numpy(R.det_labels((2, 41, 57), 12))
+    xt = torch.from_numpy(R.det_images((2, 3, 33, 49), 13))
+    data = (xs, lab, xt)
+    cfg = dict(level="multi-level", gan="LS", input_size=(57, 41), input_size_target=(49, 33))
+    G, _, _, ref = _oracle_run("multi-level", "LS", cfg, data, torch.float64, 3, bn_train=False)
+    m, _, _, got = _run_hip("multi-level", "LS", cfg, data, 3, bn_train=False)
+    for it in range(3):
+        for key, v in ref[it].items():
+            print(f"bf16 iter{it} {key}: hip={got[it][key]:.6f} fp64={v:.6f}")
+            assert abs(got[it][key] - v) <= 2e-2 * abs(v) + 1e-6, (it, key, got[it][key], v)
+    g0 = R.det_state(R.g_specs(), 1338)
+    sd = m.state_dict()
+    for gname, keys in _groups(G, "multi-level").items():
+        f, c = frob(_updates(None, keys, g0, sd), _updates(G, keys, g0))
+        print(f"bf16 {gname} update: rel-frob {f:.3e} cos {c:.6f}")
+        assert c >= 0.99, (gname, f, c)

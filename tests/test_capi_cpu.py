@@ -1,5 +1,8 @@
 """CPU: the C-ABI library loads (no GPU needed) and exports every symbol include/adaptseg.h declares."""
 import ctypes
+import os
+
+import pytest
 
 from adaptsegnet_amd import _lib
 
@@ -39,3 +42,33 @@ def test_workspace_and_kernel_selection_on_host():
     d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))  # D classifier: stride 2 keeps the direct GEMM
     kid, _ = K.conv_kernel_id(d5, 4, 32, 64, 0)
     assert (kid // 10) % 10 == 1              # skinny-N tile (256x32)
+
+
+def test_kernels_use_no_scratch(tmp_path):
+    """Every gfx950 kernel in libadaptseg.so runs without private (scratch) memory.  A kernel
+    that indexes its ConvParams argument per lane gets the whole struct copied to scratch and
+    every global load turned into a flat load (that once cost the fp32 forward conv 40 %)."""
+    import re
+    import shutil
+    import subprocess
+    from adaptsegnet_amd import _lib
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (os.path.exists(objdump) and os.path.exists(readelf)):
+        pytest.skip("ROCm LLVM tools not available")
+    so = tmp_path / "lib.so"
+    shutil.copy(_lib.LIB_PATH, so)
+    subprocess.run([objdump, "--offloading", str(so)], check=True, capture_output=True, cwd=tmp_path)
+    cos = sorted(tmp_path.glob("lib.so.*gfx950"))
+    assert cos, "no gfx950 code object in the library"
+    seen = 0
+    for co in cos:
+        notes = subprocess.run([readelf, "--notes", str(co)], check=True, capture_output=True,
+                               text=True).stdout
+        names = re.findall(r"\.name:\s+(\S+)", notes)
+        sizes = [int(v) for v in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+        assert len(names) == len(sizes)
+        bad = [n for n, s in zip(names, sizes) if s != 0]
+        assert not bad, f"kernels using scratch: {bad}"
+        seen += len(names)
+    assert seen > 50
