@@ -86,6 +86,12 @@ _SIGS = {
     "adaptseg_to_nhwc": [_I, _I, _I, _I, ctypes.POINTER(_L), _P, _P, _P],
     "adaptseg_axpy": [_L, _F, _P, _P, _I, _P],
     "adaptseg_add_i64": [_P, _L, _L, _P],
+    "adaptseg_conv2d_bnsums_size": [_DESC, ctypes.POINTER(_SZ)],
+    "adaptseg_conv2d_bwd_data_bnsums": [_DESC, _P, _PP, _P, _P, _P, _P, _P, _P, _P, _SZ,
+                                        ctypes.POINTER(_I), _P, _SZ, _P],
+    "adaptseg_bn_bwd_tiles": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "adaptseg_preprocess_workspace_size": [_I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],
+    "adaptseg_gta5_preprocess": [_I, _I, _I, _I, _I, _P, _F, _F, _F, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],

@@ -386,6 +386,23 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
   return ADAPTSEG_OK;
 }
 
+int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles, const float *dy,
+                          const float *x, const float *weight, const float *bias, const float *save_mean,
+                          const float *save_invstd, float *coef, float *dx, float *dres,
+                          adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd_tiles: C%%4==0 required");
+  AS_CHECK_ARG(partial && ntiles > 0 && dy && x && save_mean && save_invstd && coef && dx,
+               "bn_bwd_tiles: null pointer");
+  hipStream_t s = as_stream(stream);
+  bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, ntiles, partial, save_invstd, coef);
+  AS_CHECK_LAUNCH("bn_bwd_final");
+  int64_t total4 = rows * c / 4;
+  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, nullptr, x, weight, bias, save_mean,
+                                                       save_invstd, coef, dx, dres, 2, 1);
+  AS_CHECK_LAUNCH("bn_bwd_apply");
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
                     int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {

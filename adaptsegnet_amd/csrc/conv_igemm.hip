@@ -633,6 +633,57 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
 }
 
+int adaptseg_conv2d_bnsums_size(const adaptseg_conv_desc *d, size_t *bytes) {
+  AS_CHECK_ARG(bytes, "conv2d_bnsums_size: null");
+  int st = validate(d);
+  if (st) return st;
+  // data-gradient rows = input pixels; the smallest row tile any config uses (128)
+  const int64_t nt = ceil_div((int64_t)d->n * d->h * d->w, 128);
+  *bytes = (size_t)(2 * (int64_t)d->c * nt) * sizeof(float);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_bwd_data_bnsums(const adaptseg_conv_desc *d, const float *dy, const float *const *w, float *dx,
+                                    const float *bn_x, const float *bn_mean, const float *bn_invstd,
+                                    const float *bn_weight, const float *bn_bias, float *partial,
+                                    size_t partial_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                    adaptseg_stream_t stream) {
+  AS_CHECK_ARG(ntiles && partial && bn_x && bn_mean && bn_invstd, "conv bwd_data_bnsums: null BN argument");
+  *ntiles = 0;
+  Plan pl;
+  int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
+  if (st) return st;
+  AS_CHECK_ARG(dy && w && dx, "conv bwd_data_bnsums: null pointer");
+  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data_bnsums: null weight %d", s);
+  if (tapgemm_eligible(d))  // no fused sums on the tap-GEMM path: plain data gradient
+    return adaptseg_conv2d_bwd_data(d, dy, w, nullptr, nullptr, dx, 0, ws, ws_bytes, stream);
+  ConvParams &p = pl.p;
+  p.dy = dy;
+  for (int s = 0; s < d->nseg; ++s) {
+    p.wt[s] = w[s];
+    if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
+  }
+  if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
+  set_splits(pl);
+  p.out = dx;
+  p.flags = 0;
+  if (pl.fast && !pl.s2 && p.splits == 1) {
+    const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg];
+    const int nt = (int)ceil_div(p.M, bm);
+    if ((size_t)(2 * (int64_t)p.N * nt) * sizeof(float) <= partial_bytes) {
+      p.bnsum = partial;
+      p.stats_ntiles = nt;
+      p.bn_x = bn_x;
+      p.bn_mean = bn_mean;
+      p.bn_invstd = bn_invstd;
+      p.bn_w = bn_weight;
+      p.bn_b = bn_bias;
+      *ntiles = nt;
+    }
+  }
+  return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
+}
+
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
                                float *const *dw, float *const *db, int flags, void *ws,
                                size_t ws_bytes, adaptseg_stream_t stream) {

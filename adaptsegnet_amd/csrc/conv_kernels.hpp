@@ -56,6 +56,10 @@ struct ConvParams {
   FastDiv fd_taps, fd_kw;
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
+  // DGRAD (splits == 1, stride 1, no epilogue flags) feeding a train-mode BN+ReLU backward:
+  // per-row-tile sums of g = dx*[bn_affine(bn_x) > 0] and g*(bn_x - mean) -> bnsum[2][N][nt]
+  float *bnsum;
+  const float *bn_x, *bn_mean, *bn_invstd, *bn_w, *bn_b;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
 
@@ -777,6 +781,59 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
           }
         }
         if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
+      }
+    }
+    if constexpr (MODE == MODE_DGRAD && !S2) {
+      // BatchNorm(+ReLU) backward sums of this row tile (the BN whose output this data
+      // gradient is, model/deeplab_multi.py:65-98 bn1/bn2): g = dx * [relu'(bn(x))] with the
+      // ReLU mask recomputed from the BN input x, s1 = sum g, s2 = sum g * (x - mean).  The BN
+      // backward then skips its reduction pass over dx and x (bn_bwd_tiles).
+      if (p.bnsum) {
+        __syncthreads();
+        float *red = lds;  // [2][WAVES_M][BN]
+        const int nvalid = min(BM, M - bm);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = bn + wn * WTN + j * 32 + l32;
+          const int cc = min(col, p.N - 1);
+          const float mu = p.bn_mean[cc], is = p.bn_invstd[cc];
+          const float bw = p.bn_w ? p.bn_w[cc] : 1.f, bb = p.bn_b ? p.bn_b[cc] : 0.f;
+          float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              const bool ok = rl < nvalid && col < p.N;
+              const float xv = ok ? p.bn_x[(size_t)(bm + rl) * p.N + col] : 0.f;
+              const float g = (ok && (xv - mu) * is * bw + bb > 0.f) ? acc[i][j][r] : 0.f;
+              s1 += g;
+              s2 += g * (xv - mu);
+            }
+          s1 += __shfl_xor(s1, 32);
+          s2 += __shfl_xor(s2, 32);
+          if (hh == 0) {
+            red[wm * BN + wn * WTN + j * 32 + l32] = s1;
+            red[(WAVES_M + wm) * BN + wn * WTN + j * 32 + l32] = s2;
+          }
+        }
+        __syncthreads();
+        const int nt = p.stats_ntiles;
+        if (wm == 0 && hh == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = bn + wn * WTN + j * 32 + l32;
+            if (col >= p.N) continue;
+            float a = 0.f, b = 0.f;
+#pragma unroll
+            for (int q = 0; q < WAVES_M; ++q) {
+              a += red[q * BN + wn * WTN + j * 32 + l32];
+              b += red[(WAVES_M + q) * BN + wn * WTN + j * 32 + l32];
+            }
+            p.bnsum[(size_t)col * nt + tm] = a;
+            p.bnsum[((size_t)p.N + col) * nt + tm] = b;
+          }
+        }
       }
     }
   }

@@ -17,8 +17,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
     const int64_t n = (int64_t)p.k * p.nseg * p.kseg;
     conv_wpack_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, s>>>(p, wb);
   } else if (pl.mode == MODE_DGRAD) {
-    const int64_t n = (int64_t)p.c * p.ntaps * p.k;
-    conv_wpack_dgrad_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, s>>>(p, wb);
+    dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
+    conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

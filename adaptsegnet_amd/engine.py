@@ -87,10 +87,14 @@ def bn_forward(bn, x, res, relu, training, tiles=None):
     return y, (bn.running_mean, None, False)
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, sums=None):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
-    mode instead of reading the saved output y (one activation read less per pass)."""
+    mode instead of reading the saved output y (one activation read less per pass).
+    sums: the row-tile backward sums fused into the producing data-gradient conv
+    (_dgrad_into_bn), which replace the BN's own reduction pass."""
     mean, invstd, train = st
+    if sums is not None:
+        return K.bn_bwd_tiles(dy, x, bn.weight, bn.bias, mean, invstd, sums, dx=dx, dres=dres)
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
     elif mask_from_x and relu:
@@ -154,22 +158,32 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
         ws.launch(run, dy, x)
 
 
+def _dgrad_into_bn(g, dy, n, h, w, weight, bn, bn_x, st):
+    """Data gradient feeding a BN+ReLU backward; with a train-mode BN also its fused sums."""
+    mean, invstd, train = st
+    if not train:
+        return K.conv_dgrad(g, dy, n, h, w, [weight]), None
+    return K.conv_dgrad_bnsums(g, dy, n, h, w, [weight], bn_x, mean, invstd, bn.weight, bn.bias)
+
+
 def block_backward(blk, rec, gout, need_w, ws=None):
     """gout: grad of the block output (owned, modified in place).  Returns grad of the input."""
     n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
     dc3 = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout)
-    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight])
+    # conv3 / conv2 data gradients are the gradients of bn2 / bn1 outputs: their epilogues also
+    # produce those BNs' backward sums (train mode), so the BN backward is finalize + apply.
+    dy2, t2 = _dgrad_into_bn(g3, dc3, n, oh, ow, blk.conv3.weight, blk.bn2, rec.c2, rec.s2)
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
     del dc3
-    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True)
-    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
+    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, sums=t2)
+    dy1, t1 = _dgrad_into_bn(g2, dy2, n, oh, ow, blk.conv2.weight, blk.bn1, rec.c1, rec.s1)
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
     del dy2
-    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True)
+    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, sums=t1)
     if need_w and blk.conv1.weight.grad is not None:
         _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
     if blk.downsample is not None:

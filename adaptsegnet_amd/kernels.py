@@ -19,7 +19,7 @@ from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI
                    ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad_bnsums", "bn_bwd_tiles", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
@@ -198,6 +198,24 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
     return out
 
 
+def conv_dgrad_bnsums(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, bn_x, mean,
+                      invstd, bn_weight, bn_bias):
+    """dx = conv_transpose(dy, w) plus, when the kernel can fuse them, the row-tile sums of the
+    train-mode BN+ReLU backward whose output dx is the gradient of (bn_x: that BN's input):
+    returns (dx, (partial, ntiles)) or (dx, None)."""
+    d, ws, oh, ow = _desc(g, n, h, w, nhwc_strides(n, h, w, g.cin))
+    dx = torch.empty((n, h, w, g.cin), device=dy.device, dtype=torch.float32)
+    sb = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_conv2d_bnsums_size(ctypes.byref(d), ctypes.byref(sb)), "conv2d_bnsums_size")
+    partial = torch.empty(sb.value // 4, device=dy.device, dtype=torch.float32)
+    nt = ctypes.c_int(0)
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
+    check(_lib.lib().adaptseg_conv2d_bwd_data_bnsums(
+        ctypes.byref(d), _p(dy), _ptrs(weights), _p(dx), _p(bn_x), _p(mean), _p(invstd), _p(bn_weight),
+        _p(bn_bias), _p(partial), sb, ctypes.byref(nt), wp, wsz, _stream()), "conv2d_bwd_data_bnsums")
+    return dx, ((partial, nt.value) if nt.value > 0 else None)
+
+
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
                dbs=None, strides=None, accumulate: bool = True) -> None:
     """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy."""
@@ -273,6 +291,20 @@ def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=
     check(_lib.lib().adaptseg_bn_bwd(
         rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx),
         _p(dres), 1 if relu else 0, 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+    return dx
+
+
+def bn_bwd_tiles(dy, x, weight, bias, mean, invstd, sums, dx=None, dres=None):
+    """Train-mode BN+ReLU backward (mask recomputed from x) from the row-tile sums that
+    conv_dgrad_bnsums fused into the data-gradient epilogue.  dx may alias dy."""
+    partial, nt = sums
+    rows, c = dy.numel() // dy.shape[-1], dy.shape[-1]
+    if dx is None:
+        dx = torch.empty_like(dy)
+    coef = torch.empty(2 * c, device=dy.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_bn_bwd_tiles(
+        rows, c, _p(partial), nt, _p(dy), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(coef),
+        _p(dx), _p(dres), _stream()), "bn_bwd_tiles")
     return dx
 
 

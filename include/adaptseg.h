@@ -106,6 +106,20 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream);
 
+/* Data gradient dx of a conv whose input is the output of a train-mode BatchNorm+ReLU
+   (model/deeplab_multi.py:65-98, bn1/bn2 of every Bottleneck), plus the BN backward's
+   reduction straight from the accumulators: per row tile, sum g and sum g*(bn_x - mean) with
+   g = dx * [(bn_x-mean)*invstd*weight + bias > 0], into partial = [2][c][ntiles] for
+   adaptseg_bn_bwd_tiles.  *ntiles = 0 when the chosen kernel cannot fuse them (split-K,
+   stride-2 parity path, unaligned operands, tap-GEMM path): dx is still computed and the caller
+   runs adaptseg_bn_bwd.  No epilogue flags. */
+int adaptseg_conv2d_bnsums_size(const adaptseg_conv_desc *d, size_t *bytes);
+int adaptseg_conv2d_bwd_data_bnsums(const adaptseg_conv_desc *d, const float *dy, const float *const *w, float *dx,
+                                    const float *bn_x, const float *bn_mean, const float *bn_invstd,
+                                    const float *bn_weight, const float *bn_bias, float *partial,
+                                    size_t partial_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                    adaptseg_stream_t stream);
+
 /* dw[seg][k,kh,kw,c] (+)= sum_{n,oh,ow} dy * x_gathered; db[seg][k] (+)= sum dy.
    db may be NULL.  Only ADAPTSEG_EPI_ACCUMULATE is honoured. */
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
@@ -151,6 +165,14 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     const float *save_invstd, float *dx, float *dres, int relu, int train,
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
+/* adaptseg_bn_bwd (train mode, ReLU mask recomputed from x) from the row-tile sums of
+   adaptseg_conv2d_bwd_data_bnsums: a deterministic fp64 finalize into coef [2][c] (caller-
+   owned, 2*c floats), then the same apply pass.  dx may alias dy. */
+int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles, const float *dy,
+                          const float *x, const float *weight, const float *bias, const float *save_mean,
+                          const float *save_invstd, float *coef, float *dx, float *dres,
+                          adaptseg_stream_t stream);
+
 /* ------------------------------------------------------------------------------------ */
 /* Evaluation: evaluate_cityscapes.py:153-169 (interp to 1024x2048 + argmax) and          */
 /* compute_iou.py:15-28 (label_mapping + fast_hist).                                      */
@@ -162,6 +184,20 @@ int adaptseg_upsample_argmax(int n, int c, int h, int w, int oh, int ow, const f
    hist is int64 [ncls][ncls] (accumulated, never cleared). */
 int adaptseg_confusion_hist(int64_t npix, const uint8_t *gt, const int32_t *lut,
                             const uint8_t *pred, int ncls, int64_t *hist, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Input pipeline: GTA5DataSet.__getitem__ after file decode (dataset/gta5_dataset.py:47-71) */
+/* and the target loader's image path (train_gta2cityscapes_multi.py:333-336, 520-523).    */
+/* Bit-exact with Pillow's Image.resize(crop, BICUBIC) / (crop, NEAREST) 8-bit resampler.   */
+/* ------------------------------------------------------------------------------------ */
+int adaptseg_preprocess_workspace_size(int n, int in_h, int in_w, int out_h, int out_w, size_t *bytes);
+/* rgb: [n][in_h][in_w][3] uint8 (decoded RGB).  image: [n][3][out_h][out_w] float32 =
+   BGR(resize_bicubic(rgb)) - (mean_b, mean_g, mean_r) in float32 (image -= IMG_MEAN).
+   label_ids (optional, with labels): [n][in_h][in_w] uint8 class ids -> labels [n][out_h][out_w]
+   int64 = lut[resize_nearest(ids)] (lut: int32[256] id -> trainId; NULL keeps the ids). */
+int adaptseg_gta5_preprocess(int n, int in_h, int in_w, int out_h, int out_w, const uint8_t *rgb, float mean_b,
+                             float mean_g, float mean_r, float *image, const uint8_t *label_ids, const int32_t *lut,
+                             int64_t *labels, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* MaxPool2d (model/deeplab_multi.py:135: kernel 3, stride 2, pad 1, floor mode), NHWC.  */

@@ -388,3 +388,39 @@ def test_to_nhwc_and_axpy():
     c = b.clone()
     k.axpy(0.5, a, c)
     assert torch.allclose(c, b + 0.5 * a)
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1, 1), (4, 64, 128, 136, 256, 3, 2),
+                                   (4, 128, 96, 88, 128, 3, 1), (1, 64, 5, 7, 256, 1, 1)])
+@pytest.mark.parametrize("math", ["f32", "bf16"])
+def test_conv_dgrad_fused_bn_backward_sums(shape, math):
+    """conv_dgrad_bnsums + bn_bwd_tiles (BN backward reduction fused into the data-gradient
+    epilogue) == conv_dgrad + bn_bwd with the ReLU mask recomputed from x; the last shape is
+    split along K on the fp32 path, which cannot fuse and must report ntiles = 0.  Tolerance 1e-5 rel (the
+    fused path sums the same terms in row-tile order)."""
+    k = K()
+    n, cin, h, w, cout, ks, dil = shape
+    k.set_conv_math(k.MATH_BF16 if math == "bf16" else k.MATH_F32)
+    try:
+        g = torch.Generator().manual_seed(17)
+        geom = k.ConvGeom(cin, cout, ks, ks, 1, ((ks // 2) * dil,), (dil,))
+        dy = nhwc(torch.randn(n, cout, h, w, generator=g, dtype=torch.float64))
+        wt = w_cl(torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.05)
+        bx = nhwc(torch.randn(n, cin, h, w, generator=g, dtype=torch.float64) * 2 + 0.3)
+        bw = (torch.rand(cin, generator=g) + 0.5).float().to(DEV)
+        bb = (torch.randn(cin, generator=g) * 0.2).float().to(DEV)
+        rm = torch.zeros(cin, device=DEV)
+        rv = torch.ones(cin, device=DEV)
+        _, mean, invstd = k.bn_fwd_train(bx, bw, bb, rm, rv, 0.1, 1e-5, relu=True)
+        dx_ref = k.conv_dgrad(geom, dy, n, h, w, [wt])
+        ref = k.bn_bwd(dx_ref.clone(), None, bx, bw, mean, invstd, relu=True, bias=bb)
+        dx, sums = k.conv_dgrad_bnsums(geom, dy, n, h, w, [wt], bx, mean, invstd, bw, bb)
+        assert rel(dx, dx_ref) == 0.0
+        if shape[0] == 1 and math == "f32":
+            assert sums is None  # K split across blocks: no per-tile sums
+            return
+        assert sums is not None
+        got = k.bn_bwd_tiles(dx, bx, bw, bb, mean, invstd, sums, dx=dx)
+        assert rel(got, ref) < 1e-5
+    finally:
+        k.set_conv_math(k.MATH_F32)
