@@ -800,16 +800,25 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
           const float bw = p.bn_w ? p.bn_w[cc] : 1.f, bb = p.bn_b ? p.bn_b[cc] : 0.f;
           float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i) {
+            // 16 unconditional (clamped) loads in flight together, then the sums: a guarded
+            // load per element would serialise 16*TM*TN load latencies per block
+            float xv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              xv[r] = p.bn_x[(size_t)(bm + min(rl, nvalid - 1)) * p.N + cc];
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
               const bool ok = rl < nvalid && col < p.N;
-              const float xv = ok ? p.bn_x[(size_t)(bm + rl) * p.N + col] : 0.f;
-              const float g = (ok && (xv - mu) * is * bw + bb > 0.f) ? acc[i][j][r] : 0.f;
+              const float d = xv[r] - mu;
+              const float g = (ok && d * is * bw + bb > 0.f) ? acc[i][j][r] : 0.f;
               s1 += g;
-              s2 += g * (xv - mu);
+              s2 += g * d;
             }
+          }
           s1 += __shfl_xor(s1, 32);
           s2 += __shfl_xor(s2, 32);
           if (hh == 0) {

@@ -50,14 +50,13 @@ __device__ void coeffs_one(int in_size, int out_size, int o, int ks, int *bounds
   int xmax = (int)(center + support + 0.5);
   if (xmax > in_size) xmax = in_size;
   xmax -= xmin;
-  double w[kMaxKsize];
+  // two passes over the (deterministic) filter instead of a per-thread weight array, which
+  // would live in scratch: the sum first, then each normalised weight
   double ww = 0.0;
-  for (int x = 0; x < xmax; ++x) {
-    w[x] = bicubic_filter(((double)(x + xmin) - center + 0.5) * ss);
-    ww += w[x];
-  }
+  for (int x = 0; x < xmax; ++x) ww += bicubic_filter(((double)(x + xmin) - center + 0.5) * ss);
   for (int x = 0; x < ks; ++x) {
-    double v = x < xmax ? (ww != 0.0 ? w[x] / ww : w[x]) : 0.0;
+    const double w = x < xmax ? bicubic_filter(((double)(x + xmin) - center + 0.5) * ss) : 0.0;
+    const double v = ww != 0.0 ? w / ww : w;
     kk[(size_t)o * ks + x] = v < 0 ? (int)(-0.5 + v * (double)(1 << kPrecisionBits))
                                    : (int)(0.5 + v * (double)(1 << kPrecisionBits));
   }

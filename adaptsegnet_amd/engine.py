@@ -20,6 +20,8 @@ Reference semantics followed (file:line in /root/reference):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import kernels as K
@@ -158,10 +160,16 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
         ws.launch(run, dy, x)
 
 
+# BN-backward sums fused into the data-gradient epilogue: measured NET SLOWER at c2 (225 vs
+# 218 ms/step — the epilogue's extra read of the BN input costs the dgrad kernel more than the
+# bn1/bn2 reduction passes it removes, which are the small 1/4-width BNs), so opt-in only.
+_NO_BNSUMS = os.environ.get("ADAPTSEG_BNSUMS") != "1"
+
+
 def _dgrad_into_bn(g, dy, n, h, w, weight, bn, bn_x, st):
     """Data gradient feeding a BN+ReLU backward; with a train-mode BN also its fused sums."""
     mean, invstd, train = st
-    if not train:
+    if not train or _NO_BNSUMS:
         return K.conv_dgrad(g, dy, n, h, w, [weight]), None
     return K.conv_dgrad_bnsums(g, dy, n, h, w, [weight], bn_x, mean, invstd, bn.weight, bn.bias)
 

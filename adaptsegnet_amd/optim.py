@@ -51,7 +51,33 @@ class SGD:
                 first = a not in self._started
                 K.sgd_step(A.data[a:b], A.grad[a:b], self._buf[a:b], lr, self.momentum,
                            self.weight_decay, grad_scale, seg.mult, first)
-                self._started.add(a)
+                self._started.update(o for o in A.offsets if a <= o < b)
+
+    # -- resume (checkpoint.py) --------------------------------------------------------------
+    def state_dict(self, names):
+        """{param name: momentum buffer (reference layout)} for parameters that have one,
+        plus the LRs.  ``names``: arena index -> state_dict key of the model."""
+        A = self.model.arena
+        st = {}
+        if A is not None and self._buf is not None:
+            for i, (p, off) in enumerate(zip(A.params, A.offsets)):
+                if off in self._started:
+                    st[names[i]] = A._view(self._buf, p, off).detach().cpu().contiguous()
+        return {"momentum_buffer": st, "lr": [g["lr"] for g in self.param_groups]}
+
+    @torch.no_grad()
+    def load_state_dict(self, state, names):
+        A = self.model.arena
+        self._buf = torch.zeros(A.numel, dtype=torch.float32, device=A.device)
+        self._arena_id = id(A)
+        self._started = set()
+        bufs = state["momentum_buffer"]
+        for i, (p, off) in enumerate(zip(A.params, A.offsets)):
+            if names[i] in bufs:
+                A._view(self._buf, p, off).copy_(bufs[names[i]])
+                self._started.add(off)
+        for g, lr in zip(self.param_groups, state["lr"]):
+            g["lr"] = lr
 
 
 class Adam:
@@ -81,6 +107,37 @@ class Adam:
         for seg in A.segments:
             for a, b in A.runs(seg):
                 st = self._steps.get(a, 0) + 1
-                self._steps[a] = st
+                for o in A.offsets:
+                    if a <= o < b:
+                        self._steps[o] = st
                 K.adam_step(A.data[a:b], A.grad[a:b], self._m[a:b], self._v[a:b], lr,
                             self.betas[0], self.betas[1], self.eps, st, grad_scale)
+
+    # -- resume (checkpoint.py) --------------------------------------------------------------
+    def state_dict(self, names):
+        """torch.optim.Adam-like per-parameter state keyed by the model's state_dict names."""
+        A = self.model.arena
+        st = {}
+        if A is not None and self._m is not None:
+            for i, (p, off) in enumerate(zip(A.params, A.offsets)):
+                if off in self._steps:
+                    st[names[i]] = {"step": self._steps[off],
+                                    "exp_avg": A._view(self._m, p, off).detach().cpu().contiguous(),
+                                    "exp_avg_sq": A._view(self._v, p, off).detach().cpu().contiguous()}
+        return {"state": st, "lr": [g["lr"] for g in self.param_groups]}
+
+    @torch.no_grad()
+    def load_state_dict(self, state, names):
+        A = self.model.arena
+        self._m = torch.zeros(A.numel, dtype=torch.float32, device=A.device)
+        self._v = torch.zeros(A.numel, dtype=torch.float32, device=A.device)
+        self._arena_id = id(A)
+        self._steps = {}
+        for i, (p, off) in enumerate(zip(A.params, A.offsets)):
+            s = state["state"].get(names[i])
+            if s is not None:
+                A._view(self._m, p, off).copy_(s["exp_avg"])
+                A._view(self._v, p, off).copy_(s["exp_avg_sq"])
+                self._steps[off] = int(s["step"])
+        for g, lr in zip(self.param_groups, state["lr"]):
+            g["lr"] = lr
