@@ -24,6 +24,7 @@ per-replica DataParallel semantics.
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass, field
 
 import torch
@@ -52,6 +53,11 @@ class StepConfig:
     lambda_adv_target1: float = 0.0002
     lambda_adv_target2: float = 0.001
     ignore_label: int = 255
+    # run the target-domain generator forward (+ its D forward) on a second HIP stream while
+    # the source-domain backward executes (independent: same weights, read-only, separate
+    # gradient kernels); the target backward then waits for the source backward.  Results are
+    # bit-identical to the sequential order.
+    overlap_domains: bool = True
 
 
 @dataclass
@@ -91,6 +97,44 @@ class AdaptSegTrainer:
         if t is None:
             t = self._consts[key] = torch.full((), float(v), dtype=torch.float32, device=device)
         return t
+
+    # -- stream overlap of the two domains -----------------------------------------------------
+    _streams: dict = {}
+
+    def _overlap_begin(self, device):
+        """After the source forward: returns (main, side, event) or None (overlap off / CPU)."""
+        if not self.cfg.overlap_domains or device.type != "cuda":
+            return None
+        side = AdaptSegTrainer._streams.get(device.index)
+        if side is None:
+            side = AdaptSegTrainer._streams[device.index] = torch.cuda.Stream(device)
+        main = torch.cuda.current_stream(device)
+        ev = torch.cuda.Event()
+        ev.record(main)   # the target pass starts after the source forward (BN running stats)
+        return main, side, ev
+
+    def _target_ctx(self, ov):
+        if ov is None:
+            return contextlib.nullcontext()
+        main, side, ev = ov
+        side.wait_event(ev)
+        return torch.cuda.stream(side)
+
+    @staticmethod
+    def _join_source(ov):
+        """Before the target-domain G backward: the source backward (main stream) must have
+        finished writing the gradient arena it accumulates into."""
+        if ov is not None:
+            ov[1].wait_stream(ov[0])
+
+    @staticmethod
+    def _overlap_end(ov, *tensors):
+        if ov is None:
+            return
+        main, side, _ = ov
+        main.wait_stream(side)
+        for t in tensors:
+            t.record_stream(main)   # produced on the side stream, read on the main stream
 
     def _backward(self, losses, scales):
         dev = losses[0].device
@@ -190,16 +234,20 @@ class AdaptSegTrainer:
         self._set_requires_grad(D2, False)
         pred2 = self._pred_single(images, c.input_size)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
+        ov = self._overlap_begin(pred2.device)
         self._backward([loss_seg2], [inv])
         L.add("loss_seg2", loss_seg2, inv)
 
-        pred_target2 = self._pred_single(images_t, tsize)
-        d_out2 = D2(F.softmax2d(pred_target2))
-        loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
-        self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])
-        L.add("loss_adv_target2", loss_adv_target2, inv)
-        if g_done is not None:
-            g_done()
+        with self._target_ctx(ov):
+            pred_target2 = self._pred_single(images_t, tsize)
+            d_out2 = D2(F.softmax2d(pred_target2))
+            loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
+            self._join_source(ov)
+            self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])
+            L.add("loss_adv_target2", loss_adv_target2, inv)
+            if g_done is not None:
+                g_done()
+        self._overlap_end(ov, pred_target2, loss_adv_target2)
 
         self._set_requires_grad(D2, True)
         pred2 = pred2.detach()
@@ -219,21 +267,25 @@ class AdaptSegTrainer:
         pred1, pred2 = self.model(images, c.input_size)
         loss_seg1 = F.cross_entropy2d(pred1, labels, c.ignore_label)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
+        ov = self._overlap_begin(pred2.device)
         self._backward([loss_seg2, loss_seg1], [inv, c.lambda_seg * inv])
         L.add("loss_seg1", loss_seg1, inv)
         L.add("loss_seg2", loss_seg2, inv)
 
-        pred_target1, pred_target2 = self.model(images_t, tsize)
-        d_out1 = D1(F.softmax2d(pred_target1))
-        d_out2 = D2(F.softmax2d(pred_target2))
-        loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
-        loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
-        self._backward([loss_adv1, loss_adv2],
-                       [c.lambda_adv_target1 * inv, c.lambda_adv_target2 * inv])
-        L.add("loss_adv_target1", loss_adv1, inv)
-        L.add("loss_adv_target2", loss_adv2, inv)
-        if g_done is not None:
-            g_done()
+        with self._target_ctx(ov):
+            pred_target1, pred_target2 = self.model(images_t, tsize)
+            d_out1 = D1(F.softmax2d(pred_target1))
+            d_out2 = D2(F.softmax2d(pred_target2))
+            loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
+            loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
+            self._join_source(ov)
+            self._backward([loss_adv1, loss_adv2],
+                           [c.lambda_adv_target1 * inv, c.lambda_adv_target2 * inv])
+            L.add("loss_adv_target1", loss_adv1, inv)
+            L.add("loss_adv_target2", loss_adv2, inv)
+            if g_done is not None:
+                g_done()
+        self._overlap_end(ov, pred_target1, pred_target2, loss_adv1, loss_adv2)
 
         self._set_requires_grad(D1, True)
         self._set_requires_grad(D2, True)

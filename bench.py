@@ -193,6 +193,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the two domains' passes sequentially on one stream")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path with several ranks on one GPU)")
@@ -230,7 +232,8 @@ def main():
                 for t in list(m.parameters()) + list(m.buffers()):
                     dist.broadcast(t.data, 0)
     model.train()
-    scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh)
+    scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
+                      overlap_domains=not args.no_overlap)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
