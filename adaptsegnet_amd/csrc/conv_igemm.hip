@@ -326,7 +326,8 @@ void set_splits(Plan &pl) {
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
   // fwd / data-grad split only grids below one block per CU (slab + reduce traffic costs more
   // than the partial second wave it would fill); weight-grad grids are almost always tiny.
-  const int target = pl.mode == MODE_WGRAD ? 1024 : 512;
+  static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob (512 vs 1024: +1.7 % at c2)
+  const int target = pl.mode == MODE_WGRAD ? wg_target : 512;
   const int split_below = pl.mode == MODE_WGRAD ? target : 256;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
