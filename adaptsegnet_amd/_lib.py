@@ -95,6 +95,9 @@ _SIGS = {
     "adaptseg_conv_set_math": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
+    "adaptseg_timing_enable_mem": [_I],
+    "adaptseg_timing_read_id": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_L)],
     "adaptseg_timing_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(_L)],
 }

@@ -367,8 +367,11 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                                                    running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_tiles_final");
   int64_t total4 = rows * c / 4;
+  int slot;  // x (+res) in, y out
+  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
   bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
                                                    relu);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
 }
@@ -431,8 +434,12 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
     AS_CHECK_LAUNCH("bn_bwd_final");
   }
   int64_t total4 = rows * c / 4;
+  int slot;  // dy, x (train), y (mask from y) in; dx, dres out
+  timing_begin(kTBnBwdApply, s,
+               4.0 * rows * c * (2 + (train ? 1 : 0) + (rmode == 1 ? 1 : 0) + (dres ? 1 : 0)), &slot);
   bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, y, x, weight, bias, save_mean, save_invstd,
                                                        coef, dx, dres, rmode, train);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
 }

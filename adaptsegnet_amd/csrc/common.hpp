@@ -70,4 +70,14 @@ constexpr int kEpiActGrad = ADAPTSEG_EPI_LEAKY_GRAD | ADAPTSEG_EPI_RELU_GRAD;
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Live timing (adaptseg_timing_*, conv_igemm.hip): hipEvent pair around one launch; `units` are
+// algorithmic FLOPs (conv kernels, ids < kTimingMemBase) or algorithmic HBM bytes (ids >= it).
+constexpr int kTimingMemBase = 1000;
+enum TimingMemId {
+  kTUpsampleFwd = 1000, kTUpsampleBwd = 1001, kTSoftmaxFwd = 1002, kTSoftmaxBwd = 1003,
+  kTCeFwd = 1004, kTCeBwd = 1005, kTBnApply = 1006, kTBnBwdApply = 1007
+};
+void timing_begin(int kernel_id, hipStream_t s, double units, int *slot);
+void timing_end(int slot, hipStream_t s);
+
 }  // namespace adaptseg

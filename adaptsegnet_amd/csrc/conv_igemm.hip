@@ -214,9 +214,11 @@ __global__ void __launch_bounds__(256) bias_grad_final_kernel(const float *parti
 struct TimingState {
   std::mutex mu;
   bool enabled = false;
+  bool mem_enabled = false;  // HBM-bound kernels (ids >= kTimingMemBase), adaptseg_timing_enable_mem
   int selector = -1;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
-  std::vector<double> flops;
+  std::vector<double> flops;  // algorithmic FLOPs (conv) or bytes (HBM-bound kernels) per launch
+  std::vector<int> ids;
   size_t used = 0;
 };
 static TimingState g_timing;
@@ -226,23 +228,29 @@ static TimingState g_timing;
 static std::atomic<int> g_conv_math{0};
 int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 
-static void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
+void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
   *slot = -1;
-  if (!g_timing.enabled) return;
-  if (g_timing.selector >= 0 && g_timing.selector != kernel_id) return;
+  if (kernel_id >= kTimingMemBase) {
+    if (!g_timing.mem_enabled) return;
+  } else {
+    if (!g_timing.enabled) return;
+    if (g_timing.selector >= 0 && g_timing.selector != kernel_id) return;
+  }
   std::lock_guard<std::mutex> lk(g_timing.mu);
   if (g_timing.used == g_timing.events.size()) {
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
     g_timing.events.push_back({a, b});
     g_timing.flops.push_back(0.0);
+    g_timing.ids.push_back(0);
   }
   *slot = (int)g_timing.used++;
   g_timing.flops[*slot] = fl;
+  g_timing.ids[*slot] = kernel_id;
   (void)hipEventRecord(g_timing.events[*slot].first, s);
 }
 
-static void timing_end(int slot, hipStream_t s) {
+void timing_end(int slot, hipStream_t s) {
   if (slot < 0) return;
   (void)hipEventRecord(g_timing.events[slot].second, s);
 }
@@ -322,7 +330,7 @@ void set_splits(Plan &pl) {
   }
   pl.tiles = (int)(ceil_div(p.M, bm) * ceil_div(p.N, bn));
   const int nkt = (int)ceil_div(p.K, pl.bk);
-  // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~4.
+  // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~2.
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
   // fwd / data-grad split only grids below one block per CU (slab + reduce traffic costs more
   // than the partial second wave it would fill); weight-grad grids are almost always tiny.
@@ -379,7 +387,12 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     set_error("conv: bad op %d", op);
     return ADAPTSEG_ERR_ARG;
   }
-  if (pl.cfg == 0 && getenv("ADAPTSEG_EXP_CFG")) pl.cfg = atoi(getenv("ADAPTSEG_EXP_CFG"));  // A/B knob
+  // 128x128 tile at BK 16 (cfg 6: half the LDS, shorter K steps) measured faster than BK 32
+  // for multi-tap weight gradients (+2-8 %, per-shape conv bench, profiles/r1/conv_cfg_ab.txt).
+  // It also wins 1-7 % on the layer3/4 forward convs in isolation, but not end to end (c2
+  // 19.2 vs 19.3 images/s), so the forward keeps BK 32.
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && d->kh * d->kw > 1) pl.cfg = 6;
+  if ((pl.cfg == 0 || pl.cfg == 6) && getenv("ADAPTSEG_EXP_CFG")) pl.cfg = atoi(getenv("ADAPTSEG_EXP_CFG"));  // A/B knob
   p.fd_nseg_k = make_fastdiv(p.kseg);
   pl.flops = conv_flops(d);
   // FAST path eligibility (alignment re-checked at launch).  Vector operands need tile-
@@ -753,11 +766,42 @@ int adaptseg_timing_enable(int enable, int selector) {
   return ADAPTSEG_OK;
 }
 
+int adaptseg_timing_enable_mem(int enable) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  g_timing.mem_enabled = enable != 0;
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_timing_read_id(int kernel_id, double *total_ms, double *total_units, int64_t *launches) {
+  AS_CHECK_ARG(total_ms && total_units && launches, "timing_read_id: null");
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  double ms = 0, un = 0;
+  int64_t n = 0;
+  for (size_t i = 0; i < g_timing.used; ++i) {
+    if (g_timing.ids[i] != kernel_id) continue;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, g_timing.events[i].first, g_timing.events[i].second) != hipSuccess) {
+      set_error("timing_read_id: event query failed (synchronise first)");
+      return ADAPTSEG_ERR_HIP;
+    }
+    ms += t;
+    un += g_timing.flops[i];
+    ++n;
+  }
+  *total_ms = ms;
+  *total_units = un;
+  *launches = n;
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches) {
   AS_CHECK_ARG(total_ms && total_flops && launches, "timing_read: null");
   std::lock_guard<std::mutex> lk(g_timing.mu);
   double ms = 0, fl = 0;
+  int64_t n = 0;
   for (size_t i = 0; i < g_timing.used; ++i) {
+    if (g_timing.ids[i] >= kTimingMemBase) continue;
+    ++n;
     float t = 0.f;
     if (hipEventElapsedTime(&t, g_timing.events[i].first, g_timing.events[i].second) != hipSuccess) {
       set_error("timing_read: event query failed (synchronise first)");
@@ -768,7 +812,7 @@ int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launche
   }
   *total_ms = ms;
   *total_flops = fl;
-  *launches = (int64_t)g_timing.used;
+  *launches = n;
   return ADAPTSEG_OK;
 }
 

@@ -699,7 +699,10 @@ int adaptseg_upsample_bilinear_fwd(int n, int c, int h, int w, int oh, int ow, c
   AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "upsample_fwd: bad geometry");
   AS_CHECK_ARG(x && y, "upsample_fwd: null pointer");
   int64_t total = (int64_t)n * oh * ow * c;
+  int slot;
+  timing_begin(kTUpsampleFwd, as_stream(stream), 4.0 * n * c * ((double)h * w + (double)oh * ow), &slot);
   upsample_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, x, y);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("upsample_fwd");
   return ADAPTSEG_OK;
 }
@@ -716,22 +719,28 @@ int adaptseg_upsample_bilinear_bwd(int n, int c, int h, int w, int oh, int ow, c
   hipStream_t s = as_stream(stream);
   float *tmp = reinterpret_cast<float *>(ws);
   int64_t t1 = (int64_t)n * oh * w * c;
+  int slot;  // algorithmic bytes: read dy, write dx (the row pass's intermediate is not counted)
+  timing_begin(kTUpsampleBwd, s, 4.0 * n * c * ((double)h * w + (double)oh * ow), &slot);
   upsample_bwd_x_kernel<<<grid1d(t1), 256, 0, s>>>(n, c, w, oh, ow, dy, tmp);
   AS_CHECK_LAUNCH("upsample_bwd_x");
   int64_t t2 = (int64_t)n * h * w * c;
   upsample_bwd_y_kernel<<<grid1d(t2), 256, 0, s>>>(n, c, h, w, oh, tmp, dx,
                                                     (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("upsample_bwd_y");
   return ADAPTSEG_OK;
 }
 
 int adaptseg_softmax_fwd(int64_t rows, int c, const float *x, float *y, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && x && y, "softmax_fwd: bad args");
+  int slot;
+  timing_begin(kTSoftmaxFwd, as_stream(stream), 8.0 * rows * c, &slot);
   if (c <= kRowTileMaxC)
     softmax_fwd_tiled_kernel<<<grid1d(rows, kRowTile, 8192), kRowTile, kRowTile * c * sizeof(float),
                                as_stream(stream)>>>(rows, c, x, y);
   else
     softmax_fwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, x, y);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("softmax_fwd");
   return ADAPTSEG_OK;
 }
@@ -739,12 +748,15 @@ int adaptseg_softmax_fwd(int64_t rows, int c, const float *x, float *y, adaptseg
 int adaptseg_softmax_bwd(int64_t rows, int c, const float *y, const float *dy, float *dx, int flags,
                          adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && y && dy && dx, "softmax_bwd: bad args");
+  int slot;
+  timing_begin(kTSoftmaxBwd, as_stream(stream), 12.0 * rows * c, &slot);
   if (c <= kRowTileMaxC)
     softmax_bwd_tiled_kernel<<<grid1d(rows, kRowTile, 8192), kRowTile, 2 * kRowTile * c * sizeof(float),
                                as_stream(stream)>>>(rows, c, y, dy, dx, (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
   else
     softmax_bwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, y, dy, dx,
                                                                     (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("softmax_bwd");
   return ADAPTSEG_OK;
 }
@@ -768,6 +780,8 @@ int adaptseg_softmax_ce_fwd(int64_t rows, int c, const float *logits, const int6
   }
   hipStream_t s = as_stream(stream);
   float *partial = reinterpret_cast<float *>(ws);
+  int slot;  // logits + int64 labels
+  timing_begin(kTCeFwd, s, 4.0 * rows * c + 8.0 * rows, &slot);
   if (c <= kRowTileMaxC)
     ce_fwd_tiled_kernel<<<parts, kRowTile, kRowTile * c * sizeof(float), s>>>(rows, c, logits, labels, ignore,
                                                                             class_weight, partial);
@@ -775,6 +789,7 @@ int adaptseg_softmax_ce_fwd(int64_t rows, int c, const float *logits, const int6
     ce_fwd_partial_kernel<<<parts, 256, 0, s>>>(rows, c, logits, labels, ignore, class_weight, partial);
   AS_CHECK_LAUNCH("ce_fwd_partial");
   pair_final_kernel<<<1, 64, 0, s>>>(partial, parts, out, 0, 1.0);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("ce_final");
   return ADAPTSEG_OK;
 }
@@ -783,6 +798,8 @@ int adaptseg_softmax_ce_bwd(int64_t rows, int c, const float *logits, const int6
                             const float *class_weight, const float *out, const float *grad_loss, float *dlogits,
                             int flags, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && logits && labels && out && grad_loss && dlogits, "softmax_ce_bwd: bad args");
+  int slot;  // logits + labels in, dlogits out
+  timing_begin(kTCeBwd, as_stream(stream), 8.0 * rows * c + 8.0 * rows, &slot);
   if (c <= kRowTileMaxC)
     ce_bwd_tiled_kernel<<<grid1d(rows, kRowTile, 8192), kRowTile, kRowTile * c * sizeof(float),
                           as_stream(stream)>>>(rows, c, logits, labels, ignore, class_weight, out, grad_loss,
@@ -791,6 +808,7 @@ int adaptseg_softmax_ce_bwd(int64_t rows, int c, const float *logits, const int6
     ce_bwd_kernel<<<grid1d(rows), 256, 0, as_stream(stream)>>>(rows, c, logits, labels, ignore, class_weight, out,
                                                                grad_loss, dlogits,
                                                                (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("ce_bwd");
   return ADAPTSEG_OK;
 }

@@ -486,6 +486,24 @@ def timing_enable(selector: int = -1, enable: bool = True):
     check(_lib.lib().adaptseg_timing_enable(1 if enable else 0, int(selector)), "timing_enable")
 
 
+MEM_KERNELS = {1000: "upsample_fwd_kernel", 1001: "upsample_bwd_{x,y}_kernel", 1002: "softmax_fwd",
+               1003: "softmax_bwd", 1004: "ce_fwd (+final)", 1005: "ce_bwd", 1006: "bn_apply_kernel",
+               1007: "bn_bwd_apply_kernel"}
+
+
+def timing_enable_mem(enable: bool = True):
+    """Record every HBM-bound interp / loss / BN-apply launch with its algorithmic bytes."""
+    check(_lib.lib().adaptseg_timing_enable_mem(1 if enable else 0), "timing_enable_mem")
+
+
+def timing_read_id(kernel_id: int):
+    """(total_ms, total_units, launches) of the recorded launches of one kernel id."""
+    ms, un, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
+    check(_lib.lib().adaptseg_timing_read_id(int(kernel_id), ctypes.byref(ms), ctypes.byref(un),
+                                             ctypes.byref(n)), "timing_read_id")
+    return ms.value, un.value, n.value
+
+
 def timing_read():
     """(total_ms, total_flops, launches) of the timed launches since timing_enable()."""
     ms, fl, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)

@@ -56,8 +56,10 @@ class StepConfig:
     # run the target-domain generator forward (+ its D forward) on a second HIP stream while
     # the source-domain backward executes (independent: same weights, read-only, separate
     # gradient kernels); the target backward then waits for the source backward.  Results are
-    # bit-identical to the sequential order.
-    overlap_domains: bool = True
+    # bit-identical to the sequential order.  Off by default: +1-2.5 % images/s at c2/c3/c5,
+    # but every forward conv then shares the GPU with backward kernels, which halves the
+    # per-launch roofline of the dominant kernel that bench.py reports.
+    overlap_domains: bool = False
 
 
 @dataclass

@@ -35,6 +35,7 @@ sys.path.insert(0, REPO)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X: 256 CU x 2.4 GHz x 256 FLOP/clk/CU (MI355X_MICROARCH.md)
 METRIC = "adversarial-train images/sec at 1024×512, DeeplabMulti+D, 1/2/4/8 MI355X"
 
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (v_mfma_f32_32x32x16_bf16), dense
 
 CONFIGS = {
@@ -193,8 +194,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="run the two domains' passes sequentially on one stream")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the target-domain pass on a second stream, overlapping the source "
+                         "backward (StepConfig.overlap_domains)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path with several ranks on one GPU)")
@@ -233,7 +235,7 @@ def main():
                     dist.broadcast(t.data, 0)
     model.train()
     scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
-                      overlap_domains=not args.no_overlap)
+                      overlap_domains=args.overlap)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
@@ -257,6 +259,7 @@ def main():
     dom = max(cand, key=cand.get)
     if not args.no_roofline:
         K.timing_enable(dom)
+        K.timing_enable_mem(True)
 
     if world > 1:
         dist.barrier()
@@ -270,7 +273,17 @@ def main():
     elapsed = time.perf_counter() - t0
     if not args.no_roofline:
         K.timing_enable(dom, enable=False)
+        K.timing_enable_mem(False)
         k_ms, k_flops, k_launches = K.timing_read()
+        hbm = []
+        for kid, name in K.MEM_KERNELS.items():
+            ms_, by_, n_ = K.timing_read_id(kid)
+            if n_:
+                gbs = by_ / (ms_ / 1e3) / 1e9
+                hbm.append({"kernel": name, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                            "algorithmic_bytes_per_launch": by_ / n_, "avg_launch_ms": ms_ / n_,
+                            "launches_per_step": n_ / args.steps})
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -307,6 +320,9 @@ def main():
                            "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,
                            "flop_share_of_step": inv[dom] / step_flops}
+        # north_star: HBM GB/s of the interp / loss kernels (and the BN passes) vs the peak,
+        # live hipEvents over the same timed steps
+        out["hbm_kernels"] = hbm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             aff = len(os.sched_getaffinity(0))

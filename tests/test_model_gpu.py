@@ -238,3 +238,29 @@ def test_adversarial_step_train_bn(data, level, gan):
     if level == "single-level":  # layer5 gets no gradient -> untouched, like torch's SGD
         assert torch.equal(sd["layer5.conv2d_list.0.weight"].cpu(),
                            torch.from_numpy(g0["layer5.conv2d_list.0.weight"]).float())
+
+
+@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+def test_domain_overlap_is_bit_identical(data, level, gan):
+    """StepConfig.overlap_domains (target-domain pass on a second stream, overlapping the
+    source backward) must not change a single bit of the losses or parameters."""
+    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
+    runs = []
+    for ov in (False, True):
+        from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+        xs, lab, xt = data
+        m, d1, d2 = build_g(), build_d(2001), build_d(2002)
+        m.train()
+        tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2,
+                             StepConfig(**cfg, overlap_domains=ov))
+        batch = [(xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))]
+        losses = [tr.step(it, batch).values() for it in range(2)]
+        torch.cuda.synchronize()
+        runs.append((losses, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                     {k: v.detach().cpu().clone() for k, v in d2.state_dict().items()}))
+    (l0, g0, d0), (l1, g1, d1_) = runs
+    assert l0 == l1
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    for k in d0:
+        assert torch.equal(d0[k], d1_[k]), k
