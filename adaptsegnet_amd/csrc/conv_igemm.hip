@@ -426,6 +426,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.bf16 = true;
   }
   if (pl.bf16) pl.cfg = 0;
+  // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
+  if (pl.cfg == 8 && (op == ADAPTSEG_CONV_BWD_DATA || !pl.fast || pl.ae || pl.be || pl.s2)) pl.cfg = 0;
   set_splits(pl);
   return ADAPTSEG_OK;
 }

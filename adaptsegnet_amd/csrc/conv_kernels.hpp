@@ -848,8 +848,8 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
   }
 }
 
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool S2, bool AE, bool BE>
-__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_fast_kernel(const ConvParams p) {
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool S2, bool AE, bool BE, int MINB = 1>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kernel(const ConvParams p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;  // threads per block (4 or 8 waves)
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -1306,11 +1306,13 @@ struct Plan {
 // tile configs: 0 = 128x128 (2x2 waves), 1 = 256x32 (4x1), 2 = 32x256 (1x4), 3 = 64x256 (1x4),
 // 4 = 256x64 (4x1), 5 = 64x64 (2x2, small weight gradients), 6 = 128x128 with BK 16
 // (33 KB of LDS: three blocks per CU), 7 = 256x128 with 8 waves (4x2, 512 threads).  Every wave owns a 64x64, 64x32 or 32x64 block of 32x32x2 MFMA tiles.
-static const int kCfgBM[8] = {128, 256, 32, 64, 256, 64, 128, 256};
-static const int kCfgBN[8] = {128, 32, 256, 256, 64, 64, 128, 128};
-static const int kCfgThreads[8] = {256, 256, 256, 256, 256, 256, 256, 512};
+// 8 = 128x128 with BK 16 compiled for 3 blocks per CU (__launch_bounds__ min-blocks 3: the
+// accumulators move from AGPRs into the VGPR budget, 117 registers, so 3-4 waves per SIMD).
+static const int kCfgBM[9] = {128, 256, 32, 64, 256, 64, 128, 256, 128};
+static const int kCfgBN[9] = {128, 32, 256, 256, 64, 64, 128, 128, 128};
+static const int kCfgThreads[9] = {256, 256, 256, 256, 256, 256, 256, 512, 256};
 // K step of the FAST kernel per config (LDS: 2 stages x BK x (BM+BN+pad) floats)
-static int fast_bk(int cfg) { return (cfg == 4 || cfg == 6) ? 16 : 32; }
+static int fast_bk(int cfg) { return (cfg == 4 || cfg == 6 || cfg == 8) ? 16 : 32; }
 
 
 // Planning and execution (conv_igemm.hip), shared with the tap-GEMM path (conv_tapgemm.hip).

@@ -135,7 +135,8 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize):
 
 # kernel selector (adaptseg_conv2d_kernel_id) -> the kernel template rocprofv3 reports
 _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32), 3: (64, 256, 1, 4, 32),
-        4: (256, 64, 4, 1, 16), 5: (64, 64, 2, 2, 32), 6: (128, 128, 2, 2, 16), 7: (256, 128, 4, 2, 32)}
+        4: (256, 64, 4, 1, 16), 5: (64, 64, 2, 2, 32), 6: (128, 128, 2, 2, 16), 7: (256, 128, 4, 2, 32),
+        8: (128, 128, 2, 2, 16)}
 
 
 def selector_symbol(sel):
@@ -146,8 +147,9 @@ def selector_symbol(sel):
     b = lambda v: "true" if v else "false"  # noqa: E731
     if var >= 4:
         v = var - 4
+        minb = 3 if cfg == 8 else 1   # __launch_bounds__ min-blocks template argument
         return (f"igemm_fast_kernel<{op}, {bm}, {bn}, {wm}, {wn}, {bk}, {b(v & 4)}, {b(v & 2)}, "
-                f"{b(v & 1)}>")
+                f"{b(v & 1)}, {minb}>")
     return f"igemm_kernel<{op}, {bm}, {bn}, {wm}, {wn}, {b(var & 2)}, {b(var & 1)}>"
 
 

@@ -20,3 +20,7 @@ timeout -k 10 600 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-base
 # shards, gradient all-reduce, barrier + max-over-ranks timing)
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 2 --warmup 1 --backend gloo --batch 1 > gpurun_out/bench_dp2_gloo_$TAG.log 2>&1 || exit 9
 timeout -k 10 600 python tools/bench_eval.py > gpurun_out/bench_eval_$TAG.log 2>&1 || exit 10
+timeout -k 10 600 python bench.py --config c5 --steps 4 --warmup 2 --no-cpu-baseline > gpurun_out/bench_c5_$TAG.log 2>&1 || exit 11
+timeout -k 10 300 python tools/bench_preprocess.py > gpurun_out/bench_preprocess_$TAG.log 2>&1 || exit 12
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --overlap > gpurun_out/bench_c2_overlap_$TAG.log 2>&1 || exit 13
+bash tools/gpu_traffic.sh c2 || exit 14
