@@ -287,10 +287,11 @@ def test_maxpool():
 
 @pytest.mark.parametrize("hw,out", [((9, 13), (65, 97)), ((64, 128), (512, 1024)),
                                     ((90, 160), (720, 1280)), ((1, 5), (3, 9)), ((7, 7), (7, 7))])
-def test_upsample(hw, out):
+@pytest.mark.parametrize("c", [19, 40])
+def test_upsample(hw, out, c):
     k = K()
     g = torch.Generator().manual_seed(10)
-    n, c = 2, 19
+    n = 2
     x = torch.randn(n, c, *hw, generator=g, dtype=torch.float64)
     xr = x.clone().requires_grad_(True)
     y = F.interpolate(xr, size=out, mode="bilinear", align_corners=True)

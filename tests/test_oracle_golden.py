@@ -120,8 +120,10 @@ def test_two_steps_match_reference(gold, inputs, level, gan):
         np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
     for k, t in G.items():
         if t.dtype.is_floating_point:
+            # a parameter SUM can nearly cancel; atol 1e-8 absorbs the host's thread-count-
+            # dependent fp64 summation order (16 vs 8 cores: 4e-10 seen on a 0.41 sum)
             np.testing.assert_allclose(t.detach().sum().item(), float(gold[pre + "G/sum/" + k]),
-                                       rtol=1e-9, atol=1e-12, err_msg=k)
+                                       rtol=1e-9, atol=1e-8, err_msg=k)
         else:
             assert int(t) == int(gold[pre + "G/int/" + k]), k
     for k, t in D2.items():
