@@ -16,6 +16,7 @@
 // Block tile 128x128x64, 4 waves (2x2), each wave 64x64 = 2x2 MFMA tiles of 32x32x16.
 #pragma once
 #include "conv_kernels.hpp"
+#include <type_traits>
 
 namespace adaptseg {
 
@@ -61,24 +62,28 @@ __device__ __forceinline__ bf16x8 kc_frag(const char *img, int r0, int ks, int l
   return as_bf16x8(*reinterpret_cast<const uint4 *>(img + kc_off(r0 + (lane & 31), 2 * ks + (lane >> 5))));
 }
 
-template <int MODE, bool S2>
-__global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
-  constexpr int BM = 128, BN = 128, BK = kB16BK, NT = 256;
-  constexpr int WAVES_M = 2, WAVES_N = 2, TM = 2, TN = 2;
+// BN_ = 128 (4 waves, 2x2) or 256 (8 waves, 2x4; K-contiguous products only): the wider tile
+// halves the refetch of the gathered fp32 A operand, which bounds this kernel.
+template <int MODE, bool S2, int BN_ = 128>
+__global__ void __launch_bounds__(BN_ * 2, 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  constexpr int BM = 128, BN = BN_, BK = kB16BK, NT = BN_ * 2;
+  constexpr int WAVES_M = 2, WAVES_N = BN_ / 64, TM = 2, TN = 2;
   constexpr bool MC = MODE == MODE_WGRAD;      // both operands M/N-contiguous
-  constexpr int IMG = 16384;                   // bytes per operand image (128 x 64 bf16)
-  constexpr int STAGE = 2 * IMG;
-  constexpr int NQ = MC ? BM * BK / 4 / NT : BM * BK / 8 / NT;  // slots per thread per operand: 8 / 4
-  static_assert(NQ * NT * (MC ? 4 : 8) == BM * BK, "slots cover the tile");
+  static_assert(!MC || BN_ == 128, "weight-gradient images are 128 wide");
+  constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;  // bytes per operand image (bf16)
+  constexpr int STAGE = IMGA + IMGB;
+  constexpr int NQ = MC ? BM * BK / 4 / NT : BM * BK / 8 / NT;  // A slots per thread: 8 / 4 (2 at BN 256)
+  constexpr int NQB = MC ? NQ : BN * BK / 8 / NT;                // B slots per thread
+  static_assert(NQ * NT * (MC ? 4 : 8) == BM * BK && NQB * NT * (MC ? 4 : 8) == BN * BK, "slots cover the tile");
 
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
   const int tid = threadIdx.x;
   const int ntn = (p.N + BN - 1) / BN;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  int tile, split;
+  xcd_tile_split(tile, split);
   const int tm = tile / ntn, tn = tile - tm * ntn;
   const int bm = tm * BM, bn = tn * BN;
-  const int split = blockIdx.y;
   const SegRegs sr = seg_regs(p);
 
   int M = p.M, K = p.K, Hc = p.h, Wc = p.w, py = 0, px = 0, kh0 = 0, kw0 = 0, nkw = p.kw_;
@@ -105,8 +110,18 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
   // columns 4*(q&31) .. +3.
   int a_pix[NQ], a_y[NQ], a_x[NQ];
   bool a_ok[NQ];
-  int b_off[NQ], b_dy[NQ], b_dx[NQ];
-  bool b_ok[NQ];
+  int b_off[NQB], b_dy[NQB], b_dx[NQB];
+  bool b_ok[NQB];
+  if constexpr (!MC) {
+#pragma unroll
+    for (int i = 0; i < NQB; ++i) {
+      const int q = tid + NT * i;
+      const int row = q >> 3, ch = q & 7;
+      const int n = bn + row;
+      b_ok[i] = n < p.N;
+      b_off[i] = min(n, p.N - 1) * ktot + 8 * ch;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     const int q = tid + NT * i;
@@ -138,9 +153,6 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
         a_x[i] = iw;
         a_pix[i] = (((int)b * p.oh + ih) * p.ow + iw) * p.k + 8 * ch;
       }
-      const int n = bn + row;
-      b_ok[i] = n < p.N;
-      b_off[i] = min(n, p.N - 1) * ktot + 8 * ch;
     } else {
       const int col = 4 * (q & 31);
       a_ok[i] = bm + col < p.M;                    // Cout % 4 == 0
@@ -155,12 +167,17 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
     }
   }
 
-  float4 ra[MC ? NQ : 2 * NQ];
-  float4 rbf[MC ? NQ : 1];
-  uint4 rbh[MC ? 1 : NQ];
-  bool ma[NQ], mb[NQ];
+  // Two register sets: the loads for tile kt+2 are issued while tile kt+1 (already in the
+  // other set) waits to be written to LDS, so each load has two K steps of latency budget.
+  // (The weight-gradient build keeps one set: two would spill at its register budget.)
+  constexpr int NSETS = MC ? 1 : 2;
+  float4 ra[NSETS][MC ? NQ : 2 * NQ];
+  float4 rbf[NSETS][MC ? NQ : 1];
+  uint4 rbh[NSETS][MC ? 1 : NQB];
+  bool ma[NSETS][NQ], mb[NSETS][NQB];
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, auto set_) {
+    constexpr int S = decltype(set_)::value;
     const int kbase = kt * BK;
     if constexpr (MODE == MODE_FWD) {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
@@ -172,15 +189,15 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const bool v = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h && (unsigned)(a_x[i] + dx) < (unsigned)p.w;
-        ma[i] = v;
+        ma[S][i] = v;
         const float *src = p.x + (v ? a_pix[i] + soff : 0);
-        ra[2 * i] = ld4(src);
-        ra[2 * i + 1] = ld4(src + 4);
+        ra[S][2 * i] = ld4(src);
+        ra[S][2 * i + 1] = ld4(src + 4);
       }
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        mb[i] = b_ok[i];
-        rbh[i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + kbase);
+      for (int i = 0; i < NQB; ++i) {
+        mb[S][i] = b_ok[i];
+        rbh[S][i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + kbase);
       }
     } else if constexpr (MODE == MODE_DGRAD) {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
@@ -203,15 +220,15 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const bool v = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh && (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
-        ma[i] = v;
+        ma[S][i] = v;
         const float *src = p.dy + (v ? a_pix[i] + soff : 0);
-        ra[2 * i] = ld4(src);
-        ra[2 * i + 1] = ld4(src + 4);
+        ra[S][2 * i] = ld4(src);
+        ra[S][2 * i + 1] = ld4(src + 4);
       }
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        mb[i] = b_ok[i];
-        rbh[i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + wk);
+      for (int i = 0; i < NQB; ++i) {
+        mb[S][i] = b_ok[i];
+        rbh[S][i] = *reinterpret_cast<const uint4 *>(wb + b_off[i] + wk);
       }
     } else {  // WGRAD: k = output pixel
       const int krow0 = tid >> 5;
@@ -219,8 +236,8 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
       for (int i = 0; i < NQ; ++i) {
         const int m = kbase + krow0 + (NT / 32) * i;
         const bool rv = m < K;
-        ma[i] = rv && a_ok[i];
-        ra[i] = ld4(p.dy + (size_t)(rv ? m : 0) * p.k + a_pix[i]);
+        ma[S][i] = rv && a_ok[i];
+        ra[S][i] = ld4(p.dy + (size_t)(rv ? m : 0) * p.k + a_pix[i]);
         const int mm = min(m, K - 1);
         uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
         const int ow = mm - (int)t * p.ow;
@@ -228,30 +245,37 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
         const int oh = (int)t - (int)b * p.oh;
         const int iy = oh * p.stride + b_dy[i], ix = ow * p.stride + b_dx[i];
         const bool v = b_ok[i] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-        mb[i] = v;
-        rbf[i] = ld4(p.x + (v ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
+        mb[S][i] = v;
+        rbf[S][i] = ld4(p.x + (v ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
       }
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, auto set_) {
+    constexpr int S = decltype(set_)::value;
     char *As = lds + buf * STAGE;
-    char *Bs = As + IMG;
+    char *Bs = As + IMGA;
+    if constexpr (!MC) {
+#pragma unroll
+      for (int i = 0; i < NQB; ++i) {
+        const int q = tid + NT * i;
+        *reinterpret_cast<uint4 *>(Bs + kc_off(q >> 3, q & 7)) = mb[S][i] ? rbh[S][i] : make_uint4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int q = tid + NT * i;
       if constexpr (!MC) {
         const int row = q >> 3, ch = q & 7;
-        const uint2 lo = cvt4_bf16(ra[2 * i]), hi = cvt4_bf16(ra[2 * i + 1]);
-        const uint4 av = ma[i] ? make_uint4(lo.x, lo.y, hi.x, hi.y) : make_uint4(0, 0, 0, 0);
+        const uint2 lo = cvt4_bf16(ra[S][2 * i]), hi = cvt4_bf16(ra[S][2 * i + 1]);
+        const uint4 av = ma[S][i] ? make_uint4(lo.x, lo.y, hi.x, hi.y) : make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4 *>(As + kc_off(row, ch)) = av;
-        *reinterpret_cast<uint4 *>(Bs + kc_off(row, ch)) = mb[i] ? rbh[i] : make_uint4(0, 0, 0, 0);
       } else {
         const int kr = q >> 5, col = 4 * (q & 31);
         const int o = mc_off(kr, col >> 3) + 8 * ((col >> 2) & 1);
-        const uint2 av = cvt4_bf16(ra[i]), bv = cvt4_bf16(rbf[i]);
-        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? av : make_uint2(0, 0);
-        *reinterpret_cast<uint2 *>(Bs + o) = mb[i] ? bv : make_uint2(0, 0);
+        const uint2 av = cvt4_bf16(ra[S][i]), bv = cvt4_bf16(rbf[S][i]);
+        *reinterpret_cast<uint2 *>(As + o) = ma[S][i] ? av : make_uint2(0, 0);
+        *reinterpret_cast<uint2 *>(Bs + o) = mb[S][i] ? bv : make_uint2(0, 0);
       }
     }
   };
@@ -267,40 +291,65 @@ __global__ void __launch_bounds__(256) igemm_bf16_kernel(const ConvParams p, con
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (kt0 < kt1) {
-    load_tile(kt0);
-    store_tile(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
-      const char *As = lds + cur * STAGE;
-      const char *Bs = As + IMG;
-      bf16x8 a[2][TM], b[2][TN];
-      auto read_frags = [&](int ks, int slot) {
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, NSETS - 1>;
+  int cur = 0;
+  // MFMAs of one K step from LDS buffer `cur`
+  auto compute = [&]() {
+    const char *As = lds + cur * STAGE;
+    const char *Bs = As + IMGA;
+    bf16x8 a[2][TM], b[2][TN];
+    auto read_frags = [&](int ks, int slot) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          a[slot][i] = MC ? mc_frag(As, wm * 64 + i * 32, ks, lane) : kc_frag(As, wm * 64 + i * 32, ks, lane);
+      for (int i = 0; i < TM; ++i)
+        a[slot][i] = MC ? mc_frag(As, wm * 64 + i * 32, ks, lane) : kc_frag(As, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[slot][j] = MC ? mc_frag(Bs, wn * 64 + j * 32, ks, lane) : kc_frag(Bs, wn * 64 + j * 32, ks, lane);
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int cb = ks & 1;
+      if (ks + 1 < BK / 16) read_frags(ks + 1, cb ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          b[slot][j] = MC ? mc_frag(Bs, wn * 64 + j * 32, ks, lane) : kc_frag(Bs, wn * 64 + j * 32, ks, lane);
-      };
-      read_frags(0, 0);
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        const int cb = ks & 1;
-        if (ks + 1 < BK / 16) read_frags(ks + 1, cb ^ 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
-      }
-      if (more) store_tile(cur ^ 1);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (kt0 < kt1) {
+    load_tile(kt0, I0{});
+    store_tile(0, I0{});
+    if constexpr (NSETS == 2) {
+      if (kt0 + 1 < kt1) load_tile(kt0 + 1, I1{});
       __syncthreads();
-      cur ^= 1;
+      // one K step; `held` = the register set holding tile kt+1
+      auto kstep = [&](int kt, auto held) {
+        constexpr int H = decltype(held)::value;
+        using Free = std::integral_constant<int, 1 - H>;
+        if (kt + 2 < kt1) load_tile(kt + 2, Free{});
+        compute();
+        if (kt + 1 < kt1) store_tile(cur ^ 1, held);
+        __syncthreads();
+        cur ^= 1;
+      };
+      for (int kt = kt0; kt < kt1; kt += 2) {
+        kstep(kt, I1{});
+        if (kt + 1 < kt1) kstep(kt + 1, I0{});
+      }
+    } else {
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) load_tile(kt + 1, I0{});
+        compute();
+        if (more) store_tile(cur ^ 1, I0{});
+        __syncthreads();
+        cur ^= 1;
+      }
     }
   }
 

@@ -319,7 +319,7 @@ double conv_flops(const adaptseg_conv_desc *d) {
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
   if (!pl.fast) pl.s2 = pl.bf16 = false;
-  const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg], bn = pl.bf16 ? 128 : kCfgBN[pl.cfg];
+  const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg], bn = pl.bf16 ? pl.bf16_bn : kCfgBN[pl.cfg];
   pl.bk = pl.bf16 ? 64 : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
@@ -420,12 +420,18 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   }
   // bf16 conv math: the vector FAST cases whose K tiles of 64 stay inside one tap
   pl.bf16 = false;
-  if (conv_math() == 1 && pl.fast && !pl.ae && !pl.be) {
+  if (conv_math() != ADAPTSEG_MATH_F32 && pl.fast && !pl.ae && !pl.be) {
     if (op == ADAPTSEG_CONV_FWD) pl.bf16 = d->c % 64 == 0;
     else if (op == ADAPTSEG_CONV_BWD_DATA) pl.bf16 = d->k % 64 == 0;
     else pl.bf16 = true;
   }
-  if (pl.bf16) pl.cfg = 0;
+  if (pl.bf16) {
+    pl.cfg = 0;
+    // 128x256 (8 waves) halves the refetch of the gathered A operand but measured no faster
+    // (c5 27.6 vs 27.7 images/s, per-shape within +-5 %): only with ADAPTSEG_MATH_BF16_WIDE
+    const bool w256 = conv_math() == ADAPTSEG_MATH_BF16_WIDE;
+    pl.bf16_bn = (w256 && op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 256) ? 256 : 128;
+  }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
   if (pl.cfg == 8 && (op == ADAPTSEG_CONV_BWD_DATA || !pl.fast || pl.ae || pl.be || pl.s2)) pl.cfg = 0;
   set_splits(pl);
@@ -433,7 +439,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
-  if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0);
+  if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)
   if (pl.fast) return 100 * mode + 10 * pl.cfg + 4 + (pl.s2 ? 4 : 0) + (pl.ae ? 2 : 0) + (pl.be ? 1 : 0);
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
@@ -749,7 +755,8 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
 }
 
 int adaptseg_conv_set_math(int math) {
-  AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16, "conv_set_math: bad math %d", math);
+  AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16 || math == ADAPTSEG_MATH_BF16_WIDE,
+               "conv_set_math: bad math %d", math);
   g_conv_math.store(math);
   return ADAPTSEG_OK;
 }

@@ -580,6 +580,20 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
   return x * q + min(x, r) + j;
 }
 
+// Split-K grids: the dispatcher's XCD is (blockIdx.y * gridDim.x + blockIdx.x) % 8, so the
+// remap runs over the flattened (split, tile) space — each XCD then walks whole splits, and
+// the K slice of both operands that a split's tiles share is fetched into ONE L2.
+__device__ __forceinline__ void xcd_tile_split(int &tile, int &split) {
+  if (gridDim.y == 1) {
+    tile = xcd_tile(blockIdx.x, gridDim.x);
+    split = 0;
+    return;
+  }
+  const int w = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  split = w / gridDim.x;
+  tile = w - split * gridDim.x;
+}
+
 __device__ __forceinline__ float4 mask4(int m, float4 v) {
   return make_float4((m & 1) ? v.x : 0.f, (m & 2) ? v.y : 0.f, (m & 4) ? v.z : 0.f, (m & 8) ? v.w : 0.f);
 }
@@ -869,10 +883,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
 
   const int tid = threadIdx.x;
   const int ntn = (p.N + BN - 1) / BN;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  int tile, split;
+  xcd_tile_split(tile, split);
   const int tm = tile / ntn, tn = tile - tm * ntn;
   const int bm = tm * BM, bn = tn * BN;
-  const int split = blockIdx.y;
   const SegRegs sr = seg_regs(p);
 
   // Stride-2 data gradient: blockIdx.z = output-pixel parity class (py, px).  The class's
@@ -1294,7 +1308,8 @@ struct Plan {
   bool va, vb;
   bool fast;
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
-  bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x128x64 tiles, packed bf16 weights
+  bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
+  int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
   int mode;

@@ -22,11 +22,20 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(256);
-  if (pl.mode == MODE_FWD) igemm_bf16_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, wb);
-  else if (pl.mode == MODE_DGRAD && pl.s2) igemm_bf16_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, wb);
-  else if (pl.mode == MODE_DGRAD) igemm_bf16_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, wb);
-  else igemm_bf16_kernel<MODE_WGRAD, false><<<grid, block, 0, s>>>(p, wb);
+  const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;
+  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(w256 ? 512 : 256);
+  if (pl.mode == MODE_FWD) {
+    if (w256) igemm_bf16_kernel<MODE_FWD, false, 256><<<grid, block, 0, s>>>(p, wb);
+    else igemm_bf16_kernel<MODE_FWD, false, 128><<<grid, block, 0, s>>>(p, wb);
+  } else if (pl.mode == MODE_DGRAD && pl.s2) {
+    if (w256) igemm_bf16_kernel<MODE_DGRAD, true, 256><<<grid, block, 0, s>>>(p, wb);
+    else igemm_bf16_kernel<MODE_DGRAD, true, 128><<<grid, block, 0, s>>>(p, wb);
+  } else if (pl.mode == MODE_DGRAD) {
+    if (w256) igemm_bf16_kernel<MODE_DGRAD, false, 256><<<grid, block, 0, s>>>(p, wb);
+    else igemm_bf16_kernel<MODE_DGRAD, false, 128><<<grid, block, 0, s>>>(p, wb);
+  } else {
+    igemm_bf16_kernel<MODE_WGRAD, false, 128><<<grid, block, 0, s>>>(p, wb);
+  }
   return hipGetLastError();
 }
 

@@ -15,11 +15,11 @@ import torch
 
 from . import _lib
 from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
-                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_F32,
+                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_BF16_WIDE, MATH_F32,
                    ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad_bnsums", "bn_bwd_tiles", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "MATH_BF16_WIDE", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad_bnsums", "bn_bwd_tiles", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",

@@ -142,7 +142,7 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
 def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
     if cfg == 9:
-        return f"igemm_bf16_kernel<{op}, {'true' if var else 'false'}>"
+        return f"igemm_bf16_kernel<{op}, {'true' if var & 1 else 'false'}, {256 if var & 2 else 128}>"
     bm, bn, wm, wn, bk = _CFG[cfg]
     b = lambda v: "true" if v else "false"  # noqa: E731
     if var >= 4:

@@ -76,7 +76,11 @@ enum adaptseg_conv_flags {
    conv semantics; activations, gradients and epilogues stay fp32 (BASELINE config c5).
    Products the bf16 kernel does not cover (Cin or Cout not a multiple of 64 for the forward /
    data-gradient, per-element operands) stay on the fp32 path. */
-enum adaptseg_conv_math { ADAPTSEG_MATH_F32 = 0, ADAPTSEG_MATH_BF16 = 1 };
+enum adaptseg_conv_math {
+  ADAPTSEG_MATH_F32 = 0,
+  ADAPTSEG_MATH_BF16 = 1,
+  ADAPTSEG_MATH_BF16_WIDE = 2  /* BF16 with 128x256 tiles for fwd / data-grad products with N >= 256 */
+};
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);
 

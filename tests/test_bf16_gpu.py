@@ -7,6 +7,7 @@ remaining difference is fp32 accumulation order: max|err| <= 2e-5 * max|ref| (as
 path).  Against the UNROUNDED fp64 conv the error is the bf16 input rounding itself
 (~2^-9 relative per operand), checked loosely (<= 2e-2) to show the result is a conv at all.
 """
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -43,6 +44,15 @@ def bf16_math():
     k.set_conv_math(k.MATH_F32)
 
 
+@pytest.fixture(params=["bf16", "bf16_wide"])
+def bf16_any(request):
+    """Both bf16 conv maths: the default 128x128 tile and the 128x256 tile (MATH_BF16_WIDE)."""
+    k = K()
+    k.set_conv_math(k.MATH_BF16 if request.param == "bf16" else k.MATH_BF16_WIDE)
+    yield k
+    k.set_conv_math(k.MATH_F32)
+
+
 def bf(t):
     return t.to(torch.bfloat16).double()
 
@@ -70,8 +80,8 @@ def _ref(x, ws, bs, stride, pads, dils):
 
 
 @pytest.mark.parametrize("case", BF16_CASES, ids=[f"b{i}" for i in range(len(BF16_CASES))])
-def test_bf16_conv_products(case, bf16_math):
-    k = bf16_math
+def test_bf16_conv_products(case, bf16_any):
+    k = bf16_any
     n, cin, h, w, cout, ks, stride, pads, dils, bias = case
     g = torch.Generator().manual_seed(1000 + BF16_CASES.index(case))
     x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
@@ -82,10 +92,12 @@ def test_bf16_conv_products(case, bf16_math):
     oh, ow = geom.out_hw(h, w)
     gy = torch.randn(n, cout, oh, ow, generator=g, dtype=torch.float64)
 
-    # the bf16 kernel must be the one selected (kernel id 100*op + 90 + s2)
+    # the bf16 kernel must be the one selected (kernel id 100*op + 90 + s2 + 2*(tile width 256))
     for op in (0, 1, 2):
         kid, _ = k.conv_kernel_id(geom, n, h, w, op)
         assert kid // 10 % 10 == 9, (op, kid)
+        if k.get_conv_math() == k.MATH_BF16_WIDE and op < 2 and (cout if op == 0 else cin) >= 256:
+            assert kid % 10 >= 2, (op, kid)   # the 256-wide tile
 
     xd, gyd = nhwc(x), nhwc(gy)
     wd = [t.permute(0, 2, 3, 1).contiguous().float().to(DEV) for t in ws]
@@ -118,7 +130,7 @@ def test_bf16_conv_products(case, bf16_math):
 def test_bf16_fused_bn_statistics(bf16_math):
     """The bf16 forward also emits the per-row-tile BN statistics of its output."""
     k = bf16_math
-    n, cin, h, w, cout = 4, 128, 64, 72, 256   # 288 tiles: no K split, so statistics are fused
+    n, cin, h, w, cout = 4, 128, 96, 96, 256   # 288 row tiles: no K split, so statistics are fused
     g = torch.Generator().manual_seed(7)
     x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
     wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.1
