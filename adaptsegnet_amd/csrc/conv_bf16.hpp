@@ -65,7 +65,7 @@ __device__ __forceinline__ bf16x8 kc_frag(const char *img, int r0, int ks, int l
 // BN_ = 128 (4 waves, 2x2) or 256 (8 waves, 2x4; K-contiguous products only): the wider tile
 // halves the refetch of the gathered fp32 A operand, which bounds this kernel.
 template <int MODE, bool S2, int BN_ = 128>
-__global__ void __launch_bounds__(BN_ * 2, 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+__global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
   constexpr int BM = 128, BN = BN_, BK = kB16BK, NT = BN_ * 2;
   constexpr int WAVES_M = 2, WAVES_N = BN_ / 64, TM = 2, TN = 2;
   constexpr bool MC = MODE == MODE_WGRAD;      // both operands M/N-contiguous
@@ -167,10 +167,12 @@ __global__ void __launch_bounds__(BN_ * 2, 2) igemm_bf16_kernel(const ConvParams
     }
   }
 
-  // Two register sets: the loads for tile kt+2 are issued while tile kt+1 (already in the
-  // other set) waits to be written to LDS, so each load has two K steps of latency budget.
-  // (The weight-gradient build keeps one set: two would spill at its register budget.)
-  constexpr int NSETS = MC ? 1 : 2;
+  // Register staging sets.  With two, the loads for tile kt+2 are issued while tile kt+1
+  // (already in the other set) waits to be written to LDS: two K steps of latency budget.
+  // Measured: two sets made fwd / data-grad 5-8 % SLOWER (register pressure at occupancy 2),
+  // and the weight-gradient build would spill — so one set; the two-set schedule stays below
+  // for A/B (flip the constant).
+  constexpr int NSETS = 1;
   float4 ra[NSETS][MC ? NQ : 2 * NQ];
   float4 rbf[NSETS][MC ? NQ : 1];
   uint4 rbh[NSETS][MC ? 1 : NQB];

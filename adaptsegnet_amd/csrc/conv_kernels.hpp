@@ -1275,6 +1275,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
       for (int i = 0; i < TM; ++i) a[0][i] = As[hh * SA + i * 32];
 #pragma unroll
       for (int j = 0; j < TN; ++j) b[0][j] = Bs[hh * SB + j * 32];
+      // MFMA issue outranks the co-resident wave's loads / LDS stores while this tile's
+      // products run (s_setprio is scalar: the same for every lane)
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
         const int cb = (kk >> 1) & 1;
@@ -1291,6 +1294,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
       }
+      __builtin_amdgcn_s_setprio(0);
       if (more) store_tile(cur ^ 1);
       __syncthreads();
       cur ^= 1;
