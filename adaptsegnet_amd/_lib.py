@@ -92,6 +92,12 @@ _SIGS = {
     "adaptseg_bn_bwd_tiles": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adaptseg_preprocess_workspace_size": [_I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],
     "adaptseg_gta5_preprocess": [_I, _I, _I, _I, _I, _P, _F, _F, _F, _P, _P, _P, _P, _P, _SZ, _P],
+    "adaptseg_bn_bwd_affine": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _SZ, _P],
+    "adaptseg_up2_relu_cat_fwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P],
+    "adaptseg_up2_relu_cat_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "adaptseg_grid_warp_fwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "adaptseg_grid_warp_bwd_workspace_size": [_I, _I, _I, _I, ctypes.POINTER(_SZ)],
+    "adaptseg_grid_warp_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],

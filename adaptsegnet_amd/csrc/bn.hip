@@ -26,6 +26,36 @@ __device__ __forceinline__ float4 relu_mask_from_x(float4 g, float4 v, float4 m,
   return g;
 }
 
+// Activation-derivative mask of the backward (rmode): 0 none; 1 ReLU, sign from the saved output
+// y; 2 ReLU, sign recomputed from x; 3 LeakyReLU(0.2), sign from y; 4 LeakyReLU(0.2), sign from
+// x.  LeakyReLU keeps the sign, so its output is as good a mask source as ReLU's.
+__device__ __forceinline__ float4 act_mask(float4 g, int rmode, const float *y, int64_t e, float4 v, float4 m,
+                                           float4 is, float4 w, float4 b) {
+  if (rmode == 0) return g;
+  float4 o;
+  if (rmode == 1 || rmode == 3) {
+    o = *reinterpret_cast<const float4 *>(y + e);
+  } else {
+    o.x = bn_affine(v.x, m.x, is.x, w.x, b.x);
+    o.y = bn_affine(v.y, m.y, is.y, w.y, b.y);
+    o.z = bn_affine(v.z, m.z, is.z, w.z, b.z);
+    o.w = bn_affine(v.w, m.w, is.w, w.w, b.w);
+  }
+  const float k = rmode <= 2 ? 0.f : 0.2f;
+  g.x = o.x > 0.f ? g.x : k * g.x;
+  g.y = o.y > 0.f ? g.y : k * g.y;
+  g.z = o.z > 0.f ? g.z : k * g.z;
+  g.w = o.w > 0.f ? g.w : k * g.w;
+  return g;
+}
+
+// Forward activation: 0 none, 1 ReLU, 2 LeakyReLU(0.2) (model/custom_layers.py:83-96).
+__device__ __forceinline__ float fwd_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return v > 0.f ? v : 0.2f * v;
+  return v;
+}
+
 // Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
 // Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
 template <int MODE>  // 0: stats (shifted by pivot x[0][c]), 1: backward sums
@@ -47,7 +77,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
   if (cok) {
     if (MODE == 0) piv = *reinterpret_cast<const float4 *>(x + c0);
     else piv = *reinterpret_cast<const float4 *>(mean + c0);
-    if (MODE == 1 && relu == 2) {
+    if (MODE == 1 && (relu == 2 || relu == 4)) {
       is = *reinterpret_cast<const float4 *>(invstd + c0);
       ww = w ? *reinterpret_cast<const float4 *>(w + c0) : make_float4(1, 1, 1, 1);
       bb = b ? *reinterpret_cast<const float4 *>(b + c0) : make_float4(0, 0, 0, 0);
@@ -60,13 +90,8 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
         s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
       } else {
         float4 g = *reinterpret_cast<const float4 *>(dy + r * C + c0);
-        if (relu == 1) {
-          float4 o = *reinterpret_cast<const float4 *>(y + r * C + c0);
-          g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
-          g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
-        } else if (relu == 2) {
-          g = relu_mask_from_x(g, v, piv, is, ww, bb);
-        }
+        if (relu == 2) g = relu_mask_from_x(g, v, piv, is, ww, bb);
+        else if (relu) g = act_mask(g, relu, y, r * C + c0, v, piv, is, ww, bb);
         s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
         s2.x += g.x * d.x; s2.y += g.y * d.y; s2.z += g.z * d.z; s2.w += g.w * d.w;
       }
@@ -180,8 +205,11 @@ __global__ void bn_tiles_final_kernel(int C, int ntiles, const float *__restrict
 }
 
 // Finalise backward sums: store mean(g) and mean(g*xhat) per channel.
+// With dweight / dbias (trainable affine BN, the warper's): dbias += sum(g),
+// dweight += sum(g * xhat) — torch's AccumulateGrad.
 __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ partial,
-                                    const float *__restrict__ invstd, float *coef) {
+                                    const float *__restrict__ invstd, float *coef, float *dweight = nullptr,
+                                    float *dbias = nullptr) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double s1, s2;
@@ -190,6 +218,8 @@ __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float
   double n = (double)rows;
   coef[c] = (float)(s1 / n);                          // mean(g)
   coef[C + c] = (float)(s2 / n * (double)invstd[c]);  // mean(g * xhat)
+  if (dbias) dbias[c] += (float)s1;
+  if (dweight) dweight[c] += (float)(s2 * (double)invstd[c]);
 }
 
 __global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
@@ -214,7 +244,7 @@ __global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__
       o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
     }
     if (relu) {
-      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+      o.x = fwd_act(o.x, relu); o.y = fwd_act(o.y, relu); o.z = fwd_act(o.z, relu); o.w = fwd_act(o.w, relu);
     }
     reinterpret_cast<float4 *>(y)[i] = o;
   }
@@ -238,13 +268,12 @@ __global__ void bn_bwd_apply_kernel(int64_t total4, int C, const float *dy,
       v = reinterpret_cast<const float4 *>(x)[i];
       m = *reinterpret_cast<const float4 *>(mean + c);
     }
-    if (relu == 1) {
-      float4 o = reinterpret_cast<const float4 *>(y)[i];
-      g.x = o.x > 0.f ? g.x : 0.f; g.y = o.y > 0.f ? g.y : 0.f;
-      g.z = o.z > 0.f ? g.z : 0.f; g.w = o.w > 0.f ? g.w : 0.f;
-    } else if (relu == 2) {
+    if (relu == 2) {
       const float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
       g = relu_mask_from_x(g, v, m, is, ww, bb);
+    } else if (relu) {
+      const float4 bb = (relu == 4 && b) ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
+      g = act_mask(g, relu, y, i * 4, v, m, is, ww, bb);
     }
     if (dres) reinterpret_cast<float4 *>(dres)[i] = g;
     float4 o;
@@ -280,7 +309,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__rest
     for (int j = 0; j < 4; ++j) {
       float is = 1.0f / sqrtf(rv[c + j] + eps);
       float t = (o[j] - rm[c + j]) * is * (w ? w[c + j] : 1.f) + (b ? b[c + j] : 0.f) + r4[j];
-      o[j] = relu ? fmaxf(t, 0.f) : t;
+      o[j] = fwd_act(t, relu);
     }
     reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
   }
@@ -333,6 +362,7 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
                           void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
   AS_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: null pointer");
   size_t need = bn_ws_bytes(rows, c);
   if (!ws || ws_bytes < need) {
@@ -362,6 +392,7 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                 float *y, int relu, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(stats && ntiles > 0 && x && y && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
   hipStream_t s = as_stream(stream);
   bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
                                                                    running_mean, running_var, momentum, eps);
@@ -381,6 +412,7 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
                           float *y, int relu, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
   AS_CHECK_ARG(x && y && running_mean && running_var, "bn_fwd_infer: null pointer");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
   hipStream_t s = as_stream(stream);
   int64_t total4 = rows * c / 4;
   bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight,
@@ -406,14 +438,18 @@ int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles,
   return ADAPTSEG_OK;
 }
 
-int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
-                    const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
-                    int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
+                       const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
+                       int relu, int train, float *dweight, float *dbias, void *ws, size_t ws_bytes,
+                       adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
   AS_CHECK_ARG(dy && dx && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
-  AS_CHECK_ARG(!relu || y || train, "bn_bwd: relu without y needs train mode (mask from x)");
-  // relu mode: 1 = mask from the saved output y, 2 = recomputed from x (y == NULL)
-  const int rmode = relu ? (y ? 1 : 2) : 0;
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
+  AS_CHECK_ARG(!relu || y || train, "bn_bwd: activation without y needs train mode (mask from x)");
+  AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
+  // mask mode: ReLU 1 (from the saved output y) / 2 (recomputed from x, y == NULL);
+  // LeakyReLU 3 (from y) / 4 (from x)
+  const int rmode = relu == 0 ? 0 : relu == 1 ? (y ? 1 : 2) : (y ? 3 : 4);
   hipStream_t s = as_stream(stream);
   float *coef = nullptr;
   if (train) {
@@ -430,7 +466,7 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                                                                   partial);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
-                                                                   coef);
+                                                                   coef, dweight, dbias);
     AS_CHECK_LAUNCH("bn_bwd_final");
   }
   int64_t total4 = rows * c / 4;
@@ -442,6 +478,22 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
+                    const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
+                    int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dres, relu, train, nullptr,
+                     nullptr, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,
+                           const float *weight, const float *bias, const float *save_mean,
+                           const float *save_invstd, float *dx, float *dres, int act, float *dweight,
+                           float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(dweight || dbias, "bn_bwd_affine: no affine gradient requested");
+  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dres, act, 1, dweight, dbias,
+                     ws, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -536,3 +536,231 @@ def deeplab_vgg_forward(model, x):
     need_w = any(p.requires_grad for p in model._arena.params)
     grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
     return _DeeplabVGGFn.apply(model._anchors[need_w], x, model, grad)
+
+
+# ---------------------------------------------------------------------------------------
+# The fork's Warper (model/warper.py:216-267) and the prediction warp
+# (model/deeplab_multi.py:238-255).  Encoder: 4x4/2 convs, LeakyReLU(0.2) fused into the first
+# conv's epilogue and into every BN apply (the in-place LeakyReLU of the NEXT block rewrites the
+# stored skip, so the skips are post-LeakyReLU); decoder: ReLU + x2 upsample + skip concat in
+# one pass (up2_relu_cat), 3x3 conv, BN.  All BNs are train-mode with trainable affine params.
+# ---------------------------------------------------------------------------------------
+
+
+def _warper_pidx(model):
+    A = model.arena
+    return A.index_of([p for name, p in model.named_parameters()
+                       if p.requires_grad and not name.startswith("connection.")])
+
+
+class _WarperFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, model, save):
+        ctx.set_materialize_grads(False)
+        training = model.training
+        n, c, h, w = x.shape
+        xs = _input_strides(x)
+        if training:
+            K.add_i64(model._bn_counter)
+        enc, out_conv = model.encoder_blocks()
+        dec, last = model.decoder_blocks()
+        conv_bn = _conv_bn if training else _conv_plain
+        # encoder: s_k = leaky(bn(conv(s_{k-1}))), s_0 = leaky(conv(x))
+        g0 = enc[0][0].geom()
+        s = [K.conv_fwd(g0, x, n, h, w, [enc[0][0].weight], strides=xs, flags=K.EPI_LEAKY)]
+        hw = [g0.out_hw(h, w)]
+        cs, sts = [None], [None]
+        for conv, bn in enc[1:]:
+            g = conv.geom()
+            ch, cw = hw[-1]
+            cc, tiles = conv_bn(g, s[-1], n, ch, cw, conv.weight)
+            y, st = bn_forward(bn, cc, None, K.ACT_LEAKY, training, tiles)
+            s.append(y)
+            cs.append(cc)
+            sts.append(st)
+            hw.append(g.out_hw(ch, cw))
+        # The in-place ReLUs of DecoderInput / DecoderOutput rewrite the latent clone and the last
+        # decoder BN output that SkipConnectionDecode returns in warp_list (warper.py:130-144):
+        # both are produced post-ReLU here (the ReLU epilogue of the latent conv, the BN apply of
+        # the last block).  Nothing reads the pre-ReLU values: the next pass applies the ReLU
+        # anyway and its backward masks on the same sign.
+        go = out_conv.geom()
+        latent = K.conv_fwd(go, s[-1], n, hw[-1][0], hw[-1][1], [out_conv.weight], flags=K.EPI_RELU)
+        lh, lw = go.out_hw(*hw[-1])
+        # decoder: d_i = bn(conv(up2(relu(cat(skip, d_{i-1}))))), skip = s[L-1-i]
+        L = len(s) + 1
+        us, dcs, ds, dsts = [], [], [], []
+        cur, ch, cw = latent, lh, lw
+        for i, (conv, bn) in enumerate(dec):
+            skip = None if i == 0 else s[L - 1 - i]
+            u = K.up2_relu_cat_fwd(skip, cur)
+            ch, cw = 2 * ch, 2 * cw
+            cc, tiles = conv_bn(conv.geom(), u, n, ch, cw, conv.weight)
+            act = K.ACT_RELU if i == len(dec) - 1 else K.ACT_NONE
+            y, st = bn_forward(bn, cc, None, act, training, tiles)
+            us.append(u)
+            dcs.append(cc)
+            ds.append(y)
+            dsts.append(st)
+            cur = y
+        u = K.up2_relu_cat_fwd(None, cur)
+        us.append(u)
+        ch, cw = 2 * ch, 2 * cw
+        flow = K.conv_fwd(last.geom(), u, n, ch, cw, [last.weight], [last.bias])
+        wl = [K.as_nchw(latent)] + [K.as_nchw(t) for t in ds]
+        ctx.mark_non_differentiable(*wl)
+        if save:
+            ctx.model, ctx.x, ctx.xs, ctx.dims = model, x, xs, (n, h, w)
+            ctx.s, ctx.cs, ctx.sts, ctx.hw = s, cs, sts, hw
+            ctx.latent, ctx.lhw = latent, (lh, lw)
+            ctx.us, ctx.dcs, ctx.ds, ctx.dsts = us, dcs, ds, dsts
+            ctx.need_w = anchor.requires_grad
+            ctx.training = training
+        return (K.as_nchw(flow), *wl)
+
+    @staticmethod
+    def backward(ctx, gflow, *_unused):
+        nones = (None,) * 4
+        if gflow is None:
+            return nones
+        if not ctx.training:
+            raise NotImplementedError("Warper backward is implemented for train-mode BatchNorm "
+                                      "(the reference trains it with WarpModel.train(), train:217-220)")
+        model, need_w = ctx.model, ctx.need_w
+        n, h, w = ctx.dims
+        enc, out_conv = model.encoder_blocks()
+        dec, last = model.decoder_blocks()
+        if need_w:
+            model._arena.claim(_warper_pidx(model))
+        g = K.nhwc_view(gflow)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        ws = WgradStream(g.device) if need_w else None
+
+        def wgrad(conv, dy, xin, hh, ww, strides=None):
+            if need_w and conv.weight.grad is not None:
+                dbs = [conv.bias.grad] if conv.bias is not None and conv.bias.grad is not None else None
+                _wgrad(ws, conv.geom(), dy, xin, n, hh, ww, [conv.weight.grad], dbs, strides=strides)
+
+        def bn_bwd(bn, dy, y, x, st, act):
+            mean, invstd, _ = st
+            dw = bn.weight.grad if need_w else None
+            db = bn.bias.grad if need_w else None
+            if dw is None and db is None:
+                return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=act, dx=dy, bias=bn.bias)
+            return K.bn_bwd_affine(dy, y, x, bn.weight, bn.bias, mean, invstd, act, dw, db, dx=dy)
+
+        s, ds, us = ctx.s, ctx.ds, ctx.us
+        L = len(s) + 1
+        # DecoderOutput conv (+bias) on u_last at full resolution
+        wgrad(last, g, us[-1], h, w)
+        du = K.conv_dgrad(last.geom(), g, n, h, w, [last.weight])
+        del g
+        _, dd = K.up2_relu_cat_bwd(None, ds[-1], du)
+        del du
+        us[-1] = None
+        skip_grads = [None] * len(s)
+        for i in reversed(range(len(dec))):
+            conv, bn = dec[i]
+            uh, uw = ctx.us[i].shape[1], ctx.us[i].shape[2]
+            bn_bwd(bn, dd, None, ctx.dcs[i], ctx.dsts[i], K.ACT_NONE)
+            wgrad(conv, dd, us[i], uh, uw)
+            du = K.conv_dgrad(conv.geom(), dd, n, uh, uw, [conv.weight])
+            del dd
+            us[i] = ctx.dcs[i] = None
+            skip = None if i == 0 else s[L - 1 - i]
+            src = ctx.latent if i == 0 else ds[i - 1]
+            dskip, dd = K.up2_relu_cat_bwd(skip, src, du)
+            del du
+            if i > 0:
+                skip_grads[L - 1 - i] = dskip
+        dlat = dd
+        # EncoderOutput conv: its input s[-1] also feeds the first decoder skip
+        hh, ww = ctx.hw[-1]
+        wgrad(out_conv, dlat, s[-1], hh, ww)
+        gk = K.conv_dgrad(out_conv.geom(), dlat, n, hh, ww, [out_conv.weight],
+                          out=skip_grads[-1], flags=K.EPI_ACCUMULATE if skip_grads[-1] is not None else 0)
+        del dlat
+        for k in reversed(range(1, len(s))):
+            conv, bn = enc[k]
+            bn_bwd(bn, gk, s[k], ctx.cs[k], ctx.sts[k], K.ACT_LEAKY)
+            ph, pw = ctx.hw[k - 1]
+            wgrad(conv, gk, s[k - 1], ph, pw)
+            if k - 1 >= 1:
+                prev = skip_grads[k - 1]
+                gk = K.conv_dgrad(conv.geom(), gk, n, ph, pw, [conv.weight], out=prev,
+                                  flags=K.EPI_ACCUMULATE if prev is not None else 0)
+            else:   # s_0 = leaky(conv0(x)): fold leaky'(s_0) into the data-gradient epilogue
+                gk = K.conv_dgrad(conv.geom(), gk, n, ph, pw, [conv.weight], aux=s[0])
+            ctx.cs[k] = None
+        conv0 = enc[0][0]
+        wgrad(conv0, gk, ctx.x, h, w, strides=ctx.xs)
+        dx = None
+        if ctx.needs_input_grad[1]:
+            dx = K.as_nchw(K.conv_dgrad(conv0.geom(), gk, n, h, w, [conv0.weight]))
+        ctx.x = ctx.s = ctx.latent = None
+        if ws is not None:
+            ws.join()
+        return None, dx, None, None
+
+
+def warper_forward(model, x):
+    """Warper.forward(pose) (model/warper.py:263-267) on the HIP engine -> (flow, warp_list)."""
+    if not x.is_cuda:
+        raise RuntimeError("adaptsegnet_amd Warper runs on the HIP engine only; "
+                           f"got input on {x.device}")
+    if x.dtype != torch.float32:
+        raise RuntimeError(f"expected float32 input, got {x.dtype}")
+    depth = len(model.encoder_d.down_list) + 1
+    if x.shape[2] % (1 << depth) or x.shape[3] % (1 << depth):
+        raise ValueError(f"Warper: input {tuple(x.shape[2:])} must be divisible by {1 << depth} in "
+                         "both dimensions (the skip connections must match; the reference fails "
+                         "otherwise)")
+    model._ensure_arena(x.device)
+    need_w = any(p.requires_grad for p in model._arena.params)
+    grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
+    outs = _WarperFn.apply(model._anchors[need_w], x, model, grad)
+    return outs[0], list(outs[1:])
+
+
+class _GridWarpFn(torch.autograd.Function):
+    """ResNetMulti.warp on both heads with one warp field (deeplab_multi.py:190-192, 238-255)."""
+
+    @staticmethod
+    def forward(ctx, flow, x1, x2):
+        ctx.set_materialize_grads(False)
+        f = K.nhwc_view(flow)
+        if not f.is_contiguous():
+            f = f.contiguous()
+        a1 = None if x1 is None else K.nhwc_view(x1)
+        a2 = K.nhwc_view(x2)
+        y1, y2 = K.grid_warp_fwd(f, a1, a2)
+        ctx.save = (f, a1, a2)
+        return (None if y1 is None else K.as_nchw(y1)), K.as_nchw(y2)
+
+    @staticmethod
+    def backward(ctx, gy1, gy2):
+        f, a1, a2 = ctx.save
+        need_f, need_1, need_2 = ctx.needs_input_grad
+        g1 = None if gy1 is None or a1 is None else K.nhwc_view(gy1)
+        g2 = None if gy2 is None else K.nhwc_view(gy2)
+        if g1 is not None and not g1.is_contiguous():
+            g1 = g1.contiguous()
+        if g2 is not None and not g2.is_contiguous():
+            g2 = g2.contiguous()
+        if g1 is None and g2 is None:
+            return None, None, None
+        dflow, dx1, dx2 = K.grid_warp_bwd(f, a1, a2, g1, g2, need_dflow=need_f, need_dx1=need_1,
+                                          need_dx2=need_2)
+        ctx.save = None
+        return tuple(None if t is None else K.as_nchw(t) for t in (dflow, dx1, dx2))
+
+
+def grid_warp(flow, x1, x2):
+    """(warp(x1, flow), warp(x2, flow)); x1 may be None."""
+    if flow.shape[0] != x2.shape[0] or flow.shape[2:] != x2.shape[2:] or (x1 is not None and x1.shape != x2.shape):
+        raise ValueError(f"warp: warp field {tuple(flow.shape)} and predictions {tuple(x2.shape)} "
+                         "must share N, H, W")
+    if flow.shape[1] < 2 or flow.shape[1] % 2:
+        raise ValueError("warp: the warp field needs an even number (>= 2) of channels")
+    return _GridWarpFn.apply(flow, x1, x2)

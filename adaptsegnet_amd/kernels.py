@@ -252,7 +252,7 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=
     wp, wsz = _ws_args(_bn_ws(rows, c), x.device)
     check(_lib.lib().adaptseg_bn_fwd_train(
         rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
-        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), 1 if relu else 0,
+        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), int(relu),
         wp, wsz, _stream()), "bn_fwd_train")
     return y, mean, invstd
 
@@ -268,7 +268,7 @@ def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, moment
     check(_lib.lib().adaptseg_bn_fwd_train_tiles(
         rows, c, _p(stats), int(ntiles), _p(x), _p(weight), _p(bias), _p(running_mean),
         _p(running_var), float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y),
-        1 if relu else 0, _stream()), "bn_fwd_train_tiles")
+        int(relu), _stream()), "bn_fwd_train_tiles")
     return y, mean, invstd
 
 
@@ -277,7 +277,7 @@ def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu
     y = torch.empty_like(x) if out is None else out
     check(_lib.lib().adaptseg_bn_fwd_infer(
         rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps),
-        _p(res), _p(y), 1 if relu else 0, _stream()), "bn_fwd_infer")
+        _p(res), _p(y), int(relu), _stream()), "bn_fwd_infer")
     return y
 
 
@@ -290,7 +290,7 @@ def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=
     wp, wsz = _ws_args(_bn_ws(rows, c) if train else 0, dy.device)
     check(_lib.lib().adaptseg_bn_bwd(
         rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx),
-        _p(dres), 1 if relu else 0, 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+        _p(dres), int(relu), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
     return dx
 
 
@@ -306,6 +306,81 @@ def bn_bwd_tiles(dy, x, weight, bias, mean, invstd, sums, dx=None, dres=None):
         rows, c, _p(partial), nt, _p(dy), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(coef),
         _p(dx), _p(dres), _stream()), "bn_bwd_tiles")
     return dx
+
+
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2   # the BN entry points' activation codes
+
+
+def bn_bwd_affine(dy, y, x, weight, bias, mean, invstd, act, dweight=None, dbias=None, dx=None):
+    """Train-mode BN backward with trainable affine parameters: dx, plus dweight/dbias
+    accumulated (sum g*xhat, sum g).  act: ACT_NONE / ACT_RELU / ACT_LEAKY (mask from y, or
+    from x when y is None).  dx may alias dy."""
+    rows, c = dy.numel() // dy.shape[-1], dy.shape[-1]
+    if dx is None:
+        dx = torch.empty_like(dy)
+    wp, wsz = _ws_args(_bn_ws(rows, c), dy.device)
+    check(_lib.lib().adaptseg_bn_bwd_affine(
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), None,
+        int(act), _p(dweight), _p(dbias), wp, wsz, _stream()), "bn_bwd_affine")
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# Warper: decoder input (ReLU + x2 upsample + skip concat) and the prediction warp
+# ---------------------------------------------------------------------------------------
+def up2_relu_cat_fwd(s, d):
+    """NHWC up2(relu(cat(s, d))) at twice the resolution; s may be None."""
+    n, h, w, cd = d.shape
+    cs = 0 if s is None else s.shape[-1]
+    out = torch.empty((n, 2 * h, 2 * w, cs + cd), device=d.device, dtype=torch.float32)
+    check(_lib.lib().adaptseg_up2_relu_cat_fwd(n, h, w, cs, cd, _p(s), _p(d), _p(out), _stream()),
+          "up2_relu_cat_fwd")
+    return out
+
+
+def up2_relu_cat_bwd(s, d, dout, ds=None, dd=None):
+    """(ds, dd) = masked split of up2^T(dout); ds is None when s is None."""
+    n, h, w, cd = d.shape
+    cs = 0 if s is None else s.shape[-1]
+    if dd is None:
+        dd = torch.empty_like(d)
+    if s is not None and ds is None:
+        ds = torch.empty_like(s)
+    check(_lib.lib().adaptseg_up2_relu_cat_bwd(n, h, w, cs, cd, _p(s), _p(d), _p(dout), _p(ds), _p(dd),
+                                               _stream()), "up2_relu_cat_bwd")
+    return ds, dd
+
+
+def grid_warp_fwd(flow, x1, x2):
+    """ResNetMulti.warp of both heads (NHWC [n,h,w,c]; x1 may be None) by one NHWC warp field."""
+    n, h, w, c = x2.shape
+    fc = flow.shape[-1]
+    y1 = None if x1 is None else torch.empty_like(x1)
+    y2 = torch.empty_like(x2)
+    check(_lib.lib().adaptseg_grid_warp_fwd(n, c, h, w, fc, _p(flow), _p(x1), _p(x2), _p(y1), _p(y2),
+                                            _stream()), "grid_warp_fwd")
+    return y1, y2
+
+
+def grid_warp_bwd(flow, x1, x2, dy1, dy2, need_dflow=True, need_dx1=True, need_dx2=True):
+    """-> (dflow, dx1, dx2); entries not requested (or without their dy) are None."""
+    ref = dy2 if dy2 is not None else dy1
+    n, h, w, c = ref.shape
+    fc = flow.shape[-1]
+    dflow = torch.empty_like(flow) if need_dflow else None
+    dx1 = torch.empty_like(dy1) if (need_dx1 and dy1 is not None) else None
+    dx2 = torch.empty_like(dy2) if (need_dx2 and dy2 is not None) else None
+    nbytes = 0
+    if dx1 is not None or dx2 is not None:
+        b = ctypes.c_size_t(0)
+        check(_lib.lib().adaptseg_grid_warp_bwd_workspace_size(n, c, h, w, ctypes.byref(b)),
+              "grid_warp_bwd_workspace_size")
+        nbytes = b.value
+    wp, wsz = _ws_args(nbytes, ref.device)
+    check(_lib.lib().adaptseg_grid_warp_bwd(
+        n, c, h, w, fc, _p(flow), _p(x1 if dy1 is not None else None), _p(x2 if dy2 is not None else None),
+        _p(dy1), _p(dy2), _p(dflow), _p(dx1), _p(dx2), wp, wsz, _stream()), "grid_warp_bwd")
+    return dflow, dx1, dx2
 
 
 # ---------------------------------------------------------------------------------------

@@ -13,10 +13,10 @@ Reference semantics kept (file:line):
   get_1x_lr_params_NOscale / get_10x_lr_params        :196-231
   optim_parameters (1x and 10x LR groups)            :233-235
   DeeplabMulti(num_classes)                          :258-260
-Deliberate differences: ``forward`` accepts ``input_size=None`` (then the input's own
-(W, H) is used — the reference's multi-level call site train_gta2cityscapes_multi.py:597
-omits it and raises), and ``warper`` (the fork's CUDA-only grid_sample warp,
-:238-255) is out of scope and raises if given.
+  ResNetMulti.warp (tanh + linspace grid, clamp, grid_sample)  :238-255
+Deliberate difference: ``forward`` accepts ``input_size=None`` (then the input's own (W, H) is
+used — the reference's multi-level call site train_gta2cityscapes_multi.py:597 omits it and
+raises).
 """
 from __future__ import annotations
 
@@ -171,12 +171,17 @@ class ResNetMulti(nn.Module):
         return self._arena
 
     def forward(self, x, input_size=None, warper=None):
-        if warper is not None:
-            raise NotImplementedError("the fork's grid_sample warper (model/deeplab_multi.py:238-255) "
-                                      "is outside the adversarial hot path")
         if input_size is None:
             input_size = (x.shape[3], x.shape[2])
-        return engine.deeplab_multi_forward(self, x, input_size)
+        x1_up, x2_up = engine.deeplab_multi_forward(self, x, input_size)
+        if warper is not None:   # :190-192: both upsampled heads warped by the same field
+            x1_up, x2_up = engine.grid_warp(warper, x1_up, x2_up)
+        return x1_up, x2_up
+
+    @staticmethod
+    def warp(input, warper):
+        """ResNetMulti.warp (model/deeplab_multi.py:238-255) on the HIP engine."""
+        return engine.grid_warp(warper, None, input)[1]
 
 
 def DeeplabMulti(num_classes=21):

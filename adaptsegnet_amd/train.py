@@ -10,8 +10,14 @@ Resolved reference gaps:
     reference; here source predictions are upsampled to ``input_size`` and target ones to
     ``input_size_target`` (``target_size='target'``), or to the source size as the fork's
     single-level branch does (:421, ``target_size='source'``, the single-level default);
-  * ``SOURCE_ONLY = True`` (:24) is not hard-wired: the adversarial step always runs;
-  * the fork's warper (:217-220,401-405) is out of scope.
+  * ``SOURCE_ONLY = True`` (:24) is not hard-wired: ``StepConfig.level`` selects the
+    adversarial steps or ``"source-only"`` (:259-286, segmentation loss only);
+  * the fork's warper (:217-220, 271-275, 401-405) is applied when a ``Warper`` is given: its
+    field warps the source predictions (source-only and single-level).  The reference's
+    single-level branch reuses the source field for the target prediction (:421) and then
+    crashes in the target backward (the field's graph was freed by the source backward); here
+    the target is warped by the same field, detached.  The warper's parameters are in no
+    optimiser (:244,347,532), so their gradients only accumulate, as in the reference.
 Differences that do not change results: loss scalings (``lambda * loss / iter_size``) are
 passed as the initial gradient of ``backward`` instead of multiplying the loss tensors, the
 constant label tensors (:621, ...) are folded into the loss kernels, and the per-loss
@@ -36,7 +42,7 @@ from .optim import SGD, Adam, lr_poly
 
 @dataclass
 class StepConfig:
-    level: str = "single-level"          # or "multi-level"
+    level: str = "single-level"          # or "multi-level", "source-only"
     gan: str = "Vanilla"                 # "Vanilla" (BCEWithLogits) or "LS" (MSE)
     num_classes: int = 19
     input_size: tuple = (1024, 512)      # (W, H) of source images
@@ -77,15 +83,23 @@ class StepLosses:
 class AdaptSegTrainer:
     """Owns the optimisers and runs one adversarial iteration per ``step()`` call."""
 
-    def __init__(self, model, model_D1, model_D2, cfg: StepConfig, process_group=None):
+    def __init__(self, model, model_D1, model_D2, cfg: StepConfig, process_group=None, warper=None):
         self.model, self.D1, self.D2, self.cfg = model, model_D1, model_D2, cfg
+        self.warper = warper
+        if cfg.level not in ("single-level", "multi-level", "source-only"):
+            raise ValueError(f"unknown level {cfg.level!r}")
         if cfg.level == "multi-level" and model_D1 is None:
             raise ValueError("multi-level needs model_D1")
         if cfg.level == "multi-level" and getattr(model, "single_output", False):
             raise ValueError("multi-level needs a two-head generator (DeeplabMulti)")
+        if cfg.level != "source-only" and model_D2 is None:
+            raise ValueError(f"{cfg.level} needs model_D2")
+        if warper is not None and (cfg.level == "multi-level" or getattr(model, "single_output", False)):
+            raise ValueError("the warper applies to DeeplabMulti's source-only and single-level steps "
+                             "(train_gta2cityscapes_multi.py:271-275, 401-405)")
         self.opt = SGD(model, cfg.learning_rate, cfg.momentum, cfg.weight_decay)
         self.opt_D1 = Adam(model_D1, cfg.learning_rate_D, betas=(0.9, 0.99)) if model_D1 is not None else None
-        self.opt_D2 = Adam(model_D2, cfg.learning_rate_D, betas=(0.9, 0.99))
+        self.opt_D2 = Adam(model_D2, cfg.learning_rate_D, betas=(0.9, 0.99)) if model_D2 is not None else None
         self.kind = F.BCE if cfg.gan == "Vanilla" else F.MSE
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -198,16 +212,20 @@ class AdaptSegTrainer:
         c = self.cfg
         L = StepLosses()
         self.opt.zero_grad()
-        self.opt_D2.zero_grad()
-        if self.opt_D1 is not None:
-            self.opt_D1.zero_grad()
+        for o in (self.opt_D1, self.opt_D2):
+            if o is not None:
+                o.zero_grad()
         self.adjust_learning_rate(i_iter)
         inv = 1.0 / c.iter_size
         tsize = self._target_size()
         batches = list(batches)
         self._pending = []
-        for idx, (images, labels, images_t) in enumerate(batches):
+        for idx, batch in enumerate(batches):
             g_done = (lambda: self._start_sync((self.model,))) if idx == len(batches) - 1 else None
+            if c.level == "source-only":
+                self._sub_source_only(batch[0], batch[1], inv, L, g_done)
+                continue
+            images, labels, images_t = batch
             if c.level == "single-level":
                 self._sub_single(images, labels, images_t, inv, tsize, L, g_done)
             else:
@@ -218,30 +236,45 @@ class AdaptSegTrainer:
         self._finish_sync()
         gs = 1.0 / self.world
         self.opt.step(grad_scale=gs)
-        if self.opt_D1 is not None:
-            self.opt_D1.step(grad_scale=gs)
-        self.opt_D2.step(grad_scale=gs)
+        for o in (self.opt_D1, self.opt_D2):
+            if o is not None:
+                o.step(grad_scale=gs)
         return L
 
-    def _pred_single(self, images, size):
-        """The single-level prediction at ``size`` = (W, H): DeeplabMulti's second head, or a
-        single-map model (DeeplabVGG, config c4) followed by the caller-side ``interp``."""
+    def _pred_single(self, images, size, flow=None):
+        """The single-level prediction at ``size`` = (W, H): DeeplabMulti's second head (warped
+        by ``flow`` when given), or a single-map model (DeeplabVGG, config c4) followed by the
+        caller-side ``interp``."""
         if getattr(self.model, "single_output", False):
             return F.interp(self.model(images), (size[1], size[0]))
-        return self.model(images, size)[1]
+        return self.model(images, size, flow)[1]
+
+    def _flow(self, images):
+        return None if self.warper is None else self.warper(images)[0]
+
+    def _sub_source_only(self, images, labels, inv, L, g_done=None):
+        """train_gta2cityscapes_multi.py:259-286: warper (if any), segmentation loss on the
+        second head, backward; the step is the generator's SGD only."""
+        pred2 = self._pred_single(images, self.cfg.input_size, self._flow(images))
+        loss_seg2 = F.cross_entropy2d(pred2, labels, self.cfg.ignore_label)
+        self._backward([loss_seg2], [inv])
+        L.add("loss_seg2", loss_seg2, inv)
+        if g_done is not None:
+            g_done()
 
     def _sub_single(self, images, labels, images_t, inv, tsize, L, g_done=None):
         """train_gta2cityscapes_multi.py:385-461."""
         c, D2 = self.cfg, self.D2
         self._set_requires_grad(D2, False)
-        pred2 = self._pred_single(images, c.input_size)
+        flow = self._flow(images)
+        pred2 = self._pred_single(images, c.input_size, flow)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         ov = self._overlap_begin(pred2.device)
         self._backward([loss_seg2], [inv])
         L.add("loss_seg2", loss_seg2, inv)
 
         with self._target_ctx(ov):
-            pred_target2 = self._pred_single(images_t, tsize)
+            pred_target2 = self._pred_single(images_t, tsize, None if flow is None else flow.detach())
             d_out2 = D2(F.softmax2d(pred_target2))
             loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
             self._join_source(ov)

@@ -138,7 +138,9 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
 int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes);
 
 /* x,y: [rows][c].  Writes save_mean/save_invstd[c]; updates running stats (may be NULL).
-   y = (x-mean)*invstd*weight + bias (+ res) then ReLU if relu != 0. */
+   y = act((x-mean)*invstd*weight + bias (+ res)).  The `relu` argument of every BN entry point
+   selects the activation: 0 none, 1 ReLU, 2 LeakyReLU(0.2) (the warper's DownConvolution,
+   model/custom_layers.py:83-96). */
 int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight,
                           const float *bias, float *running_mean, float *running_var,
                           float momentum, float eps, float *save_mean, float *save_invstd,
@@ -159,7 +161,7 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
                           float eps, const float *res, float *y, int relu,
                           adaptseg_stream_t stream);
 
-/* Backward of bn_fwd_train.  g = dy * (relu ? (y > 0) : 1).
+/* Backward of bn_fwd_train.  g = dy * act'(y) (relu: 0 none, 1 ReLU, 2 LeakyReLU(0.2)).
    dx = weight*invstd*(g - mean(g) - xhat*mean(g*xhat)); dres = g if dres != NULL.
    y == NULL with relu (train mode, BN without residual): the mask is recomputed from x as
    (x-mean)*invstd*weight + bias > 0 — one tensor read less in both passes.
@@ -168,6 +170,15 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     const float *weight, const float *bias, const float *save_mean,
                     const float *save_invstd, float *dx, float *dres, int relu, int train,
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+
+/* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's
+   NaiveConvolution norms, model/custom_layers.py:25-33): additionally dbias[c] += sum(g),
+   dweight[c] += sum(g * xhat) (accumulated, as torch's AccumulateGrad; either may be NULL).
+   act: 0 none, 1 ReLU, 2 LeakyReLU(0.2); its mask comes from y, or from x when y == NULL. */
+int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,
+                           const float *weight, const float *bias, const float *save_mean,
+                           const float *save_invstd, float *dx, float *dres, int act, float *dweight,
+                           float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd (train mode, ReLU mask recomputed from x) from the row-tile sums of
    adaptseg_conv2d_bwd_data_bnsums: a deterministic fp64 finalize into coef [2][c] (caller-
@@ -273,6 +284,37 @@ int adaptseg_sgd_step(int64_t n, float *param, const float *grad, float *mom, fl
 int adaptseg_adam_step(int64_t n, float *param, const float *grad, float *exp_avg,
                        float *exp_avg_sq, float lr, float beta1, float beta2, float eps,
                        int step, float grad_scale, adaptseg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* The fork's Warper: model/warper.py:216-267, its decoder blocks  */
+/* model/custom_layers.py:117-188 and the prediction warp model/deeplab_multi.py:238-255.  */
+/* ------------------------------------------------------------------------------------ */
+/* out[n][2h][2w][cs+cd] = Upsample(x2, bilinear, align_corners=False)(ReLU(cat(s, d), dim=C)):
+   one decoder block's input (SkipConnectionDecode.forward, model/warper.py:130-144, then
+   UpConvolution's ReLU(inplace) + nn.Upsample).  s [n][h][w][cs] may be NULL with cs = 0 (the
+   DecoderInput / DecoderOutput blocks); d [n][h][w][cd].  cs, cd multiples of 4. */
+int adaptseg_up2_relu_cat_fwd(int n, int h, int w, int cs, int cd, const float *s, const float *d,
+                              float *out, adaptseg_stream_t stream);
+/* Adjoint: ds = dS * (s > 0), dd = dD * (d > 0) where (dS, dD) = the channel split of
+   Upsample^T(dout); written (not accumulated), fixed summation order. */
+int adaptseg_up2_relu_cat_bwd(int n, int h, int w, int cs, int cd, const float *s, const float *d,
+                              const float *dout, float *ds, float *dd, adaptseg_stream_t stream);
+/* ResNetMulti.warp: grid = clamp(tanh(flow[..., last channel pair]) + meshgrid(linspace(-1, 1,
+   w), linspace(-1, 1, h)), -1, 1); y = grid_sample(x, grid) (bilinear, zeros padding,
+   align_corners=False).  x, y NHWC [n][h][w][c]; flow NHWC [n][h][w][fc] (fc even).  Two
+   inputs share one grid (the two heads, deeplab_multi.py:190-192); x1/y1 may be NULL. */
+int adaptseg_grid_warp_fwd(int n, int c, int h, int w, int fc, const float *flow, const float *x1,
+                           const float *x2, float *y1, float *y2, adaptseg_stream_t stream);
+int adaptseg_grid_warp_bwd_workspace_size(int n, int c, int h, int w, size_t *bytes);
+/* dflow (written; [n][h][w][fc], zero outside the last pair) = the warp field's gradient summed
+   over both heads (needs x1/x2 for every given dy); dx1/dx2 (written, optional) = the input
+   gradients.  The input gradient is a data-dependent scatter: it accumulates in 64-bit fixed
+   point (integer atomics, so the result is independent of scheduling), with the scale chosen
+   per call from max|dy| so no sum can overflow; rounding <= 2^-42 * max|dy| at 1024x2048. */
+int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow, const float *x1,
+                           const float *x2, const float *dy1, const float *dy2, float *dflow,
+                           float *dx1, float *dx2, void *ws, size_t ws_bytes,
+                           adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Plumbing kernels.                                                                      */
