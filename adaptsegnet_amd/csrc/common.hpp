@@ -75,7 +75,8 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 constexpr int kTimingMemBase = 1000;
 enum TimingMemId {
   kTUpsampleFwd = 1000, kTUpsampleBwd = 1001, kTSoftmaxFwd = 1002, kTSoftmaxBwd = 1003,
-  kTCeFwd = 1004, kTCeBwd = 1005, kTBnApply = 1006, kTBnBwdApply = 1007
+  kTCeFwd = 1004, kTCeBwd = 1005, kTBnApply = 1006, kTBnBwdApply = 1007,
+  kTUp2Fwd = 1008, kTUp2Bwd = 1009, kTWarpFwd = 1010, kTWarpDflow = 1011, kTWarpScatter = 1012
 };
 void timing_begin(int kernel_id, hipStream_t s, double units, int *slot);
 void timing_end(int slot, hipStream_t s);

@@ -355,7 +355,10 @@ int adaptseg_up2_relu_cat_fwd(int n, int h, int w, int cs, int cd, const float *
                "up2_relu_cat_fwd: bad shape (cs=%d cd=%d: multiples of 4, cd > 0)", cs, cd);
   AS_CHECK_ARG(d && out && (cs == 0 || s), "up2_relu_cat_fwd: null pointer");
   const int64_t total = (int64_t)n * 4 * h * w * ((cs + cd) / 4);
+  int slot;  // inputs once, the 4x output once
+  timing_begin(kTUp2Fwd, as_stream(stream), 20.0 * n * h * w * (cs + cd), &slot);
   up2_relu_cat_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, h, w, cs, cd, s, d, out);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("up2_relu_cat_fwd");
   return ADAPTSEG_OK;
 }
@@ -366,7 +369,10 @@ int adaptseg_up2_relu_cat_bwd(int n, int h, int w, int cs, int cd, const float *
                "up2_relu_cat_bwd: bad shape (cs=%d cd=%d)", cs, cd);
   AS_CHECK_ARG(d && dout && dd && (cs == 0 || (s && ds)), "up2_relu_cat_bwd: null pointer");
   const int64_t total = (int64_t)n * h * w * ((cs + cd) / 4);
+  int slot;  // dout (4x) + the mask sources in, ds/dd out
+  timing_begin(kTUp2Bwd, as_stream(stream), 24.0 * n * h * w * (cs + cd), &slot);
   up2_relu_cat_bwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, h, w, cs, cd, s, d, dout, ds, dd);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("up2_relu_cat_bwd");
   return ADAPTSEG_OK;
 }
@@ -377,7 +383,10 @@ int adaptseg_grid_warp_fwd(int n, int c, int h, int w, int fc, const float *flow
   AS_CHECK_ARG((int64_t)h * w < (1ll << 30), "grid_warp_fwd: h*w too large");
   AS_CHECK_ARG(flow && (x1 || x2) && (!x1 || y1) && (!x2 || y2), "grid_warp_fwd: null pointer");
   const int64_t total = (int64_t)n * h * w * c;
+  int slot;  // the field, each head's input and output once
+  timing_begin(kTWarpFwd, as_stream(stream), 4.0 * n * h * w * (2 + 2 * c * ((x1 ? 1 : 0) + (x2 ? 1 : 0))), &slot);
   grid_warp_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, fc, flow, x1, x2, y1, y2);
+  timing_end(slot, as_stream(stream));
   AS_CHECK_LAUNCH("grid_warp_fwd");
   return ADAPTSEG_OK;
 }
@@ -399,8 +408,11 @@ int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow
   hipStream_t s = as_stream(stream);
   const int64_t total = (int64_t)n * h * w * c;
   if (dflow) {
+    int slot;  // field in and out, x and dy of each head once
+    timing_begin(kTWarpDflow, s, 4.0 * n * h * w * (4 + 2 * c * ((dy1 ? 1 : 0) + (dy2 ? 1 : 0))), &slot);
     grid_warp_dflow_kernel<<<grid1d((int64_t)n * h * w), 256, 0, s>>>(n, c, h, w, fc, flow, x1, x2, dy1, dy2,
                                                                        dflow);
+    timing_end(slot, s);
     AS_CHECK_LAUNCH("grid_warp_dflow");
   }
   if (dx1 || dx2) {
@@ -416,6 +428,8 @@ int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow
       const float *dy = head ? dy2 : dy1;
       float *dx = head ? dx2 : dx1;
       if (!dx) continue;
+      int slot;  // algorithmic: the field and dy in, dx out (accumulator passes not counted)
+      timing_begin(kTWarpScatter, s, 4.0 * n * h * w * (2 + 2 * c), &slot);
       if (hipMemsetAsync(ws, 0, need, s) != hipSuccess) {
         set_error("grid_warp_bwd: hipMemsetAsync failed");
         return ADAPTSEG_ERR_HIP;
@@ -425,6 +439,7 @@ int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow
       grid_scatter_kernel<<<grid1d(total), 256, 0, s>>>(n, c, h, w, fc, flow, dy, mbits, acc);
       AS_CHECK_LAUNCH("grid_warp_scatter");
       fixed_to_float_kernel<<<grid1d(total), 256, 0, s>>>(total, h * w, acc, mbits, dx);
+      timing_end(slot, s);
       AS_CHECK_LAUNCH("grid_warp_fixed_to_float");
     }
   }

@@ -344,7 +344,9 @@ int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
 /* HBM-bound kernels (the interp / loss / BN passes): when enabled, every launch of upsample
    fwd (id 1000) / bwd (1001), softmax fwd (1002) / bwd (1003), cross-entropy fwd (1004) / bwd
-   (1005), BN apply (1006) / backward apply (1007) is bracketed the same way with its
+   (1005), BN apply (1006) / backward apply (1007), the warper's up2_relu_cat fwd (1008) / bwd
+   (1009), grid warp fwd (1010) / field gradient (1011) / input-gradient scatter (1012, all of its
+   passes) is bracketed the same way with its
    ALGORITHMIC bytes (compulsory reads + writes at the op interface) as units. */
 int adaptseg_timing_enable_mem(int enable);
 int adaptseg_timing_read_id(int kernel_id, double *total_ms, double *total_units, int64_t *launches);
