@@ -337,9 +337,14 @@ void set_splits(Plan &pl) {
   static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob (512 vs 1024: +1.7 % at c2)
   const int target = pl.mode == MODE_WGRAD ? wg_target : 512;
   const int split_below = pl.mode == MODE_WGRAD ? target : 256;
+  // Rounding: the blocks of a split grid are equal work, so the grid takes (the most blocks
+  // any CU runs) x (one block's K range).  tiles * splits must therefore not overshoot a
+  // multiple of the CU count: ceil(512 / 36) = 15 splits puts 3 blocks on 28 CUs (0.2 units)
+  // where 14 puts at most 2 on every CU (0.143).  Round down (A/B knob: ADAPTSEG_EXP_SPLITCEIL).
+  static const bool split_ceil = getenv("ADAPTSEG_EXP_SPLITCEIL") != nullptr;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = (int)ceil_div(target, pl.tiles);
+    splits = split_ceil ? (int)ceil_div(target, pl.tiles) : std::max(1, target / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
