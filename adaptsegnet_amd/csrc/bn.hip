@@ -14,7 +14,7 @@
 namespace adaptseg {
 
 // ReLU mask without reading y: y > 0  <=>  (x - mean)*invstd*w + b > 0, evaluated with the
-// same expression bn_apply_kernel uses (valid for BNs without a residual input).
+// same expression bn_apply2d_kernel uses (valid for BNs without a residual input).
 __device__ __forceinline__ float bn_affine(float v, float m, float is, float w, float b) {
   return (v - m) * is * w + b;
 }
@@ -222,75 +222,6 @@ __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float
   if (dweight) dweight[c] += (float)(s2 * (double)invstd[c]);
 }
 
-__global__ void bn_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
-                                const float *__restrict__ mean, const float *__restrict__ invstd,
-                                const float *__restrict__ w, const float *__restrict__ b,
-                                const float *__restrict__ res, float *__restrict__ y, int relu) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int c = (int)((i * 4) % C);
-    float4 v = reinterpret_cast<const float4 *>(x)[i];
-    float4 m = *reinterpret_cast<const float4 *>(mean + c);
-    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
-    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
-    float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
-    float4 o;
-    o.x = bn_affine(v.x, m.x, is.x, ww.x, bb.x);
-    o.y = bn_affine(v.y, m.y, is.y, ww.y, bb.y);
-    o.z = bn_affine(v.z, m.z, is.z, ww.z, bb.z);
-    o.w = bn_affine(v.w, m.w, is.w, ww.w, bb.w);
-    if (res) {
-      float4 r = reinterpret_cast<const float4 *>(res)[i];
-      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
-    }
-    if (relu) {
-      o.x = fwd_act(o.x, relu); o.y = fwd_act(o.y, relu); o.z = fwd_act(o.z, relu); o.w = fwd_act(o.w, relu);
-    }
-    reinterpret_cast<float4 *>(y)[i] = o;
-  }
-}
-
-// dx / dres may alias dy (in-place gradient): each element is read before it is written.
-__global__ void bn_bwd_apply_kernel(int64_t total4, int C, const float *dy,
-                                    const float *__restrict__ y, const float *__restrict__ x,
-                                    const float *__restrict__ w, const float *__restrict__ b,
-                                    const float *__restrict__ mean,
-                                    const float *__restrict__ invstd, const float *__restrict__ coef,
-                                    float *dx, float *dres, int relu, int train) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int c = (int)((i * 4) % C);
-    float4 g = reinterpret_cast<const float4 *>(dy)[i];
-    float4 is = *reinterpret_cast<const float4 *>(invstd + c);
-    float4 ww = w ? *reinterpret_cast<const float4 *>(w + c) : make_float4(1, 1, 1, 1);
-    float4 v = make_float4(0, 0, 0, 0), m = v;
-    if (train) {
-      v = reinterpret_cast<const float4 *>(x)[i];
-      m = *reinterpret_cast<const float4 *>(mean + c);
-    }
-    if (relu == 2) {
-      const float4 bb = b ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
-      g = relu_mask_from_x(g, v, m, is, ww, bb);
-    } else if (relu) {
-      const float4 bb = (relu == 4 && b) ? *reinterpret_cast<const float4 *>(b + c) : make_float4(0, 0, 0, 0);
-      g = act_mask(g, relu, y, i * 4, v, m, is, ww, bb);
-    }
-    if (dres) reinterpret_cast<float4 *>(dres)[i] = g;
-    float4 o;
-    if (train) {
-      float4 mg = *reinterpret_cast<const float4 *>(coef + c);
-      float4 mgx = *reinterpret_cast<const float4 *>(coef + C + c);
-      o.x = ww.x * is.x * (g.x - mg.x - (v.x - m.x) * is.x * mgx.x);
-      o.y = ww.y * is.y * (g.y - mg.y - (v.y - m.y) * is.y * mgx.y);
-      o.z = ww.z * is.z * (g.z - mg.z - (v.z - m.z) * is.z * mgx.z);
-      o.w = ww.w * is.w * (g.w - mg.w - (v.w - m.w) * is.w * mgx.w);
-    } else {
-      o.x = g.x * ww.x * is.x; o.y = g.y * ww.y * is.y; o.z = g.z * ww.z * is.z; o.w = g.w * ww.w * is.w;
-    }
-    reinterpret_cast<float4 *>(dx)[i] = o;
-  }
-}
-
 __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
@@ -313,6 +244,135 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__rest
     }
     reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
   }
+}
+
+// Channel-major apply passes: a block is tc channel quads x (256/tc) row lanes, so a thread
+// loads its channels' parameters once and walks rows (no per-element channel modulo); rows
+// are unrolled x4 with all loads issued before any store (dx / dres / y may alias dy / x:
+// every element is still read before it is written, by the same thread).
+constexpr int kApplyUnroll = 4;
+
+__device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+
+__global__ void __launch_bounds__(256)
+bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, const float *__restrict__ mean,
+                  const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
+                  const float *res, float *y, int act) {
+  const int tr = 256 / tc;
+  const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
+  const int c0 = (blockIdx.x * tc + cq) * 4;
+  if (c0 >= C) return;
+  const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  const float4 m = ld4c(mean + c0), is = ld4c(invstd + c0);
+  const float4 ww = w ? ld4c(w + c0) : make_float4(1, 1, 1, 1);
+  const float4 bb = b ? ld4c(b + c0) : make_float4(0, 0, 0, 0);
+  for (int64_t r = r0 + rl; r < r1; r += kApplyUnroll * tr) {
+    float4 v[kApplyUnroll], q[kApplyUnroll];
+#pragma unroll
+    for (int u = 0; u < kApplyUnroll; ++u) {
+      const int64_t ru = r + (int64_t)u * tr;
+      const bool ok = ru < r1;
+      const int64_t e = (ok ? ru : r) * C + c0;
+      v[u] = ld4c(x + e);
+      q[u] = res ? ld4c(res + e) : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kApplyUnroll; ++u) {
+      const int64_t ru = r + (int64_t)u * tr;
+      if (ru >= r1) break;
+      float4 o;
+      o.x = fwd_act(bn_affine(v[u].x, m.x, is.x, ww.x, bb.x) + q[u].x, act);
+      o.y = fwd_act(bn_affine(v[u].y, m.y, is.y, ww.y, bb.y) + q[u].y, act);
+      o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
+      o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
+      st4(y + ru * C + c0, o);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, const float *y, const float *x,
+                      const float *__restrict__ w, const float *__restrict__ b, const float *__restrict__ mean,
+                      const float *__restrict__ invstd, const float *__restrict__ coef, float *dx, float *dres,
+                      int rmode, int train) {
+  const int tr = 256 / tc;
+  const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
+  const int c0 = (blockIdx.x * tc + cq) * 4;
+  if (c0 >= C) return;
+  const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  const float4 z4 = make_float4(0, 0, 0, 0);
+  const float4 is = ld4c(invstd + c0);
+  const float4 ww = w ? ld4c(w + c0) : make_float4(1, 1, 1, 1);
+  const float4 m = train ? ld4c(mean + c0) : z4;
+  const float4 mg = train ? ld4c(coef + c0) : z4, mgx = train ? ld4c(coef + C + c0) : z4;
+  const float4 bb = ((rmode == 2 || rmode == 4) && b) ? ld4c(b + c0) : z4;
+  const bool need_y = rmode == 1 || rmode == 3;
+  for (int64_t r = r0 + rl; r < r1; r += kApplyUnroll * tr) {
+    float4 g[kApplyUnroll], v[kApplyUnroll], o4[kApplyUnroll];
+#pragma unroll
+    for (int u = 0; u < kApplyUnroll; ++u) {
+      const int64_t ru = r + (int64_t)u * tr;
+      const int64_t e = (ru < r1 ? ru : r) * C + c0;
+      g[u] = ld4c(dy + e);
+      v[u] = train ? ld4c(x + e) : z4;
+      o4[u] = need_y ? ld4c(y + e) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < kApplyUnroll; ++u) {
+      const int64_t ru = r + (int64_t)u * tr;
+      if (ru >= r1) break;
+      const int64_t e = ru * C + c0;
+      float4 gg = g[u];
+      if (rmode) {
+        float4 o;
+        if (need_y) {
+          o = o4[u];
+        } else {
+          o.x = bn_affine(v[u].x, m.x, is.x, ww.x, bb.x);
+          o.y = bn_affine(v[u].y, m.y, is.y, ww.y, bb.y);
+          o.z = bn_affine(v[u].z, m.z, is.z, ww.z, bb.z);
+          o.w = bn_affine(v[u].w, m.w, is.w, ww.w, bb.w);
+        }
+        const float k = rmode <= 2 ? 0.f : 0.2f;
+        gg.x = o.x > 0.f ? gg.x : k * gg.x;
+        gg.y = o.y > 0.f ? gg.y : k * gg.y;
+        gg.z = o.z > 0.f ? gg.z : k * gg.z;
+        gg.w = o.w > 0.f ? gg.w : k * gg.w;
+      }
+      if (dres) st4(dres + e, gg);
+      float4 out;
+      if (train) {
+        out.x = ww.x * is.x * (gg.x - mg.x - (v[u].x - m.x) * is.x * mgx.x);
+        out.y = ww.y * is.y * (gg.y - mg.y - (v[u].y - m.y) * is.y * mgx.y);
+        out.z = ww.z * is.z * (gg.z - mg.z - (v[u].z - m.z) * is.z * mgx.z);
+        out.w = ww.w * is.w * (gg.w - mg.w - (v[u].w - m.w) * is.w * mgx.w);
+      } else {
+        out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
+      }
+      st4(dx + e, out);
+    }
+  }
+}
+
+struct ApplyPlan {
+  int tc, cblocks, rsplits;
+  int64_t per;
+};
+
+static ApplyPlan apply_plan(int64_t rows, int C) {
+  ApplyPlan a;
+  a.tc = std::min(C / 4, 64);
+  if (a.tc < 1) a.tc = 1;
+  while (256 % a.tc) --a.tc;
+  a.cblocks = (int)ceil_div(C / 4, a.tc);
+  const int tr = 256 / a.tc;
+  const int want = std::max(1, 2048 / a.cblocks);  // ~8 blocks per CU
+  const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * kApplyUnroll));
+  a.rsplits = (int)std::min<int64_t>(want, maxs);
+  a.per = ceil_div(rows, a.rsplits);
+  a.rsplits = (int)ceil_div(rows, a.per);
+  return a;
 }
 
 struct ReducePlan {
@@ -379,9 +439,9 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
                                                                    save_invstd, running_mean, running_var,
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
-  int64_t total4 = rows * c / 4;
-  bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
-                                                   relu);
+  const ApplyPlan ap = apply_plan(rows, c);
+  bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
+                                                                 weight, bias, res, y, relu);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
 }
@@ -397,11 +457,11 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
   bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
                                                                    running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_tiles_final");
-  int64_t total4 = rows * c / 4;
+  const ApplyPlan ap = apply_plan(rows, c);
   int slot;  // x (+res) in, y out
   timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
-  bn_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, save_mean, save_invstd, weight, bias, res, y,
-                                                   relu);
+  bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
+                                                                 weight, bias, res, y, relu);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
@@ -431,9 +491,10 @@ int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles,
   hipStream_t s = as_stream(stream);
   bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, ntiles, partial, save_invstd, coef);
   AS_CHECK_LAUNCH("bn_bwd_final");
-  int64_t total4 = rows * c / 4;
-  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, nullptr, x, weight, bias, save_mean,
-                                                       save_invstd, coef, dx, dres, 2, 1);
+  const ApplyPlan ap = apply_plan(rows, c);
+  bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, nullptr, x, weight,
+                                                                     bias, save_mean, save_invstd, coef, dx, dres,
+                                                                     2, 1);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
 }
@@ -469,12 +530,14 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
                                                                    coef, dweight, dbias);
     AS_CHECK_LAUNCH("bn_bwd_final");
   }
-  int64_t total4 = rows * c / 4;
   int slot;  // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
-               4.0 * rows * c * (2 + (train ? 1 : 0) + (rmode == 1 ? 1 : 0) + (dres ? 1 : 0)), &slot);
-  bn_bwd_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, dy, y, x, weight, bias, save_mean, save_invstd,
-                                                       coef, dx, dres, rmode, train);
+               4.0 * rows * c * (2 + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)),
+               &slot);
+  const ApplyPlan ap = apply_plan(rows, c);
+  bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, y, x, weight, bias,
+                                                                     save_mean, save_invstd, coef, dx, dres, rmode,
+                                                                     train);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
