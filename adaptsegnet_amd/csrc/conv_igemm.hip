@@ -19,6 +19,7 @@
 // grids are split along K into fp32 slabs that a deterministic reduce kernel sums.
 #include <atomic>
 #include "conv_kernels.hpp"
+#include "conv_thin.hpp"
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -515,6 +516,13 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
 }
 
 
+// Thin convs (Cout <= 4) go to the vector-ALU kernels of conv_thin.hip (A/B knob:
+// ADAPTSEG_NO_THIN=1 keeps them on the implicit GEMM).
+bool use_thin(const adaptseg_conv_desc *d, int op) {
+  static const bool off = getenv("ADAPTSEG_NO_THIN") != nullptr;
+  return !off && thin_eligible(d, op);
+}
+
 }  // namespace adaptseg
 
 using namespace adaptseg;
@@ -534,6 +542,7 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
     b = std::max(b, g.slab_bytes);
   }
   if (tapgemm_eligible(d)) b = std::max(b, tapgemm_workspace(d, op));
+  if (use_thin(d, op)) b = std::max(b, thin_workspace(d, op));
   if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
     // bias-gradient partials
     int per, splits;
@@ -550,6 +559,11 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
   int st = make_plan(d, op, pl);
   if (st) return st;
   // alignment-dependent downgrades are not known here; report the aligned choice
+  if (use_thin(d, op)) {
+    *kernel_id = thin_kernel_id(op);
+    *splits = 1;
+    return ADAPTSEG_OK;
+  }
   if (tapgemm_eligible(d)) return tapgemm_kernel_id(d, op, kernel_id, splits);
   *kernel_id = ::adaptseg::kernel_id(pl, op);
   *splits = pl.p.splits;
@@ -567,6 +581,9 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
   AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv fwd: residual flag without res");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd: null weight %d", s);
+  if (use_thin(d, ADAPTSEG_CONV_FWD) &&
+      thin_fwd(d, x, w[0], bias ? bias[0] : nullptr, res, y, flags, as_stream(stream)) == ADAPTSEG_OK)
+    return ADAPTSEG_OK;
   if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg))
     return tapgemm_fwd(d, x, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
   ConvParams &p = pl.p;
@@ -641,6 +658,9 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
   AS_CHECK_ARG((flags & kEpiActGrad) != kEpiActGrad, "conv bwd_data: LEAKY_GRAD and RELU_GRAD");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data: null weight %d", s);
+  if (use_thin(d, ADAPTSEG_CONV_BWD_DATA) &&
+      thin_dgrad(d, dy, w[0], res, aux, dx, flags, as_stream(stream)) == ADAPTSEG_OK)
+    return ADAPTSEG_OK;
   if (tapgemm_eligible(d) && aligned16(dy) && aligned16(dx) && segs_aligned(w, d->nseg) &&
       (!res || aligned16(res)) && (!aux || aligned16(aux)))
     return tapgemm_bwd_data(d, dy, w, res, aux, dx, flags, ws, ws_bytes, as_stream(stream));
@@ -720,7 +740,14 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
   AS_CHECK_ARG(dy && x && dw, "conv bwd_weight: null pointer");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
   hipStream_t s = as_stream(stream);
-  if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(dw, d->nseg)) {
+  int thin_st = ADAPTSEG_ERR_ARG;
+  if (use_thin(d, ADAPTSEG_CONV_BWD_WEIGHT)) {
+    thin_st = thin_wgrad(d, dy, x, dw[0], flags, ws, ws_bytes, s);
+    if (thin_st != ADAPTSEG_OK && thin_st != ADAPTSEG_ERR_ARG) return thin_st;
+  }
+  if (thin_st == ADAPTSEG_OK) {
+    st = ADAPTSEG_OK;
+  } else if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(dw, d->nseg)) {
     st = tapgemm_bwd_weight(d, dy, x, dw, flags, ws, ws_bytes, s);
   } else {
     ConvParams &p = pl.p;

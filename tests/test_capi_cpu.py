@@ -39,9 +39,11 @@ def test_workspace_and_kernel_selection_on_host():
     #                                           1x1 GEMM with N = 36 taps x 19 (pad 704)
     dgrad, _ = K.conv_kernel_id(aspp, 4, 64, 128, 1)
     assert dgrad == 104                       # dX = G * W', K = 704: vector data-grad
-    d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))  # D classifier: stride 2 keeps the direct GEMM
+    d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))  # D classifier (Cout 1): the thin kernels
     kid, _ = K.conv_kernel_id(d5, 4, 32, 64, 0)
-    assert (kid // 10) % 10 == 1              # skinny-N tile (256x32)
+    assert kid == 80                          # vector-ALU thin forward
+    kid, _ = K.conv_kernel_id(d5, 4, 32, 64, 1)
+    assert kid // 100 == 1 and kid % 100 < 80  # stride-2 data grad stays on the implicit GEMM
 
 
 def test_kernels_use_no_scratch(tmp_path):

@@ -59,7 +59,43 @@ CONV_CASES = [
     (2, 64, 30, 34, 256, 1, 1, (0,), (1,), False),        # wgrad 256x64 tile (M'=256, N'=64)
     (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),          # wgrad ~192 K-splits (16-group reduce)
     (1, 32, 8, 10, 320, 1, 1, (0,), (1,), True),          # bias grad with Cout > 256
+    (2, 64, 16, 24, 2, 3, 1, (1,), (1,), True),           # thin: the warper's output conv (Cout 2)
+    (2, 32, 10, 14, 3, 3, 1, (2,), (2,), False),          # thin: Cout 3, dilated
+    (1, 16, 9, 7, 4, 1, 1, (0,), (1,), True),             # thin: Cout 4, 1x1
 ]
+
+
+def test_thin_conv_selection_and_epilogues():
+    """Cout <= 4 convs run on the vector-ALU kernels (conv_thin.hip): selector 100*op + 80
+    (stride-2 data gradients stay on the implicit GEMM), with the igemm epilogue semantics."""
+    k = K()
+    n, cin, h, w, cout = 2, 64, 12, 18, 2
+    geom = k.ConvGeom(cin, cout, 3, 3, 1, (1,), (1,))
+    for op in (0, 1, 2):
+        assert k.conv_kernel_id(geom, n, h, w, op)[0] == 100 * op + 80
+    g2 = k.ConvGeom(128, 1, 4, 4, 2, (1,), (1,))           # D classifier
+    assert k.conv_kernel_id(g2, n, 8, 10, 0)[0] == 80
+    assert k.conv_kernel_id(g2, n, 8, 10, 1)[0] != 180
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    res = torch.randn(n, cout, h, w, generator=g, dtype=torch.float64)
+    prev = torch.randn(n, cout, h, w, generator=g, dtype=torch.float64)
+    ref = F.relu(F.conv2d(x, wt, b, 1, 1) + prev + res)
+    out = nhwc(prev)
+    k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)], [b.float().to(DEV)], out=out, res=nhwc(res),
+               flags=k.EPI_ACCUMULATE | k.EPI_RELU)
+    assert rel(nchw(out), ref) < 2e-5
+    gy = torch.randn(n, cout, h, w, generator=g, dtype=torch.float64)
+    aux = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    prev_dx = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    dref = torch.nn.grad.conv2d_input(x.shape, wt, gy, 1, 1) + prev_dx
+    dref = torch.where(aux > 0, dref, 0.2 * dref)
+    dx = nhwc(prev_dx)
+    k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)], out=dx, aux=nhwc(aux), flags=k.EPI_ACCUMULATE)
+    assert rel(nchw(dx), dref) < 2e-5
+
 
 
 def _ref_conv(x, ws, bs, stride, pads, dils):
