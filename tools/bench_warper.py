@@ -37,7 +37,7 @@ def timed(fn, steps, warmup):
     for i in range(steps):
         fn(warmup + i)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    return (time.perf_counter() - t0) / max(steps, 1)
 
 
 def cpu_baseline(threads):
