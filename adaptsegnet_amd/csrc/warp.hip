@@ -180,97 +180,144 @@ __device__ __forceinline__ Tap warp_tap(const float *flow, int fc, int64_t pix, 
 
 __device__ __forceinline__ bool inb(int y, int x, int h, int w) { return y >= 0 && y < h && x >= 0 && x < w; }
 
-// y[b][Y][X][c] = bilinear sample of x at the warped point (zeros outside); one thread per
-// output element, both heads (x1 may be NULL).
+// Per-block cache of the sample taps of floor(256 / C) consecutive pixels: computed once per
+// pixel (two tanh and the double-precision linspace) instead of once per channel.
+struct TapCache {
+  float nw[256], ne[256], sw[256], se[256];
+  int x0[256], y0[256], b[256];
+};
+
+__device__ __forceinline__ void fill_taps(TapCache &tc, int pb, int64_t base, int64_t total, const float *flow,
+                                          int fc, int h, int w) {
+  if (threadIdx.x < pb && base + threadIdx.x < total) {
+    const int64_t pix = base + threadIdx.x;
+    const int x = (int)(pix % w);
+    const int64_t t2 = pix / w;
+    const int y = (int)(t2 % h);
+    const Tap t = warp_tap(flow, fc, pix, y, x, h, w);
+    tc.nw[threadIdx.x] = t.nw;
+    tc.ne[threadIdx.x] = t.ne;
+    tc.sw[threadIdx.x] = t.sw;
+    tc.se[threadIdx.x] = t.se;
+    tc.x0[threadIdx.x] = t.x0;
+    tc.y0[threadIdx.x] = t.y0;
+    tc.b[threadIdx.x] = (int)(t2 / h);
+  }
+}
+
+// y[b][Y][X][c] = bilinear sample of x at the warped point (zeros outside); a block handles
+// floor(256 / C) pixels, one thread per (pixel, channel), both heads (x1 may be NULL).
 __global__ void __launch_bounds__(256)
 grid_warp_fwd_kernel(int n, int C, int h, int w, int fc, const float *__restrict__ flow,
                      const float *__restrict__ x1, const float *__restrict__ x2, float *__restrict__ y1,
                      float *__restrict__ y2) {
-  const int64_t total = (int64_t)n * h * w * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const int64_t pix = i / C;
-    const int x = (int)(pix % w);
-    const int64_t t2 = pix / w;
-    const int y = (int)(t2 % h), b = (int)(t2 / h);
-    const Tap t = warp_tap(flow, fc, pix, y, x, h, w);
-    const int64_t img = (int64_t)b * h * w;
-    const bool bnw = inb(t.y0, t.x0, h, w), bne = inb(t.y0, t.x0 + 1, h, w);
-    const bool bsw = inb(t.y0 + 1, t.x0, h, w), bse = inb(t.y0 + 1, t.x0 + 1, h, w);
-    const int64_t pnw = (img + (int64_t)t.y0 * w + t.x0) * C + c;
-    for (int head = 0; head < 2; ++head) {
-      const float *xp = head ? x2 : x1;
-      float *yp = head ? y2 : y1;
-      if (!xp) continue;
-      float o = 0.f;
-      if (bnw) o += xp[pnw] * t.nw;
-      if (bne) o += xp[pnw + C] * t.ne;
-      if (bsw) o += xp[pnw + (int64_t)w * C] * t.sw;
-      if (bse) o += xp[pnw + (int64_t)(w + 1) * C] * t.se;
-      yp[i] = o;
+  __shared__ TapCache tc;
+  const int pb = 256 / C;
+  const int j = threadIdx.x / C, c = threadIdx.x - (threadIdx.x / C) * C;
+  const int64_t total = (int64_t)n * h * w;
+  for (int64_t base = (int64_t)blockIdx.x * pb; base < total; base += (int64_t)gridDim.x * pb) {
+    fill_taps(tc, pb, base, total, flow, fc, h, w);
+    __syncthreads();
+    const int64_t pix = base + j;
+    if (j < pb && pix < total) {
+      const int x0 = tc.x0[j], y0 = tc.y0[j];
+      const bool bnw = inb(y0, x0, h, w), bne = inb(y0, x0 + 1, h, w);
+      const bool bsw = inb(y0 + 1, x0, h, w), bse = inb(y0 + 1, x0 + 1, h, w);
+      const int64_t pnw = (((int64_t)tc.b[j] * h + y0) * w + x0) * C + c;
+      const int64_t i = pix * C + c;
+      for (int head = 0; head < 2; ++head) {
+        const float *xp = head ? x2 : x1;
+        float *yp = head ? y2 : y1;
+        if (!xp) continue;
+        float o = 0.f;
+        if (bnw) o += xp[pnw] * tc.nw[j];
+        if (bne) o += xp[pnw + C] * tc.ne[j];
+        if (bsw) o += xp[pnw + (int64_t)w * C] * tc.sw[j];
+        if (bse) o += xp[pnw + (int64_t)(w + 1) * C] * tc.se[j];
+        yp[i] = o;
+      }
     }
+    __syncthreads();
   }
 }
 
 // Gradient of the warp field: per pixel, sum over channels (and both heads) of dy times the
 // derivative of the bilinear sample, times size/2 (unnormalize), the clamp mask (pass where
-// -1 <= pre <= 1, as torch's clamp backward) and tanh' = 1 - tanh^2.
+// -1 <= pre <= 1, as torch's clamp backward) and tanh' = 1 - tanh^2.  A block handles
+// floor(256 / C) pixels with one thread per (pixel, channel) — coalesced dy and corner reads —
+// and one thread per pixel then sums its C channel terms from LDS in channel order.
 __global__ void __launch_bounds__(256)
 grid_warp_dflow_kernel(int n, int C, int h, int w, int fc, const float *__restrict__ flow,
                        const float *__restrict__ x1, const float *__restrict__ x2,
                        const float *__restrict__ dy1, const float *__restrict__ dy2,
                        float *__restrict__ dflow) {
+  __shared__ float rx[256], ry[256];
+  const int pb = 256 / C;                     // pixels per block iteration
+  const int j = threadIdx.x / C, c = threadIdx.x - (threadIdx.x / C) * C;
   const int64_t total = (int64_t)n * h * w;
-  for (int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; pix < total;
-       pix += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(pix % w);
-    const int64_t t2 = pix / w;
-    const int y = (int)(t2 % h), b = (int)(t2 / h);
-    const Tap t = warp_tap(flow, fc, pix, y, x, h, w);
-    const int64_t img = (int64_t)b * h * w;
-    const bool bnw = inb(t.y0, t.x0, h, w), bne = inb(t.y0, t.x0 + 1, h, w);
-    const bool bsw = inb(t.y0 + 1, t.x0, h, w), bse = inb(t.y0 + 1, t.x0 + 1, h, w);
-    const int64_t pnw = (img + (int64_t)t.y0 * w + t.x0) * C;
-    const float fx = (float)t.x0, fy = (float)t.y0;
-    const float ix_se = fx + 1.f, iy_se = fy + 1.f;
+  for (int64_t base = (int64_t)blockIdx.x * pb; base < total; base += (int64_t)gridDim.x * pb) {
+    const int64_t pix = base + j;
     float gix = 0.f, giy = 0.f;
-    for (int head = 0; head < 2; ++head) {
-      const float *xp = head ? x2 : x1;
-      const float *gp = head ? dy2 : dy1;
-      if (!xp || !gp) continue;
-      const float *g = gp + pix * C;
-      for (int c = 0; c < C; ++c) {
-        const float go = g[c];
+    if (j < pb && pix < total) {
+      const int x = (int)(pix % w);
+      const int64_t t2 = pix / w;
+      const int y = (int)(t2 % h), b = (int)(t2 / h);
+      const Tap t = warp_tap(flow, fc, pix, y, x, h, w);
+      const bool bnw = inb(t.y0, t.x0, h, w), bne = inb(t.y0, t.x0 + 1, h, w);
+      const bool bsw = inb(t.y0 + 1, t.x0, h, w), bse = inb(t.y0 + 1, t.x0 + 1, h, w);
+      const int64_t pnw = (((int64_t)b * h + t.y0) * w + t.x0) * C + c;
+      const float fx = (float)t.x0, fy = (float)t.y0;
+      const float ix_se = fx + 1.f, iy_se = fy + 1.f;
+      for (int head = 0; head < 2; ++head) {
+        const float *xp = head ? x2 : x1;
+        const float *gp = head ? dy2 : dy1;
+        if (!xp || !gp) continue;
+        const float go = gp[pix * C + c];
         if (bnw) {
-          const float v = xp[pnw + c];
+          const float v = xp[pnw];
           gix -= v * (iy_se - t.iy) * go;
           giy -= v * (ix_se - t.ix) * go;
         }
         if (bne) {
-          const float v = xp[pnw + C + c];
+          const float v = xp[pnw + C];
           gix += v * (iy_se - t.iy) * go;
           giy -= v * (t.ix - fx) * go;
         }
         if (bsw) {
-          const float v = xp[pnw + (int64_t)w * C + c];
+          const float v = xp[pnw + (int64_t)w * C];
           gix -= v * (t.iy - fy) * go;
           giy += v * (ix_se - t.ix) * go;
         }
         if (bse) {
-          const float v = xp[pnw + (int64_t)(w + 1) * C + c];
+          const float v = xp[pnw + (int64_t)(w + 1) * C];
           gix += v * (t.iy - fy) * go;
           giy += v * (t.ix - fx) * go;
         }
       }
     }
-    float dgx = gix * ((float)w / 2.f), dgy = giy * ((float)h / 2.f);
-    dgx = (t.gx_pre >= -1.f && t.gx_pre <= 1.f) ? dgx : 0.f;
-    dgy = (t.gy_pre >= -1.f && t.gy_pre <= 1.f) ? dgy : 0.f;
-    float *o = dflow + pix * fc;
-    for (int k = 0; k < fc - 2; ++k) o[k] = 0.f;
-    o[fc - 2] = dgx * (1.f - t.tx * t.tx);
-    o[fc - 1] = dgy * (1.f - t.ty * t.ty);
+    rx[threadIdx.x] = gix;
+    ry[threadIdx.x] = giy;
+    __syncthreads();
+    const int64_t op = base + threadIdx.x;
+    if (threadIdx.x < pb && op < total) {
+      float sx = 0.f, sy = 0.f;
+      for (int k = 0; k < C; ++k) {
+        sx += rx[threadIdx.x * C + k];
+        sy += ry[threadIdx.x * C + k];
+      }
+      const int x = (int)(op % w);
+      const int64_t t2 = op / w;
+      const int y = (int)(t2 % h);
+      const Tap t = warp_tap(flow, fc, op, y, x, h, w);
+      float dgx = sx * ((float)w / 2.f), dgy = sy * ((float)h / 2.f);
+      dgx = (t.gx_pre >= -1.f && t.gx_pre <= 1.f) ? dgx : 0.f;
+      dgy = (t.gy_pre >= -1.f && t.gy_pre <= 1.f) ? dgy : 0.f;
+      float *o = dflow + op * fc;
+      for (int k = 0; k < fc - 2; ++k) o[k] = 0.f;
+      o[fc - 2] = dgx * (1.f - t.tx * t.tx);
+      o[fc - 1] = dgy * (1.f - t.ty * t.ty);
+    }
+    __syncthreads();
   }
 }
 
@@ -306,29 +353,31 @@ __global__ void __launch_bounds__(256)
 grid_scatter_kernel(int n, int C, int h, int w, int fc, const float *__restrict__ flow,
                     const float *__restrict__ dy, const unsigned int *__restrict__ mbits,
                     unsigned long long *__restrict__ acc) {
+  __shared__ TapCache tc;
   const unsigned int mb = *mbits;
-  if (mb == 0u) return;  // dy == 0: nothing to scatter
+  if (mb == 0u) return;  // dy == 0: nothing to scatter (uniform over the grid)
   const double scale = ldexp(1.0, fixed_exp(mb, h * w));
-  const int64_t total = (int64_t)n * h * w * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float go = dy[i];
-    if (go == 0.f) continue;
-    const int c = (int)(i % C);
-    const int64_t pix = i / C;
-    const int x = (int)(pix % w);
-    const int64_t t2 = pix / w;
-    const int y = (int)(t2 % h), b = (int)(t2 / h);
-    const Tap t = warp_tap(flow, fc, pix, y, x, h, w);
-    const int64_t pnw = (((int64_t)b * h + t.y0) * w + t.x0) * C + c;
-    if (inb(t.y0, t.x0, h, w))
-      atomicAdd(acc + pnw, (unsigned long long)llrint((double)(go * t.nw) * scale));
-    if (inb(t.y0, t.x0 + 1, h, w))
-      atomicAdd(acc + pnw + C, (unsigned long long)llrint((double)(go * t.ne) * scale));
-    if (inb(t.y0 + 1, t.x0, h, w))
-      atomicAdd(acc + pnw + (int64_t)w * C, (unsigned long long)llrint((double)(go * t.sw) * scale));
-    if (inb(t.y0 + 1, t.x0 + 1, h, w))
-      atomicAdd(acc + pnw + (int64_t)(w + 1) * C, (unsigned long long)llrint((double)(go * t.se) * scale));
+  const int pb = 256 / C;
+  const int j = threadIdx.x / C, c = threadIdx.x - (threadIdx.x / C) * C;
+  const int64_t total = (int64_t)n * h * w;
+  for (int64_t base = (int64_t)blockIdx.x * pb; base < total; base += (int64_t)gridDim.x * pb) {
+    fill_taps(tc, pb, base, total, flow, fc, h, w);
+    __syncthreads();
+    const int64_t pix = base + j;
+    const float go = (j < pb && pix < total) ? dy[pix * C + c] : 0.f;
+    if (go != 0.f) {
+      const int x0 = tc.x0[j], y0 = tc.y0[j];
+      const int64_t pnw = (((int64_t)tc.b[j] * h + y0) * w + x0) * C + c;
+      if (inb(y0, x0, h, w))
+        atomicAdd(acc + pnw, (unsigned long long)llrint((double)(go * tc.nw[j]) * scale));
+      if (inb(y0, x0 + 1, h, w))
+        atomicAdd(acc + pnw + C, (unsigned long long)llrint((double)(go * tc.ne[j]) * scale));
+      if (inb(y0 + 1, x0, h, w))
+        atomicAdd(acc + pnw + (int64_t)w * C, (unsigned long long)llrint((double)(go * tc.sw[j]) * scale));
+      if (inb(y0 + 1, x0 + 1, h, w))
+        atomicAdd(acc + pnw + (int64_t)(w + 1) * C, (unsigned long long)llrint((double)(go * tc.se[j]) * scale));
+    }
+    __syncthreads();
   }
 }
 
@@ -379,7 +428,8 @@ int adaptseg_up2_relu_cat_bwd(int n, int h, int w, int cs, int cd, const float *
 
 int adaptseg_grid_warp_fwd(int n, int c, int h, int w, int fc, const float *flow, const float *x1,
                            const float *x2, float *y1, float *y2, adaptseg_stream_t stream) {
-  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && fc >= 2 && fc % 2 == 0, "grid_warp_fwd: bad shape");
+  AS_CHECK_ARG(n > 0 && c > 0 && c <= 256 && h > 0 && w > 0 && fc >= 2 && fc % 2 == 0,
+               "grid_warp_fwd: bad shape (1 <= c <= 256)");
   AS_CHECK_ARG((int64_t)h * w < (1ll << 30), "grid_warp_fwd: h*w too large");
   AS_CHECK_ARG(flow && (x1 || x2) && (!x1 || y1) && (!x2 || y2), "grid_warp_fwd: null pointer");
   const int64_t total = (int64_t)n * h * w * c;
@@ -400,7 +450,8 @@ int adaptseg_grid_warp_bwd_workspace_size(int n, int c, int h, int w, size_t *by
 int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow, const float *x1,
                            const float *x2, const float *dy1, const float *dy2, float *dflow, float *dx1,
                            float *dx2, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && fc >= 2 && fc % 2 == 0, "grid_warp_bwd: bad shape");
+  AS_CHECK_ARG(n > 0 && c > 0 && c <= 256 && h > 0 && w > 0 && fc >= 2 && fc % 2 == 0,
+               "grid_warp_bwd: bad shape (1 <= c <= 256)");
   AS_CHECK_ARG((int64_t)h * w < (1ll << 30), "grid_warp_bwd: h*w too large");
   AS_CHECK_ARG(flow && (dy1 || dy2), "grid_warp_bwd: null pointer");
   AS_CHECK_ARG(!dflow || ((!dy1 || x1) && (!dy2 || x2)), "grid_warp_bwd: dflow needs the sampled inputs");
@@ -410,8 +461,8 @@ int adaptseg_grid_warp_bwd(int n, int c, int h, int w, int fc, const float *flow
   if (dflow) {
     int slot;  // field in and out, x and dy of each head once
     timing_begin(kTWarpDflow, s, 4.0 * n * h * w * (4 + 2 * c * ((dy1 ? 1 : 0) + (dy2 ? 1 : 0))), &slot);
-    grid_warp_dflow_kernel<<<grid1d((int64_t)n * h * w), 256, 0, s>>>(n, c, h, w, fc, flow, x1, x2, dy1, dy2,
-                                                                       dflow);
+    grid_warp_dflow_kernel<<<grid1d((int64_t)n * h * w * c), 256, 0, s>>>(n, c, h, w, fc, flow, x1, x2, dy1, dy2,
+                                                                           dflow);
     timing_end(slot, s);
     AS_CHECK_LAUNCH("grid_warp_dflow");
   }

@@ -301,13 +301,13 @@ int adaptseg_up2_relu_cat_bwd(int n, int h, int w, int cs, int cd, const float *
                               const float *dout, float *ds, float *dd, adaptseg_stream_t stream);
 /* ResNetMulti.warp: grid = clamp(tanh(flow[..., last channel pair]) + meshgrid(linspace(-1, 1,
    w), linspace(-1, 1, h)), -1, 1); y = grid_sample(x, grid) (bilinear, zeros padding,
-   align_corners=False).  x, y NHWC [n][h][w][c]; flow NHWC [n][h][w][fc] (fc even).  Two
+   align_corners=False).  x, y NHWC [n][h][w][c] (c <= 256); flow NHWC [n][h][w][fc] (fc even).  Two
    inputs share one grid (the two heads, deeplab_multi.py:190-192); x1/y1 may be NULL. */
 int adaptseg_grid_warp_fwd(int n, int c, int h, int w, int fc, const float *flow, const float *x1,
                            const float *x2, float *y1, float *y2, adaptseg_stream_t stream);
 int adaptseg_grid_warp_bwd_workspace_size(int n, int c, int h, int w, size_t *bytes);
 /* dflow (written; [n][h][w][fc], zero outside the last pair) = the warp field's gradient summed
-   over both heads (needs x1/x2 for every given dy); dx1/dx2 (written, optional) = the input
+   over both heads (needs x1/x2 for every given dy; c <= 256); dx1/dx2 (written, optional) = the input
    gradients.  The input gradient is a data-dependent scatter: it accumulates in 64-bit fixed
    point (integer atomics, so the result is independent of scheduling), with the scale chosen
    per call from max|dy| so no sum can overflow; rounding <= 2^-42 * max|dy| at 1024x2048. */
