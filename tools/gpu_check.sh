@@ -24,3 +24,4 @@ timeout -k 10 600 python bench.py --config c5 --steps 4 --warmup 2 --no-cpu-base
 timeout -k 10 300 python tools/bench_preprocess.py > gpurun_out/bench_preprocess_$TAG.log 2>&1 || exit 12
 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --overlap > gpurun_out/bench_c2_overlap_$TAG.log 2>&1 || exit 13
 bash tools/gpu_traffic.sh c2 || exit 14
+timeout -k 10 600 python tools/bench_warper.py > gpurun_out/bench_warper_$TAG.log 2>&1 || exit 15
