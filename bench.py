@@ -180,9 +180,19 @@ def cpu_baseline(threads):
     t0 = time.perf_counter()
     R.oracle_step(G, None, D2, opts, cfg, 0, [(xs, lab, xt)])
     dt = time.perf_counter() - t0
+    # BASELINE config c1 (the reference's CPU-runnable case): forward + CrossEntropy2d, 1x3x321x321
+    x1 = torch.from_numpy(R.det_images((1, 3, 321, 321), 5)).float()
+    l1 = torch.from_numpy(R.det_labels((1, 321, 321), 6))
+    t1 = time.perf_counter()
+    with torch.no_grad():
+        R.cross_entropy2d(R.g_forward(G, x1, (321, 321), train=True)[1], l1)
+    c1 = time.perf_counter() - t1
     return {"value": 1.0 / dt, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": "1 single-level adversarial step (oracle/reference_torch.py, stock PyTorch "
-                      f"CPU fp32), batch 1, source+target 1024x512; {dt:.2f} s"}
+                      f"CPU fp32), batch 1, source+target 1024x512; {dt:.2f} s",
+            "c1_forward_ce_s": c1,
+            "calibration": "the port times within +6 % (step) / -12 % (c1) of the reference's own "
+                           "modules on the same cores (profiles/r1/cpu_calibration.json)"}
 
 
 def main():
@@ -307,6 +317,8 @@ def main():
                    "global_batch": batch * world, "parallelism": f"dp{world}",
                    "step_conv_tflop": step_flops / 1e12,
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
+                   # algorithmic conv FLOPs / step time / (n_gpu x peak)
+                   "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    "losses_last_step": losses},
     }
     if not args.no_roofline and k_launches:
