@@ -264,3 +264,44 @@ def test_domain_overlap_is_bit_identical(data, level, gan):
         assert torch.equal(g0[k], g1[k]), k
     for k in d0:
         assert torch.equal(d0[k], d1_[k]), k
+
+
+@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+def test_iter_size_two_accumulates_sub_batches(data, level, gan):
+    """iter_size = 2 (train:569-683 sub-iteration loop): two sub-batches per step, each loss
+    scaled by 1/iter_size, gradients accumulated before one optimiser step.  Eval-mode BN, 2
+    steps, vs the fp64 oracle at the same tolerances as test_adversarial_step_eval_bn."""
+    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    xs, lab, xt = data
+    xs2 = torch.from_numpy(R.det_images(tuple(xs.shape), 31))
+    lab2 = torch.from_numpy(R.det_labels(tuple(lab.shape), 32))
+    xt2 = torch.from_numpy(R.det_images(tuple(xt.shape), 33))
+    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33), iter_size=2)
+    subs = [(xs, lab, xt), (xs2, lab2, xt2)]
+
+    def oracle(dtype):
+        G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=dtype, trainable=R.g_trainable)
+        D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=dtype, trainable=lambda k: True)
+        D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=dtype, trainable=lambda k: True)
+        opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
+        b = [(a.to(dtype), l, t.to(dtype)) for a, l, t in subs]
+        return G, [R.oracle_step(G, D1, D2, opts, cfg, it, b, bn_train=False) for it in range(2)]
+
+    G, ref = oracle(torch.float64)
+    G32, _ = oracle(torch.float32)
+    m, d1, d2 = build_g(), build_d(2001), build_d(2002)
+    m.eval()
+    tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2, StepConfig(**cfg))
+    dev = [(a.float().to(DEV), l.to(DEV), t.float().to(DEV)) for a, l, t in subs]
+    got = [tr.step(it, dev).values() for it in range(2)]
+    for it in range(2):
+        for k, v in ref[it].items():
+            assert abs(got[it][k] - v) <= 1e-4 * abs(v) + 1e-7, (it, k, got[it][k], v)
+    g0 = R.det_state(R.g_specs(), 1338)
+    sd = m.state_dict()
+    for gname, keys in _groups(G, level).items():
+        dref = _updates(G, keys, g0)
+        f, _ = frob(_updates(None, keys, g0, sd), dref)
+        f32, _ = frob(_updates(G32, keys, g0), dref)
+        assert f <= 2 * f32 + 1e-4, (gname, f, f32)
