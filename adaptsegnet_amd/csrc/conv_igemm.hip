@@ -333,11 +333,15 @@ void set_splits(Plan &pl) {
   const int nkt = (int)ceil_div(p.K, pl.bk);
   // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~2.
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
-  // fwd / data-grad split only grids below one block per CU (slab + reduce traffic costs more
-  // than the partial second wave it would fill); weight-grad grids are almost always tiny.
+  // weight-grad grids are almost always tiny.
   static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob (512 vs 1024: +1.7 % at c2)
-  const int target = pl.mode == MODE_WGRAD ? wg_target : 512;
-  const int split_below = pl.mode == MODE_WGRAD ? target : 256;
+  static const int fd_target = getenv("ADAPTSEG_EXP_FDTARGET") ? atoi(getenv("ADAPTSEG_EXP_FDTARGET")) : 512;  // A/B knob
+  const int target = pl.mode == MODE_WGRAD ? wg_target : fd_target;
+  // fwd / data-grad: grids of at most one block per CU (<= 256 tiles) split K in two — one
+  // resident block per CU hides no latency (c3 target-domain layer3: +0.6 % step; grids of up
+  // to two blocks per CU split to four measured 2 % slower).  A/B knobs below.
+  static const int fd_below = getenv("ADAPTSEG_EXP_SPLITBELOW") ? atoi(getenv("ADAPTSEG_EXP_SPLITBELOW")) : 257;
+  const int split_below = pl.mode == MODE_WGRAD ? target : fd_below;
   // Rounding: the blocks of a split grid are equal work, so the grid takes (the most blocks
   // any CU runs) x (one block's K range).  tiles * splits must therefore not overshoot a
   // multiple of the CU count: ceil(512 / 36) = 15 splits puts 3 blocks on 28 CUs (0.2 units)
