@@ -399,10 +399,16 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   }
   // 128x128 tile at BK 16 (cfg 6: half the LDS, shorter K steps) measured faster than BK 32
   // for multi-tap weight gradients (+2-8 %, per-shape conv bench, profiles/r1/conv_cfg_ab.txt).
-  // It also wins 1-7 % on the layer3/4 forward convs in isolation, but not end to end (c2
-  // 19.2 vs 19.3 images/s), so the forward keeps BK 32.
   if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && d->kh * d->kw > 1) pl.cfg = 6;
   if ((pl.cfg == 0 || pl.cfg == 6) && getenv("ADAPTSEG_EXP_CFG")) pl.cfg = atoi(getenv("ADAPTSEG_EXP_CFG"));  // A/B knob
+  // Forward products on the occupancy-3 BK-16 tile (cfg 8): +0.9 % c2 / +0.8 % c3 end to end
+  // (tools/ab_cfg3.sh, two alternating runs each) and 0.67 -> 0.69 of peak on the dominant
+  // forward symbol.  The weight gradients stay on cfg 6 (cfg 8 there: -0.7 %).  Non-FAST /
+  // per-element / stride-2 plans fall back to cfg 0 below.  A/B knob: ADAPTSEG_EXP_FWDCFG.
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_FWD) {
+    static const int fwd_cfg = getenv("ADAPTSEG_EXP_FWDCFG") ? atoi(getenv("ADAPTSEG_EXP_FWDCFG")) : 8;
+    pl.cfg = fwd_cfg;
+  }
   p.fd_nseg_k = make_fastdiv(p.kseg);
   pl.flops = conv_flops(d);
   // FAST path eligibility (alignment re-checked at launch).  Vector operands need tile-

@@ -30,12 +30,12 @@ def test_workspace_and_kernel_selection_on_host():
     from adaptsegnet_amd import kernels as K
     g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
     kid, splits = K.conv_kernel_id(g, 4, 64, 128, 0)
-    assert kid == 4 and splits == 1           # fwd, 128x128 tile, FAST gather, no K split
+    assert kid == 84 and splits == 1          # fwd, 128x128 BK16 occupancy-3 tile (cfg 8), FAST, no K split
     kid, splits = K.conv_kernel_id(g, 4, 64, 128, 2)
     assert kid // 100 == 2 and splits > 1     # weight grad splits K = N*OH*OW
     aspp = K.ConvGeom(2048, 19, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24))
     kid, _ = K.conv_kernel_id(aspp, 4, 64, 128, 0)
-    assert kid == 4                           # tap-GEMM: the 19-class head runs as a dense
+    assert kid == 84                          # tap-GEMM: the 19-class head runs as a dense
     #                                           1x1 GEMM with N = 36 taps x 19 (pad 704)
     dgrad, _ = K.conv_kernel_id(aspp, 4, 64, 128, 1)
     assert dgrad == 104                       # dX = G * W', K = 704: vector data-grad
