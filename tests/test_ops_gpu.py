@@ -189,7 +189,7 @@ def test_aspp_tap_gemm_epilogues(rates):
     bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in rates]
     geom = k.ConvGeom(cin, cout, 3, 3, 1, rates, rates)
     sel, _ = k.conv_kernel_id(geom, n, h, w, 0)
-    assert sel % 100 // 10 == 0, sel  # 128x128 tile of the dense 1x1 GEMM, not the 256x32 tile
+    assert sel % 100 // 10 in (0, 8), sel  # a 128x128 tile of the dense 1x1 GEMM, not 256x32
     ref = _ref_conv(x, ws, bs, 1, rates, rates)
     res = torch.randn(ref.shape, generator=g, dtype=torch.float64)
     wd, bd = [w_cl(t) for t in ws], [t.float().to(DEV) for t in bs]
