@@ -405,6 +405,13 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   // (tools/ab_cfg3.sh, two alternating runs each) and 0.67 -> 0.69 of peak on the dominant
   // forward symbol.  The weight gradients stay on cfg 6 (cfg 8 there: -0.7 %).  Non-FAST /
   // per-element / stride-2 plans fall back to cfg 0 below.  A/B knob: ADAPTSEG_EXP_FWDCFG.
+  // Measured and rejected (tools/ab_cfg4.sh, two alternating runs): data gradient on cfg 6
+  // (BK16, 4 blocks/CU instead of 2) -1.1 % c2 / -0.7 % c3; 1x1 weight gradients on cfg 6
+  // -0.3 % / -1.1 %, on cfg 8 -1.2 % / -1.8 %.
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_DATA && getenv("ADAPTSEG_EXP_DGCFG"))  // A/B knob
+    pl.cfg = atoi(getenv("ADAPTSEG_EXP_DGCFG"));
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && getenv("ADAPTSEG_EXP_WGCFG"))  // A/B knob (1x1)
+    pl.cfg = atoi(getenv("ADAPTSEG_EXP_WGCFG"));
   if (pl.cfg == 0 && op == ADAPTSEG_CONV_FWD) {
     static const int fwd_cfg = getenv("ADAPTSEG_EXP_FWDCFG") ? atoi(getenv("ADAPTSEG_EXP_FWDCFG")) : 8;
     pl.cfg = fwd_cfg;
