@@ -334,7 +334,9 @@ void set_splits(Plan &pl) {
   // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~2.
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
   // weight-grad grids are almost always tiny.
-  static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob (512 vs 1024: +1.7 % at c2)
+  // weight-gradient split target 512 blocks (two per CU), rounded down: 384 / 768 / 1024
+  // measured -3.2 / -2.3 / -2.5 % at c2 and -2.8 / -3.1 / -3.2 % at c3 (tools/ab_wgt2.sh)
+  static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob
   static const int fd_target = getenv("ADAPTSEG_EXP_FDTARGET") ? atoi(getenv("ADAPTSEG_EXP_FDTARGET")) : 512;  // A/B knob
   const int target = pl.mode == MODE_WGRAD ? wg_target : fd_target;
   // fwd / data-grad: grids of at most one block per CU (<= 256 tiles) split K in two — one
