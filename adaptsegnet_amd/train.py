@@ -37,6 +37,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
+from . import engine
 from . import functional as F
 from .optim import SGD, Adam, lr_poly
 
@@ -230,6 +231,12 @@ class AdaptSegTrainer:
         return L
 
     def _step(self, i_iter, batches):
+        if os.environ.get("ADAPTSEG_EXP_DEFERJOIN") == "1":
+            with engine.deferred_wgrad_join():
+                return self._step_body(i_iter, batches)
+        return self._step_body(i_iter, batches)
+
+    def _step_body(self, i_iter, batches):
         """batches: iterable of ``iter_size`` tuples (images, labels, images_target).
 
         Multi-GPU: the generator's gradients are final after its adversarial backward of the
@@ -248,7 +255,8 @@ class AdaptSegTrainer:
         batches = list(batches)
         self._pending = []
         for idx, batch in enumerate(batches):
-            g_done = (lambda: self._start_sync((self.model,))) if idx == len(batches) - 1 else None
+            g_done = (lambda: (engine.join_deferred(), self._start_sync((self.model,)))) \
+                if idx == len(batches) - 1 else None
             if c.level == "source-only":
                 self._sub_source_only(batch[0], batch[1], inv, L, g_done)
                 continue
@@ -257,6 +265,7 @@ class AdaptSegTrainer:
                 self._sub_single(images, labels, images_t, inv, tsize, L, g_done)
             else:
                 self._sub_multi(images, labels, images_t, inv, tsize, L, g_done)
+        engine.join_deferred()   # weight gradients complete before the collectives / optimisers
         if not batches:
             self._start_sync((self.model,))
         self._start_sync((self.D1, self.D2))
