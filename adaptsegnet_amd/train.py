@@ -68,8 +68,9 @@ class StepConfig:
     # but every forward conv then shares the GPU with backward kernels, which halves the
     # per-launch roofline of the dominant kernel that bench.py reports.
     overlap_domains: bool = False
-    # HIP stream priority of the step's main chain (None: the caller's stream); see step()
-    main_priority: int | None = -1
+    # HIP stream priority of the step's main chain (None: the caller's stream; "auto": high
+    # for DeeplabMulti, the caller's stream for DeeplabVGG); see step()
+    main_priority: int | str | None = "auto"
 
 
 @dataclass
@@ -210,11 +211,15 @@ class AdaptSegTrainer:
 
     def step(self, i_iter, batches):
         """One iteration.  The step's main chain (forwards, data gradients, BN, losses,
-        optimisers) runs on a HIP stream of priority ``cfg.main_priority`` (default -1, high), so
-        the hardware scheduler favours it over the weight-gradient side stream that fills the
-        gaps: +0.9 % c2, +0.2 % c3 (tools/ab_prio.sh).  The caller's stream waits for it at the
-        end.  ``main_priority=None`` or ``ADAPTSEG_EXP_HIPRIO=0`` runs on the caller's stream."""
+        optimisers) runs on a HIP stream of priority ``cfg.main_priority`` (-1, high, for
+        DeeplabMulti), so the hardware scheduler favours it over the weight-gradient side stream
+        that fills the gaps the HBM-bound BN passes leave: +0.9 % c2, +0.2 % c3, ±0 c5, but
+        -1.7 % for DeeplabVGG (c4: no BN, so it runs on the caller's stream; tools/ab_prio*.sh).
+        The caller's stream waits for it at the end.  ``main_priority=None`` or
+        ``ADAPTSEG_EXP_HIPRIO=0`` runs on the caller's stream."""
         prio = self.cfg.main_priority
+        if prio == "auto":   # VGG has no BN passes for the side stream to fill: -1.7 % with it
+            prio = None if getattr(self.model, "single_output", False) else -1
         dev = next(self.model.parameters()).device
         if prio is None or os.environ.get("ADAPTSEG_EXP_HIPRIO") == "0" or dev.type != "cuda":
             return self._step(i_iter, batches)
