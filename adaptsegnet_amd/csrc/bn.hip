@@ -10,6 +10,7 @@
 // HBM-bound.
 #include "common.hpp"
 #include <algorithm>
+#include <cstdlib>
 
 namespace adaptseg {
 
@@ -387,7 +388,10 @@ static ReducePlan reduce_plan(int64_t rows, int C) {
   // tc must divide 256
   while (256 % r.tc) --r.tc;
   r.cblocks = (int)ceil_div(C, 4 * r.tc);
-  int want = std::max(1, 512 / r.cblocks);
+  // 512 blocks: 256 / 1024 measured -2 % / -4.5 % at c2 (tools/ab_bnr2.sh) — the reduction
+  // shares the chip with the weight-gradient GEMMs, more blocks take CUs from them
+  static const int wantb = getenv("ADAPTSEG_EXP_BNR") ? atoi(getenv("ADAPTSEG_EXP_BNR")) : 512;  // A/B knob
+  int want = std::max(1, wantb / r.cblocks);
   int tr = 256 / r.tc;
   int64_t max_splits = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * 8));
   r.splits = (int)std::min<int64_t>(want, max_splits);
