@@ -368,7 +368,10 @@ static ApplyPlan apply_plan(int64_t rows, int C) {
   while (256 % a.tc) --a.tc;
   a.cblocks = (int)ceil_div(C / 4, a.tc);
   const int tr = 256 / a.tc;
-  const int want = std::max(1, 2048 / a.cblocks);  // ~8 blocks per CU
+  // ~2 blocks per CU: the apply passes run beside the weight-gradient GEMMs; 512 blocks measured
+  // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (tools/ab_bna.sh, two runs each)
+  static const int wantb = getenv("ADAPTSEG_EXP_BNA") ? atoi(getenv("ADAPTSEG_EXP_BNA")) : 512;  // A/B knob
+  const int want = std::max(1, wantb / a.cblocks);
   const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * kApplyUnroll));
   a.rsplits = (int)std::min<int64_t>(want, maxs);
   a.per = ceil_div(rows, a.rsplits);
