@@ -521,7 +521,9 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     if (vec) {
       const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
       const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
-      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
+      // grid cap: 512 / 1024 / 8192 measured within +-0.2 % (tools/ab_redcap.sh)
+      static const int cap = getenv("ADAPTSEG_EXP_REDCAP") ? atoi(getenv("ADAPTSEG_EXP_REDCAP")) : 8192;  // A/B knob
+      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), cap);
       if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
       else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
       else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
