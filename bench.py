@@ -222,7 +222,11 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # RCCL on a high-priority stream, like the step's main chain (StepConfig.main_priority):
+            # the G all-reduce launched mid-step must not queue behind the discriminator kernels
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
         else:
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
