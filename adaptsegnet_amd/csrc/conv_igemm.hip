@@ -320,6 +320,7 @@ double conv_flops(const adaptseg_conv_desc *d) {
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
   if (!pl.fast) pl.s2 = pl.bf16 = false;
+  if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
   const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg], bn = pl.bf16 ? pl.bf16_bn : kCfgBN[pl.cfg];
   pl.bk = pl.bf16 ? 64 : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
@@ -410,8 +411,18 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   // Measured and rejected (tools/ab_cfg4.sh, two alternating runs): data gradient on cfg 6
   // (BK16, 4 blocks/CU instead of 2) -1.1 % c2 / -0.7 % c3; 1x1 weight gradients on cfg 6
   // -0.3 % / -1.1 %, on cfg 8 -1.2 % / -1.8 %.
-  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_DATA && getenv("ADAPTSEG_EXP_DGCFG"))  // A/B knob
-    pl.cfg = atoi(getenv("ADAPTSEG_EXP_DGCFG"));
+  // Stride-1 1x1 vector data gradients on the occupancy-3 BK-16 tile too (cfg 8: 121 VGPRs,
+  // no AGPRs, once the opt-in fused BN-sum epilogue is compiled out of that build; the cfg-0
+  // build needs 157 VGPRs + 64 AGPRs = 2 waves per SIMD).  tools/ab_dgcfg.sh, two alternating
+  // runs each: 1x1 only +2.5 % c2 / +1.8 % c3 / +-0 c5; every stride-1 product (3x3 too,
+  // ADAPTSEG_EXP_DG8_ALL) +1.6 % c2 but -4.4 % c3.  A/B knob: ADAPTSEG_EXP_DGCFG.
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_DATA) {
+    static const int dg_cfg = getenv("ADAPTSEG_EXP_DGCFG") ? atoi(getenv("ADAPTSEG_EXP_DGCFG")) : 8;
+    static const bool dg8_all = getenv("ADAPTSEG_EXP_DG8_ALL") != nullptr;  // A/B knob
+    pl.cfg = dg_cfg;
+    if (pl.cfg == 8 && !(d->stride == 1 && d->k % 16 == 0 && d->c % 4 == 0)) pl.cfg = 0;
+    if (pl.cfg == 8 && !dg8_all && d->kh * d->kw > 1) pl.cfg = 0;
+  }
   if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && getenv("ADAPTSEG_EXP_WGCFG"))  // A/B knob (1x1)
     pl.cfg = atoi(getenv("ADAPTSEG_EXP_WGCFG"));
   if (pl.cfg == 0 && op == ADAPTSEG_CONV_FWD) {
@@ -458,7 +469,13 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     pl.bf16_bn = (w256 && op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 256) ? 256 : 128;
   }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
-  if (pl.cfg == 8 && (op == ADAPTSEG_CONV_BWD_DATA || !pl.fast || pl.ae || pl.be || pl.s2)) pl.cfg = 0;
+  if (pl.cfg == 8 && (!pl.fast || pl.ae || pl.be || pl.s2)) {
+    if (op == ADAPTSEG_CONV_BWD_DATA) {  // screened above: unreachable unless misaligned
+      set_error("conv: data-gradient plan on cfg 8 without vector FAST operands");
+      return ADAPTSEG_ERR_ARG;
+    }
+    pl.cfg = 0;
+  }
   set_splits(pl);
   return ADAPTSEG_OK;
 }
@@ -732,6 +749,10 @@ int adaptseg_conv2d_bwd_data_bnsums(const adaptseg_conv_desc *d, const float *dy
     if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
   }
   if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
+  if (pl.cfg == 8 && !pl.bf16) {  // the fused BN-sum epilogue lives in the cfg-0 (BK 32) build
+    pl.cfg = 0;
+    pl.ae = d->k % fast_bk(0) != 0;
+  }
   set_splits(pl);
   p.out = dx;
   p.flags = 0;

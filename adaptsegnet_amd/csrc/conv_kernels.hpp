@@ -650,7 +650,7 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
 // (per segment, optional accumulate) and the fwd / data-grad epilogue (bias, accumulate,
 // residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
 // `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2>
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, bool BNSUM>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
                                                int bm, int bn, int tm, int tn, int split, int M, int Hc,
                                                int Wc, int py, int px, float *lds) {
@@ -797,7 +797,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
         if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
       }
     }
-    if constexpr (MODE == MODE_DGRAD && !S2) {
+    if constexpr (MODE == MODE_DGRAD && !S2 && BNSUM) {  // (not in the occupancy-3 build)
       // BatchNorm(+ReLU) backward sums of this row tile (the BN whose output this data
       // gradient is, model/deeplab_multi.py:65-98 bn1/bn2): g = dx * [relu'(bn(x))] with the
       // ReLU mask recomputed from the BN input x, s1 = sum g, s2 = sum g * (x - mean).  The BN
@@ -1302,7 +1302,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
   }
 
   // ---- epilogue ----
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, MINB == 1>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
 }
 
 

@@ -38,7 +38,12 @@ def test_workspace_and_kernel_selection_on_host():
     assert kid == 84                          # tap-GEMM: the 19-class head runs as a dense
     #                                           1x1 GEMM with N = 36 taps x 19 (pad 704)
     dgrad, _ = K.conv_kernel_id(aspp, 4, 64, 128, 1)
-    assert dgrad == 104                       # dX = G * W', K = 704: vector data-grad
+    assert dgrad == 184                       # dX = G * W', K = 704: 1x1 vector data-grad on cfg 8
+    kid, _ = K.conv_kernel_id(g, 4, 64, 128, 1)
+    assert kid == 104                         # 3x3 stride-1 data grad: 128x128 BK32 tile (cfg 0)
+    c1 = K.ConvGeom(1024, 256, 1, 1, 1, (0,), (1,))
+    kid, _ = K.conv_kernel_id(c1, 4, 64, 128, 1)
+    assert kid == 184                         # 1x1 data grad: occupancy-3 BK16 tile (cfg 8)
     d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))  # D classifier (Cout 1): the thin kernels
     kid, _ = K.conv_kernel_id(d5, 4, 32, 64, 0)
     assert kid == 80                          # vector-ALU thin forward
