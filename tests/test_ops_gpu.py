@@ -62,6 +62,9 @@ CONV_CASES = [
     (2, 64, 16, 24, 2, 3, 1, (1,), (1,), True),           # thin: the warper's output conv (Cout 2)
     (2, 32, 10, 14, 3, 3, 1, (2,), (2,), False),          # thin: Cout 3, dilated
     (1, 16, 9, 7, 4, 1, 1, (0,), (1,), True),             # thin: Cout 4, 1x1
+    (2, 256, 17, 23, 64, 1, 1, (0,), (1,), False),        # 1x1 dgrad on the occupancy-3 BK16 tile, ragged M
+    (2, 100, 13, 9, 48, 1, 1, (0,), (1,), False),         # ... ragged N (Cin 100), K = 48 (BK16 but not BK32)
+    (1, 1024, 3, 5, 256, 1, 1, (0,), (1,), False),        # ... split-K (M = 15: one row tile)
 ]
 
 
@@ -428,7 +431,8 @@ def test_to_nhwc_and_axpy():
 
 
 @pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1, 1), (4, 64, 128, 136, 256, 3, 2),
-                                   (4, 128, 96, 88, 128, 3, 1), (1, 64, 5, 7, 256, 1, 1)])
+                                   (4, 128, 96, 88, 128, 3, 1), (1, 64, 5, 7, 256, 1, 1),
+                                   (2, 128, 20, 18, 48, 1, 1)])
 @pytest.mark.parametrize("math", ["f32", "bf16"])
 def test_conv_dgrad_fused_bn_backward_sums(shape, math):
     """conv_dgrad_bnsums + bn_bwd_tiles (BN backward reduction fused into the data-gradient
