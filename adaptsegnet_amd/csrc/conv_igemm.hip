@@ -342,7 +342,9 @@ void set_splits(Plan &pl) {
   const int target = pl.mode == MODE_WGRAD ? wg_target : fd_target;
   // fwd / data-grad: grids of at most one block per CU (<= 256 tiles) split K in two — one
   // resident block per CU hides no latency (c3 target-domain layer3: +0.6 % step; grids of up
-  // to two blocks per CU split to four measured 2 % slower).  A/B knobs below.
+  // to two blocks per CU split to four measured 2 % slower).  A/B knobs below.  Re-measured
+  // after the data-gradient tile changes (tools/ab_splitbelow2.sh): 129 -0.1 % c2 / -1.2 % c3,
+  // 513 +0.2 % / +0.2 % (noise): 257 kept.
   static const int fd_below = getenv("ADAPTSEG_EXP_SPLITBELOW") ? atoi(getenv("ADAPTSEG_EXP_SPLITBELOW")) : 257;
   const int split_below = pl.mode == MODE_WGRAD ? target : fd_below;
   // Rounding: the blocks of a split grid are equal work, so the grid takes (the most blocks
