@@ -64,6 +64,7 @@ _SIGS = {
     "adaptseg_confusion_hist": [_L, _P, _P, _P, _I, _P, _P],
     "adaptseg_bn_fwd_train_tiles": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _I, _P],
     "adaptseg_conv2d_bnstats_size": [_DESC, ctypes.POINTER(ctypes.c_size_t)],
+    "adaptseg_conv2d_bnstats_tiles": [_DESC, ctypes.POINTER(_I)],
     "adaptseg_conv2d_fwd_bnstats": [_DESC, _P, _PP, _P, _P, _SZ, ctypes.POINTER(ctypes.c_int), _P, _SZ, _P],
     "adaptseg_bn_fwd_infer": [_L, _I, _P, _P, _P, _P, _P, _F, _P, _P, _I, _P],
     "adaptseg_bn_bwd": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
@@ -86,10 +87,6 @@ _SIGS = {
     "adaptseg_to_nhwc": [_I, _I, _I, _I, ctypes.POINTER(_L), _P, _P, _P],
     "adaptseg_axpy": [_L, _F, _P, _P, _I, _P],
     "adaptseg_add_i64": [_P, _L, _L, _P],
-    "adaptseg_conv2d_bnsums_size": [_DESC, ctypes.POINTER(_SZ)],
-    "adaptseg_conv2d_bwd_data_bnsums": [_DESC, _P, _PP, _P, _P, _P, _P, _P, _P, _P, _SZ,
-                                        ctypes.POINTER(_I), _P, _SZ, _P],
-    "adaptseg_bn_bwd_tiles": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adaptseg_preprocess_workspace_size": [_I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],
     "adaptseg_gta5_preprocess": [_I, _I, _I, _I, _I, _P, _F, _F, _F, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_bn_bwd_affine": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _SZ, _P],

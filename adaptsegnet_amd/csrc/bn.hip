@@ -369,9 +369,8 @@ static ApplyPlan apply_plan(int64_t rows, int C) {
   a.cblocks = (int)ceil_div(C / 4, a.tc);
   const int tr = 256 / a.tc;
   // ~2 blocks per CU: the apply passes run beside the weight-gradient GEMMs; 512 blocks measured
-  // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (tools/ab_bna.sh, two runs each)
-  static const int wantb = getenv("ADAPTSEG_EXP_BNA") ? atoi(getenv("ADAPTSEG_EXP_BNA")) : 512;  // A/B knob
-  const int want = std::max(1, wantb / a.cblocks);
+  // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (two runs each)
+  const int want = std::max(1, 512 / a.cblocks);
   const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * kApplyUnroll));
   a.rsplits = (int)std::min<int64_t>(want, maxs);
   a.per = ceil_div(rows, a.rsplits);
@@ -391,10 +390,9 @@ static ReducePlan reduce_plan(int64_t rows, int C) {
   // tc must divide 256
   while (256 % r.tc) --r.tc;
   r.cblocks = (int)ceil_div(C, 4 * r.tc);
-  // 512 blocks: 256 / 1024 measured -2 % / -4.5 % at c2 (tools/ab_bnr2.sh) — the reduction
-  // shares the chip with the weight-gradient GEMMs, more blocks take CUs from them
-  static const int wantb = getenv("ADAPTSEG_EXP_BNR") ? atoi(getenv("ADAPTSEG_EXP_BNR")) : 512;  // A/B knob
-  int want = std::max(1, wantb / r.cblocks);
+  // 512 blocks: 256 / 1024 measured -2 % / -4.5 % at c2 — the reduction shares the chip with
+  // the weight-gradient GEMMs, more blocks take CUs from them
+  int want = std::max(1, 512 / r.cblocks);
   int tr = 256 / r.tc;
   int64_t max_splits = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * 8));
   r.splits = (int)std::min<int64_t>(want, max_splits);
@@ -485,24 +483,6 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
   bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight,
                                                          bias, res, y, relu);
   AS_CHECK_LAUNCH("bn_infer_apply");
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles, const float *dy,
-                          const float *x, const float *weight, const float *bias, const float *save_mean,
-                          const float *save_invstd, float *coef, float *dx, float *dres,
-                          adaptseg_stream_t stream) {
-  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd_tiles: C%%4==0 required");
-  AS_CHECK_ARG(partial && ntiles > 0 && dy && x && save_mean && save_invstd && coef && dx,
-               "bn_bwd_tiles: null pointer");
-  hipStream_t s = as_stream(stream);
-  bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, ntiles, partial, save_invstd, coef);
-  AS_CHECK_LAUNCH("bn_bwd_final");
-  const ApplyPlan ap = apply_plan(rows, c);
-  bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, nullptr, x, weight,
-                                                                     bias, save_mean, save_invstd, coef, dx, dres,
-                                                                     2, 1);
-  AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
 }
 

@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
     }
   }
 
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, true>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }
 

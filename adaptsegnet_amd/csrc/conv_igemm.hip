@@ -332,29 +332,23 @@ void set_splits(Plan &pl) {
   }
   pl.tiles = (int)(ceil_div(p.M, bm) * ceil_div(p.N, bn));
   const int nkt = (int)ceil_div(p.K, pl.bk);
-  // fwd / data-grad: ~2 blocks per CU; weight-grad (K = every output pixel, few tiles): ~2.
+  // Split targets (measured on the step, not per shape; tools/ab.sh):
+  //  * weight gradients: ~512 blocks (two per CU), rounded down — 384 / 768 / 1024 measured
+  //    -3.2 / -2.3 / -2.5 % at c2 and -2.8 / -3.1 / -3.2 % at c3;
+  //  * fwd / data-grad: only grids of at most one block per CU (<= 256 tiles) split, to ~512
+  //    blocks — one resident block per CU hides no latency (c3 target-domain layer3: +0.6 %
+  //    step); splitting grids of up to two blocks per CU measured 2 % slower, a threshold of
+  //    129 tiles -0.1 % c2 / -1.2 % c3.
   // >= 4 K-steps per split keeps the slab traffic small next to the GEMM.
-  // weight-grad grids are almost always tiny.
-  // weight-gradient split target 512 blocks (two per CU), rounded down: 384 / 768 / 1024
-  // measured -3.2 / -2.3 / -2.5 % at c2 and -2.8 / -3.1 / -3.2 % at c3 (tools/ab_wgt2.sh)
-  static const int wg_target = getenv("ADAPTSEG_EXP_WGT") ? atoi(getenv("ADAPTSEG_EXP_WGT")) : 512;  // A/B knob
-  static const int fd_target = getenv("ADAPTSEG_EXP_FDTARGET") ? atoi(getenv("ADAPTSEG_EXP_FDTARGET")) : 512;  // A/B knob
-  const int target = pl.mode == MODE_WGRAD ? wg_target : fd_target;
-  // fwd / data-grad: grids of at most one block per CU (<= 256 tiles) split K in two — one
-  // resident block per CU hides no latency (c3 target-domain layer3: +0.6 % step; grids of up
-  // to two blocks per CU split to four measured 2 % slower).  A/B knobs below.  Re-measured
-  // after the data-gradient tile changes (tools/ab_splitbelow2.sh): 129 -0.1 % c2 / -1.2 % c3,
-  // 513 +0.2 % / +0.2 % (noise): 257 kept.
-  static const int fd_below = getenv("ADAPTSEG_EXP_SPLITBELOW") ? atoi(getenv("ADAPTSEG_EXP_SPLITBELOW")) : 257;
-  const int split_below = pl.mode == MODE_WGRAD ? target : fd_below;
-  // Rounding: the blocks of a split grid are equal work, so the grid takes (the most blocks
-  // any CU runs) x (one block's K range).  tiles * splits must therefore not overshoot a
-  // multiple of the CU count: ceil(512 / 36) = 15 splits puts 3 blocks on 28 CUs (0.2 units)
-  // where 14 puts at most 2 on every CU (0.143).  Round down (A/B knob: ADAPTSEG_EXP_SPLITCEIL).
-  static const bool split_ceil = getenv("ADAPTSEG_EXP_SPLITCEIL") != nullptr;
+  // Rounding: the blocks of a split grid are equal work, so the grid takes (the most blocks any
+  // CU runs) x (one block's K range); tiles * splits must not overshoot a multiple of the CU
+  // count: ceil(512 / 36) = 15 splits puts 3 blocks on 28 CUs (0.2 units) where 14 puts at most
+  // 2 on every CU (0.143) — round down.
+  constexpr int kSplitTarget = 512;
+  const int split_below = pl.mode == MODE_WGRAD ? kSplitTarget : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = split_ceil ? (int)ceil_div(target, pl.tiles) : std::max(1, target / pl.tiles);
+    splits = std::max(1, kSplitTarget / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -405,32 +399,20 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   // 128x128 tile at BK 16 (cfg 6: half the LDS, shorter K steps) measured faster than BK 32
   // for multi-tap weight gradients (+2-8 %, per-shape conv bench, profiles/r1/conv_cfg_ab.txt).
   if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && d->kh * d->kw > 1) pl.cfg = 6;
-  if ((pl.cfg == 0 || pl.cfg == 6) && getenv("ADAPTSEG_EXP_CFG")) pl.cfg = atoi(getenv("ADAPTSEG_EXP_CFG"));  // A/B knob
   // Forward products on the occupancy-3 BK-16 tile (cfg 8): +0.9 % c2 / +0.8 % c3 end to end
-  // (tools/ab_cfg3.sh, two alternating runs each) and 0.67 -> 0.69 of peak on the dominant
-  // forward symbol.  The weight gradients stay on cfg 6 (cfg 8 there: -0.7 %).  Non-FAST /
-  // per-element / stride-2 plans fall back to cfg 0 below.  A/B knob: ADAPTSEG_EXP_FWDCFG.
-  // Measured and rejected (tools/ab_cfg4.sh, two alternating runs): data gradient on cfg 6
-  // (BK16, 4 blocks/CU instead of 2) -1.1 % c2 / -0.7 % c3; 1x1 weight gradients on cfg 6
-  // -0.3 % / -1.1 %, on cfg 8 -1.2 % / -1.8 %.
+  // (two alternating runs each) and 0.67 -> 0.69 of peak on the dominant forward symbol.  The
+  // weight gradients stay on cfg 6 (cfg 8 there: -0.7 %).  Non-FAST / per-element / stride-2
+  // plans fall back to cfg 0 below.  Measured and rejected: data gradient on cfg 6 (BK16, 4
+  // blocks/CU instead of 2) -1.1 % c2 / -0.7 % c3; 1x1 weight gradients on cfg 6 -0.3 % /
+  // -1.1 %, on cfg 8 -1.2 % / -1.8 %.
   // Stride-1 1x1 vector data gradients on the occupancy-3 BK-16 tile too (cfg 8: 121 VGPRs,
-  // no AGPRs, once the opt-in fused BN-sum epilogue is compiled out of that build; the cfg-0
-  // build needs 157 VGPRs + 64 AGPRs = 2 waves per SIMD).  tools/ab_dgcfg.sh, two alternating
-  // runs each: 1x1 only +2.5 % c2 / +1.8 % c3 / +-0 c5; every stride-1 product (3x3 too,
-  // ADAPTSEG_EXP_DG8_ALL) +1.6 % c2 but -4.4 % c3.  A/B knob: ADAPTSEG_EXP_DGCFG.
-  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_DATA) {
-    static const int dg_cfg = getenv("ADAPTSEG_EXP_DGCFG") ? atoi(getenv("ADAPTSEG_EXP_DGCFG")) : 8;
-    static const bool dg8_all = getenv("ADAPTSEG_EXP_DG8_ALL") != nullptr;  // A/B knob
-    pl.cfg = dg_cfg;
-    if (pl.cfg == 8 && !(d->stride == 1 && d->k % 16 == 0 && d->c % 4 == 0)) pl.cfg = 0;
-    if (pl.cfg == 8 && !dg8_all && d->kh * d->kw > 1) pl.cfg = 0;
-  }
-  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_WEIGHT && getenv("ADAPTSEG_EXP_WGCFG"))  // A/B knob (1x1)
-    pl.cfg = atoi(getenv("ADAPTSEG_EXP_WGCFG"));
-  if (pl.cfg == 0 && op == ADAPTSEG_CONV_FWD) {
-    static const int fwd_cfg = getenv("ADAPTSEG_EXP_FWDCFG") ? atoi(getenv("ADAPTSEG_EXP_FWDCFG")) : 8;
-    pl.cfg = fwd_cfg;
-  }
+  // no AGPRs; the cfg-0 build needs 2 waves per SIMD): +2.5 % c2 / +1.8 % c3 / +-0 c5.  Every
+  // stride-1 product (3x3 too) on it measured +1.6 % c2 but -4.4 % c3, so the 3x3 ones stay on
+  // cfg 0 (its min-blocks-2 build, conv_launch_body.inc).
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_BWD_DATA && d->stride == 1 && d->k % 16 == 0 && d->c % 4 == 0 &&
+      d->kh * d->kw == 1)
+    pl.cfg = 8;
+  if (pl.cfg == 0 && op == ADAPTSEG_CONV_FWD) pl.cfg = 8;
   p.fd_nseg_k = make_fastdiv(p.kseg);
   pl.flops = conv_flops(d);
   // FAST path eligibility (alignment re-checked at launch).  Vector operands need tile-
@@ -540,9 +522,8 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     if (vec) {
       const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
       const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
-      // grid cap: 512 / 1024 / 8192 measured within +-0.2 % (tools/ab_redcap.sh)
-      static const int cap = getenv("ADAPTSEG_EXP_REDCAP") ? atoi(getenv("ADAPTSEG_EXP_REDCAP")) : 8192;  // A/B knob
-      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), cap);
+      // grid cap: 512 / 1024 / 8192 measured within +-0.2 %
+      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
       if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
       else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
       else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
@@ -556,12 +537,8 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
 }
 
 
-// Thin convs (Cout <= 4) go to the vector-ALU kernels of conv_thin.hip (A/B knob:
-// ADAPTSEG_NO_THIN=1 keeps them on the implicit GEMM).
-bool use_thin(const adaptseg_conv_desc *d, int op) {
-  static const bool off = getenv("ADAPTSEG_NO_THIN") != nullptr;
-  return !off && thin_eligible(d, op);
-}
+// Thin convs (Cout <= 4) go to the vector-ALU kernels of conv_thin.hip.
+bool use_thin(const adaptseg_conv_desc *d, int op) { return thin_eligible(d, op); }
 
 }  // namespace adaptseg
 
@@ -653,6 +630,17 @@ int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
   return ADAPTSEG_OK;
 }
 
+int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
+  AS_CHECK_ARG(ntiles, "conv2d_bnstats_tiles: null");
+  *ntiles = 0;
+  Plan pl;
+  int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
+  if (st) return st;
+  if (tapgemm_eligible(d)) return ADAPTSEG_OK;
+  if (pl.fast && pl.p.splits == 1) *ntiles = (int)ceil_div(pl.p.M, pl.bf16 ? 128 : kCfgBM[pl.cfg]);
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w, float *y,
                                 float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
                                 adaptseg_stream_t stream) {
@@ -717,61 +705,6 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   p.res = res;
   p.aux = aux;
   p.flags = flags;
-  return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
-}
-
-int adaptseg_conv2d_bnsums_size(const adaptseg_conv_desc *d, size_t *bytes) {
-  AS_CHECK_ARG(bytes, "conv2d_bnsums_size: null");
-  int st = validate(d);
-  if (st) return st;
-  // data-gradient rows = input pixels; the smallest row tile any config uses (128)
-  const int64_t nt = ceil_div((int64_t)d->n * d->h * d->w, 128);
-  *bytes = (size_t)(2 * (int64_t)d->c * nt) * sizeof(float);
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_conv2d_bwd_data_bnsums(const adaptseg_conv_desc *d, const float *dy, const float *const *w, float *dx,
-                                    const float *bn_x, const float *bn_mean, const float *bn_invstd,
-                                    const float *bn_weight, const float *bn_bias, float *partial,
-                                    size_t partial_bytes, int *ntiles, void *ws, size_t ws_bytes,
-                                    adaptseg_stream_t stream) {
-  AS_CHECK_ARG(ntiles && partial && bn_x && bn_mean && bn_invstd, "conv bwd_data_bnsums: null BN argument");
-  *ntiles = 0;
-  Plan pl;
-  int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
-  if (st) return st;
-  AS_CHECK_ARG(dy && w && dx, "conv bwd_data_bnsums: null pointer");
-  for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data_bnsums: null weight %d", s);
-  if (tapgemm_eligible(d))  // no fused sums on the tap-GEMM path: plain data gradient
-    return adaptseg_conv2d_bwd_data(d, dy, w, nullptr, nullptr, dx, 0, ws, ws_bytes, stream);
-  ConvParams &p = pl.p;
-  p.dy = dy;
-  for (int s = 0; s < d->nseg; ++s) {
-    p.wt[s] = w[s];
-    if (reinterpret_cast<uintptr_t>(w[s]) & 15) pl.vb = pl.fast = false;
-  }
-  if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
-  if (pl.cfg == 8 && !pl.bf16) {  // the fused BN-sum epilogue lives in the cfg-0 (BK 32) build
-    pl.cfg = 0;
-    pl.ae = d->k % fast_bk(0) != 0;
-  }
-  set_splits(pl);
-  p.out = dx;
-  p.flags = 0;
-  if (pl.fast && !pl.s2 && p.splits == 1) {
-    const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg];
-    const int nt = (int)ceil_div(p.M, bm);
-    if ((size_t)(2 * (int64_t)p.N * nt) * sizeof(float) <= partial_bytes) {
-      p.bnsum = partial;
-      p.stats_ntiles = nt;
-      p.bn_x = bn_x;
-      p.bn_mean = bn_mean;
-      p.bn_invstd = bn_invstd;
-      p.bn_w = bn_weight;
-      p.bn_b = bn_bias;
-      *ntiles = nt;
-    }
-  }
   return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
 }
 

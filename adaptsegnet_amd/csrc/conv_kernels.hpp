@@ -56,10 +56,6 @@ struct ConvParams {
   FastDiv fd_taps, fd_kw;
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
-  // DGRAD (splits == 1, stride 1, no epilogue flags) feeding a train-mode BN+ReLU backward:
-  // per-row-tile sums of g = dx*[bn_affine(bn_x) > 0] and g*(bn_x - mean) -> bnsum[2][N][nt]
-  float *bnsum;
-  const float *bn_x, *bn_mean, *bn_invstd, *bn_w, *bn_b;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
 
@@ -650,7 +646,7 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
 // (per segment, optional accumulate) and the fwd / data-grad epilogue (bias, accumulate,
 // residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
 // `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, bool BNSUM>
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
                                                int bm, int bn, int tm, int tn, int split, int M, int Hc,
                                                int Wc, int py, int px, float *lds) {
@@ -795,68 +791,6 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
           }
         }
         if (tid == 0 && tn == 0) p.stats[tm] = (float)nvalid;
-      }
-    }
-    if constexpr (MODE == MODE_DGRAD && !S2 && BNSUM) {  // (not in the occupancy-3 build)
-      // BatchNorm(+ReLU) backward sums of this row tile (the BN whose output this data
-      // gradient is, model/deeplab_multi.py:65-98 bn1/bn2): g = dx * [relu'(bn(x))] with the
-      // ReLU mask recomputed from the BN input x, s1 = sum g, s2 = sum g * (x - mean).  The BN
-      // backward then skips its reduction pass over dx and x (bn_bwd_tiles).
-      if (p.bnsum) {
-        __syncthreads();
-        float *red = lds;  // [2][WAVES_M][BN]
-        const int nvalid = min(BM, M - bm);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = bn + wn * WTN + j * 32 + l32;
-          const int cc = min(col, p.N - 1);
-          const float mu = p.bn_mean[cc], is = p.bn_invstd[cc];
-          const float bw = p.bn_w ? p.bn_w[cc] : 1.f, bb = p.bn_b ? p.bn_b[cc] : 0.f;
-          float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            // 16 unconditional (clamped) loads in flight together, then the sums: a guarded
-            // load per element would serialise 16*TM*TN load latencies per block
-            float xv[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              xv[r] = p.bn_x[(size_t)(bm + min(rl, nvalid - 1)) * p.N + cc];
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rl = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              const bool ok = rl < nvalid && col < p.N;
-              const float d = xv[r] - mu;
-              const float g = (ok && d * is * bw + bb > 0.f) ? acc[i][j][r] : 0.f;
-              s1 += g;
-              s2 += g * d;
-            }
-          }
-          s1 += __shfl_xor(s1, 32);
-          s2 += __shfl_xor(s2, 32);
-          if (hh == 0) {
-            red[wm * BN + wn * WTN + j * 32 + l32] = s1;
-            red[(WAVES_M + wm) * BN + wn * WTN + j * 32 + l32] = s2;
-          }
-        }
-        __syncthreads();
-        const int nt = p.stats_ntiles;
-        if (wm == 0 && hh == 0) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = bn + wn * WTN + j * 32 + l32;
-            if (col >= p.N) continue;
-            float a = 0.f, b = 0.f;
-#pragma unroll
-            for (int q = 0; q < WAVES_M; ++q) {
-              a += red[q * BN + wn * WTN + j * 32 + l32];
-              b += red[(WAVES_M + q) * BN + wn * WTN + j * 32 + l32];
-            }
-            p.bnsum[(size_t)col * nt + tm] = a;
-            p.bnsum[((size_t)p.N + col) * nt + tm] = b;
-          }
-        }
       }
     }
   }
@@ -1302,7 +1236,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
   }
 
   // ---- epilogue ----
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, MINB == 1>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
 }
 
 

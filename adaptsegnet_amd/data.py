@@ -17,15 +17,12 @@ Split of the work:
 """
 from __future__ import annotations
 
-import ctypes
 import os.path as osp
 
 import numpy as np
 import torch
 
-from . import _lib
-from ._lib import check
-from .kernels import _p, _stream, _ws_args
+from .ops import OPS
 
 IMG_MEAN = np.array((104.00698793, 116.66876762, 122.67891434), dtype=np.float32)  # train:30
 ID_TO_TRAINID = {7: 0, 8: 1, 11: 2, 12: 3, 13: 4, 17: 5, 19: 6, 20: 7, 21: 8, 22: 9, 23: 10, 24: 11,
@@ -71,15 +68,9 @@ def preprocess(images: torch.Tensor, labels: torch.Tensor | None = None, crop_si
         lab_out = torch.empty((n, oh, ow), device=images.device, dtype=torch.int64)
         if lut is None:
             lut = trainid_lut(images.device)
-    b = ctypes.c_size_t(0)
-    check(_lib.lib().adaptseg_preprocess_workspace_size(n, h, w, oh, ow, ctypes.byref(b)),
-          "preprocess_workspace_size")
-    wp, wsz = _ws_args(b.value, images.device)
     m = np.asarray(mean, dtype=np.float32)
-    check(_lib.lib().adaptseg_gta5_preprocess(
-        n, h, w, oh, ow, _p(images), float(m[0]), float(m[1]), float(m[2]), _p(out),
-        _p(labels), _p(lut) if labels is not None else None, _p(lab_out), wp, wsz, _stream()),
-        "gta5_preprocess")
+    OPS.gta5_preprocess(images, [float(m[0]), float(m[1]), float(m[2])], out, labels,
+                        lut if labels is not None else None, lab_out)
     return out, lab_out
 
 

@@ -20,8 +20,6 @@ Reference semantics followed (file:line in /root/reference):
 """
 from __future__ import annotations
 
-import contextlib
-import os
 
 import torch
 
@@ -64,41 +62,8 @@ class WgradStream:
 
     def join(self):
         if self.used:
-            if _DEFERRED_JOIN["on"]:
-                _DEFERRED_JOIN["pending"].add(self.side)
-            else:
-                self.main.wait_stream(self.side)
+            self.main.wait_stream(self.side)
             self.used = False
-
-
-# Deferred weight-gradient joins (used by AdaptSegTrainer inside a step): a backward normally
-# makes the main stream wait for its weight-gradient side stream before returning, so `.grad`
-# is complete in stream order for any caller.  Inside the trainer nothing reads the gradient
-# arenas until the all-reduce / optimiser, so the trainer can defer those waits and join once,
-# right before them — the main chain never idles behind a side-stream backlog mid-step.
-# Measured +0.2 % c2 / +0.3 % c3 (tools/ab_defer.sh): opt-in (ADAPTSEG_EXP_DEFERJOIN=1).
-_DEFERRED_JOIN = {"on": False, "pending": set()}
-
-
-@contextlib.contextmanager
-def deferred_wgrad_join():
-    prev = _DEFERRED_JOIN["on"]
-    _DEFERRED_JOIN["on"] = True
-    try:
-        yield
-    finally:
-        _DEFERRED_JOIN["on"] = prev
-        join_deferred()
-
-
-def join_deferred():
-    """The current stream waits for every weight-gradient side stream whose join was deferred."""
-    pending = _DEFERRED_JOIN["pending"]
-    if pending:
-        main = torch.cuda.current_stream()
-        for side in pending:
-            main.wait_stream(side)
-        pending.clear()
 
 
 # ---------------------------------------------------------------------------------------
@@ -123,14 +88,10 @@ def bn_forward(bn, x, res, relu, training, tiles=None):
     return y, (bn.running_mean, None, False)
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, sums=None):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
-    mode instead of reading the saved output y (one activation read less per pass).
-    sums: the row-tile backward sums fused into the producing data-gradient conv
-    (_dgrad_into_bn), which replace the BN's own reduction pass."""
+    mode instead of reading the saved output y (one activation read less per pass)."""
     mean, invstd, train = st
-    if sums is not None:
-        return K.bn_bwd_tiles(dy, x, bn.weight, bn.bias, mean, invstd, sums, dx=dx, dres=dres)
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
     elif mask_from_x and relu:
@@ -194,38 +155,22 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
         ws.launch(run, dy, x)
 
 
-# BN-backward sums fused into the data-gradient epilogue: measured NET SLOWER at c2 (225 vs
-# 218 ms/step — the epilogue's extra read of the BN input costs the dgrad kernel more than the
-# bn1/bn2 reduction passes it removes, which are the small 1/4-width BNs), so opt-in only.
-_NO_BNSUMS = os.environ.get("ADAPTSEG_BNSUMS") != "1"
-
-
-def _dgrad_into_bn(g, dy, n, h, w, weight, bn, bn_x, st):
-    """Data gradient feeding a BN+ReLU backward; with a train-mode BN also its fused sums."""
-    mean, invstd, train = st
-    if not train or _NO_BNSUMS:
-        return K.conv_dgrad(g, dy, n, h, w, [weight]), None
-    return K.conv_dgrad_bnsums(g, dy, n, h, w, [weight], bn_x, mean, invstd, bn.weight, bn.bias)
-
-
 def block_backward(blk, rec, gout, need_w, ws=None):
     """gout: grad of the block output (owned, modified in place).  Returns grad of the input."""
     n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
     dc3 = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout)
-    # conv3 / conv2 data gradients are the gradients of bn2 / bn1 outputs: their epilogues also
-    # produce those BNs' backward sums (train mode), so the BN backward is finalize + apply.
-    dy2, t2 = _dgrad_into_bn(g3, dc3, n, oh, ow, blk.conv3.weight, blk.bn2, rec.c2, rec.s2)
+    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight])
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
     del dc3
-    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, sums=t2)
-    dy1, t1 = _dgrad_into_bn(g2, dy2, n, oh, ow, blk.conv2.weight, blk.bn1, rec.c1, rec.s1)
+    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True)
+    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
     del dy2
-    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, sums=t1)
+    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True)
     if need_w and blk.conv1.weight.grad is not None:
         _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
     if blk.downsample is not None:

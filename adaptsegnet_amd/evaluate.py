@@ -18,9 +18,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _lib
 from . import kernels as K
-from ._lib import check
+from .ops import OPS
 
 # Cityscapes id -> trainId (the devkit's label2train; 19 classes of dataset/gta5_dataset.py:27-29)
 CITYSCAPES_TRAIN_IDS = {7: 0, 8: 1, 11: 2, 12: 3, 13: 4, 17: 5, 19: 6, 20: 7, 21: 8, 22: 9, 23: 10,
@@ -47,8 +46,7 @@ def upsample_argmax(logits: torch.Tensor, out_hw) -> torch.Tensor:
     n, h, w, c = x.shape
     oh, ow = int(out_hw[0]), int(out_hw[1])
     out = torch.empty((n, oh, ow), dtype=torch.uint8, device=logits.device)
-    check(_lib.lib().adaptseg_upsample_argmax(n, c, h, w, oh, ow, K._p(x), K._p(out), K._stream()),
-          "upsample_argmax")
+    OPS.upsample_argmax(x, out)
     return out
 
 
@@ -77,8 +75,7 @@ class ConfusionMatrix:
         if gt_ids.numel() != pred.numel():
             raise RuntimeError(f"ConfusionMatrix.update: {gt_ids.numel()} labels vs {pred.numel()} predictions")
         gt_ids, pred = gt_ids.contiguous(), pred.contiguous()
-        check(_lib.lib().adaptseg_confusion_hist(gt_ids.numel(), K._p(gt_ids), K._p(self.lut), K._p(pred),
-                                                 self.n, K._p(self.hist), K._stream()), "confusion_hist")
+        OPS.confusion_hist(gt_ids, self.lut, pred, self.n, self.hist)
 
     def numpy(self) -> np.ndarray:
         return self.hist.cpu().numpy()

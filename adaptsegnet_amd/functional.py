@@ -47,11 +47,13 @@ def softmax2d(x: torch.Tensor) -> torch.Tensor:
 
 class _CrossEntropy2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, ignore, weight):
+    def forward(ctx, logits, labels, ignore, weight, total):
         x = K.nhwc_view(logits)
-        out = K.ce_fwd(x, labels, ignore, weight)
+        out = K.ce_fwd(x, labels, ignore, weight)   # [mean, denominator]
         ctx.save_for_backward(x, labels, out, weight)
-        ctx.ignore = ignore
+        ctx.ignore, ctx.total = ignore, total
+        if total:   # reduction='sum': mean * denominator; an empty selection sums to 0
+            return torch.where(out[1] > 0, out[0] * out[1], torch.zeros_like(out[0]))
         return out[0]
 
     @staticmethod
@@ -59,17 +61,22 @@ class _CrossEntropy2d(torch.autograd.Function):
         x, labels, out, weight = ctx.saved_tensors
         if g.dim() == 0:
             g = g.reshape(1)
+        if ctx.total:   # d(sum)/dlogits = denominator * d(mean)/dlogits
+            g = g * out[1:2]
         dl = K.ce_bwd(x, labels, out, g.contiguous(), ctx.ignore, weight)
-        return K.as_nchw(dl), None, None, None
+        return K.as_nchw(dl), None, None, None, None
 
 
 def cross_entropy2d(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = 255,
-                    weight: torch.Tensor | None = None) -> torch.Tensor:
-    """Mean softmax cross entropy over pixels whose label is >= 0 and != ignore_index.
+                    weight: torch.Tensor | None = None, reduction: str = "mean") -> torch.Tensor:
+    """Softmax cross entropy over pixels whose label is >= 0 and != ignore_index.
 
-    logits: [N, C, H, W] fp32; labels: [N, H, W] int64.  Returns a 0-dim device tensor;
-    an all-ignored batch gives NaN like the reference.
+    logits: [N, C, H, W] fp32; labels: [N, H, W] int64.  reduction 'mean' (weighted by
+    ``weight[label]`` when given) or 'sum'.  Returns a 0-dim device tensor; an all-ignored
+    batch gives NaN for the mean (like the reference) and 0 for the sum (F.cross_entropy).
     """
+    if reduction not in ("mean", "sum"):
+        raise ValueError(f"cross_entropy2d: reduction {reduction!r} (expected 'mean' or 'sum')")
     _check(logits, "cross_entropy2d")
     if labels.dtype != torch.int64:
         raise RuntimeError(f"cross_entropy2d: labels must be int64 (got {labels.dtype})")
@@ -79,7 +86,7 @@ def cross_entropy2d(logits: torch.Tensor, labels: torch.Tensor, ignore_index: in
     labels = labels.contiguous()
     if weight is not None:
         weight = weight.to(device=logits.device, dtype=torch.float32).contiguous()
-    return _CrossEntropy2d.apply(logits, labels, int(ignore_index), weight)
+    return _CrossEntropy2d.apply(logits, labels, int(ignore_index), weight, reduction == "sum")
 
 
 class _AdvLoss(torch.autograd.Function):

@@ -1,0 +1,462 @@
+"""``torch.ops.adaptseg``: the native op surface as PyTorch custom operators.
+
+Every compute launch of the package goes through one of these operators (registered with
+``torch.library``: a schema, a CUDA (= HIP on ROCm) kernel and a fake/meta kernel), so the
+launches are visible to the dispatcher — torch.profiler records them by name, FakeTensor /
+``torch.library.opcheck`` can trace them — while the native boundary stays the C ABI of
+include/adaptseg.h: each CUDA kernel below is a thin ctypes call into libadaptseg.so.
+
+There is no CPU kernel: calling an op on CPU tensors raises NotImplementedError from the
+dispatcher (the product path has no fallback).  All ops are out-variant: outputs (and
+state such as BN running statistics or optimiser buffers) are caller-allocated and declared
+mutable (``Tensor(a!)``) in the schema, every op returns ``()``, and ``adaptsegnet_amd.kernels``
+allocates and calls them.  Activations are NHWC buffers ``[n, h, w, c]`` (the physical layout
+of channels_last NCHW tensors) unless an argument says otherwise; conv weights are any
+tensors whose memory is [Cout][KH][KW][Cin] (the modules' NCHW-shaped channels_last
+parameters), their logical shape given by ``w_shape`` = [Cout, Cin, KH, KW].  Some engine
+calls alias a read-only input with a mutable output (in-place BN backward, residual folded
+into the data-gradient output); the kernels support that, and it is why these ops are not
+meant for torch.compile's functionalization.
+
+Reference call sites the ops stand in for (file:line in /root/reference):
+  conv2d_*            nn.Conv2d in model/deeplab_multi.py:64-75,112,128 / discriminator.py:10-14
+  bn_*                nn.BatchNorm2d (+ReLU, residual)  model/deeplab_multi.py:65-101,130-135
+  maxpool2d_*         nn.MaxPool2d(3, 2, 1)             model/deeplab_multi.py:135
+  upsample_bilinear_* nn.Upsample(bilinear, align_corners=True)  model/deeplab_multi.py:188-189
+  softmax_*           F.softmax(pred)                   train_gta2cityscapes_multi.py:617-618
+  softmax_ce_*        nn.CrossEntropyLoss(ignore_index=255) / CrossEntropy2d  train:546, utils/loss.py:7-36
+  adv_loss_*          BCEWithLogitsLoss / MSELoss vs a constant label  train:542-545,620-624
+  sgd_step/adam_step  optim.SGD / optim.Adam            train:532-540
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, MATH_F32, ConvDesc, check
+
+LIB = torch.library.Library("adaptseg", "DEF")
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _ptrs(ts):
+    return _lib.ptr_array([None if t is None else t.data_ptr() for t in ts])
+
+
+# One growing scratch buffer per (device, stream): ops on one stream run in order, so reusing
+# it across consecutive calls is race-free.  Caller-owned from the C ABI's point of view.
+_WS: dict = {}
+
+
+def workspace(nbytes: int, device: torch.device):
+    if nbytes == 0:
+        return None
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        cap = max(nbytes, 0 if buf is None else int(buf.numel() * 1.25))
+        buf = torch.empty(cap, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _ws_args(nbytes: int, device):
+    w = workspace(nbytes, device)
+    return (ctypes.c_void_p(w.data_ptr()) if w is not None else None), ctypes.c_size_t(nbytes)
+
+
+# ---------------------------------------------------------------------------------------
+# Conv descriptors (host planning only: no GPU needed)
+# ---------------------------------------------------------------------------------------
+_DESC_CACHE: dict = {}
+_CONV_MATH = [MATH_F32]
+
+
+def conv_desc(n, c, h, w, strides, cout, kh, kw, stride, pads, dils):
+    """(ConvDesc, {op: workspace bytes}, oh, ow) of one conv product, cached."""
+    key = (n, c, h, w, strides, cout, kh, kw, stride, pads, dils, _CONV_MATH[0])
+    d = _DESC_CACHE.get(key)
+    if d is None:
+        p, dl = pads[0], dils[0]
+        oh = (h + 2 * p - dl * (kh - 1) - 1) // stride + 1
+        ow = (w + 2 * p - dl * (kw - 1) - 1) // stride + 1
+        desc = ConvDesc()
+        desc.n, desc.c, desc.h, desc.w = n, c, h, w
+        for i in range(4):
+            desc.in_stride[i] = strides[i]
+        desc.k, desc.oh, desc.ow = cout, oh, ow
+        desc.kh, desc.kw, desc.stride, desc.nseg = kh, kw, stride, len(pads)
+        for i in range(len(pads)):
+            desc.pad[i] = pads[i]
+            desc.dil[i] = dils[i]
+        ws = {}
+        for op in (CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT):
+            b = ctypes.c_size_t(0)
+            check(_lib.lib().adaptseg_conv2d_workspace_size(ctypes.byref(desc), op, ctypes.byref(b)),
+                  "conv2d_workspace_size")
+            ws[op] = b.value
+        d = _DESC_CACHE[key] = (desc, ws, oh, ow)
+    return d
+
+
+def set_math(math: int) -> None:
+    check(_lib.lib().adaptseg_conv_set_math(int(math)), "conv_set_math")
+    _CONV_MATH[0] = int(math)
+
+
+def _wdesc(in_shape, in_stride, w_shape, stride, pad, dil):
+    co, _ci, kh, kw = w_shape
+    n, c, h, w = in_shape
+    return conv_desc(n, c, h, w, tuple(in_stride), co, kh, kw, stride, tuple(pad), tuple(dil))
+
+
+def _nhwc_strides(n, h, w, c):
+    return (h * w * c, 1, w * c, c)
+
+
+# ---------------------------------------------------------------------------------------
+# Registration
+# ---------------------------------------------------------------------------------------
+def _fake(*args, **kwargs):
+    return None
+
+
+NAMES: list = []
+
+
+def _op(schema):
+    """Define adaptseg::<schema> with the decorated function as its CUDA kernel."""
+    name = schema.split("(", 1)[0]
+
+    def deco(fn):
+        NAMES.append(name)
+        LIB.define(schema)
+        LIB.impl(name, fn, "CUDA")
+        torch.library.register_fake(f"adaptseg::{name}", _fake, lib=LIB)
+        return fn
+    return deco
+
+
+# ---- convolution ------------------------------------------------------------------------
+@_op("conv2d_fwd(Tensor x, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, int[] in_shape, "
+     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_fwd(x, weight, bias, res, out, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    check(_lib.lib().adaptseg_conv2d_fwd(
+        ctypes.byref(d), _p(x), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out), flags,
+        wp, wsz, _stream()), "conv2d_fwd")
+
+
+@_op("conv2d_fwd_bnstats(Tensor x, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, int[] in_shape, "
+     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int ntiles) -> ()")
+def _conv2d_fwd_bnstats(x, weight, out, stats, in_shape, in_stride, w_shape, stride, pad, dil, ntiles):
+    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    nt = ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv2d_fwd_bnstats(
+        ctypes.byref(d), _p(x), _ptrs(weight), _p(out), _p(stats), ctypes.c_size_t(stats.numel() * 4),
+        ctypes.byref(nt), wp, wsz, _stream()), "conv2d_fwd_bnstats")
+    if nt.value != ntiles:
+        raise RuntimeError(f"conv2d_fwd_bnstats: planned {ntiles} statistics tiles, the launch produced "
+                           f"{nt.value} (unaligned operand?)")
+
+
+@_op("conv2d_bwd_data(Tensor dy, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, int[] in_shape, "
+     "int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_bwd_data(dy, weight, res, aux, dx, in_shape, w_shape, stride, pad, dil, flags):
+    n, c, h, w = in_shape
+    d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
+    check(_lib.lib().adaptseg_conv2d_bwd_data(
+        ctypes.byref(d), _p(dy), _ptrs(weight), _p(res), _p(aux), _p(dx), flags, wp, wsz, _stream()),
+        "conv2d_bwd_data")
+
+
+@_op("conv2d_bwd_weight(Tensor dy, Tensor x, Tensor(a!)[] dw, Tensor(b!)[] db, int[] in_shape, "
+     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_bwd_weight(dy, x, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dy.device)
+    check(_lib.lib().adaptseg_conv2d_bwd_weight(
+        ctypes.byref(d), _p(dy), _p(x), _ptrs(dw), _ptrs(db) if len(db) else None, flags, wp, wsz,
+        _stream()), "conv2d_bwd_weight")
+
+
+# ---- batch norm (x as [rows, C]: the NHWC buffer) ------------------------------------------
+_BN_WS: dict = {}
+
+
+def bn_ws_bytes(rows, c):
+    v = _BN_WS.get((rows, c))
+    if v is None:
+        b = ctypes.c_size_t(0)
+        check(_lib.lib().adaptseg_bn_workspace_size(rows, c, ctypes.byref(b)), "bn_workspace_size")
+        v = _BN_WS[(rows, c)] = b.value
+    return v
+
+
+def _rc(t):
+    c = t.shape[-1]
+    return t.numel() // c, c
+
+
+@_op("bn_fwd_train(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+     "Tensor? res, Tensor(c!) y, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
+def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, mean, invstd, momentum, eps, act):
+    rows, c = _rc(x)
+    wp, wsz = _ws_args(bn_ws_bytes(rows, c), x.device)
+    check(_lib.lib().adaptseg_bn_fwd_train(
+        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(momentum), float(eps),
+        _p(mean), _p(invstd), _p(res), _p(y), int(act), wp, wsz, _stream()), "bn_fwd_train")
+
+
+@_op("bn_fwd_train_tiles(Tensor x, Tensor stats, int ntiles, Tensor? weight, Tensor? bias, "
+     "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!) y, Tensor(d!) mean, "
+     "Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
+def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, mean, invstd,
+                        momentum, eps, act):
+    rows, c = _rc(x)
+    check(_lib.lib().adaptseg_bn_fwd_train_tiles(
+        rows, c, _p(stats), int(ntiles), _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
+        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), int(act), _stream()),
+        "bn_fwd_train_tiles")
+
+
+@_op("bn_fwd_infer(Tensor x, Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
+     "Tensor? res, Tensor(a!) y, float eps, int act) -> ()")
+def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, eps, act):
+    rows, c = _rc(x)
+    check(_lib.lib().adaptseg_bn_fwd_infer(
+        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps), _p(res), _p(y),
+        int(act), _stream()), "bn_fwd_infer")
+
+
+@_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
+     "Tensor(a!) dx, Tensor(b!)? dres, int act, bool train) -> ()")
+def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dres, act, train):
+    rows, c = _rc(dy)
+    wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)
+    check(_lib.lib().adaptseg_bn_bwd(
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dres), int(act),
+        1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+
+
+@_op("bn_bwd_affine(Tensor dy, Tensor? y, Tensor x, Tensor? weight, Tensor? bias, Tensor mean, "
+     "Tensor invstd, Tensor(a!) dx, int act, Tensor(b!)? dweight, Tensor(c!)? dbias) -> ()")
+def _bn_bwd_affine(dy, y, x, weight, bias, mean, invstd, dx, act, dweight, dbias):
+    rows, c = _rc(dy)
+    wp, wsz = _ws_args(bn_ws_bytes(rows, c), dy.device)
+    check(_lib.lib().adaptseg_bn_bwd_affine(
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), None, int(act),
+        _p(dweight), _p(dbias), wp, wsz, _stream()), "bn_bwd_affine")
+
+
+# ---- warper -------------------------------------------------------------------------------
+@_op("up2_relu_cat_fwd(Tensor? s, Tensor d, Tensor(a!) out) -> ()")
+def _up2_relu_cat_fwd(s, d, out):
+    n, h, w, cd = d.shape
+    cs = 0 if s is None else s.shape[-1]
+    check(_lib.lib().adaptseg_up2_relu_cat_fwd(n, h, w, cs, cd, _p(s), _p(d), _p(out), _stream()),
+          "up2_relu_cat_fwd")
+
+
+@_op("up2_relu_cat_bwd(Tensor? s, Tensor d, Tensor dout, Tensor(a!)? ds, Tensor(b!) dd) -> ()")
+def _up2_relu_cat_bwd(s, d, dout, ds, dd):
+    n, h, w, cd = d.shape
+    cs = 0 if s is None else s.shape[-1]
+    check(_lib.lib().adaptseg_up2_relu_cat_bwd(n, h, w, cs, cd, _p(s), _p(d), _p(dout), _p(ds), _p(dd),
+                                               _stream()), "up2_relu_cat_bwd")
+
+
+@_op("grid_warp_fwd(Tensor flow, Tensor? x1, Tensor x2, Tensor(a!)? y1, Tensor(b!) y2) -> ()")
+def _grid_warp_fwd(flow, x1, x2, y1, y2):
+    n, h, w, c = x2.shape
+    check(_lib.lib().adaptseg_grid_warp_fwd(n, c, h, w, flow.shape[-1], _p(flow), _p(x1), _p(x2), _p(y1),
+                                            _p(y2), _stream()), "grid_warp_fwd")
+
+
+@_op("grid_warp_bwd(Tensor flow, Tensor? x1, Tensor? x2, Tensor? dy1, Tensor? dy2, Tensor(a!)? dflow, "
+     "Tensor(b!)? dx1, Tensor(c!)? dx2) -> ()")
+def _grid_warp_bwd(flow, x1, x2, dy1, dy2, dflow, dx1, dx2):
+    ref = dy2 if dy2 is not None else dy1
+    n, h, w, c = ref.shape
+    nbytes = 0
+    if dx1 is not None or dx2 is not None:
+        b = ctypes.c_size_t(0)
+        check(_lib.lib().adaptseg_grid_warp_bwd_workspace_size(n, c, h, w, ctypes.byref(b)),
+              "grid_warp_bwd_workspace_size")
+        nbytes = b.value
+    wp, wsz = _ws_args(nbytes, ref.device)
+    check(_lib.lib().adaptseg_grid_warp_bwd(
+        n, c, h, w, flow.shape[-1], _p(flow), _p(x1), _p(x2), _p(dy1), _p(dy2), _p(dflow), _p(dx1), _p(dx2),
+        wp, wsz, _stream()), "grid_warp_bwd")
+
+
+# ---- pooling / interpolation / softmax / losses ------------------------------------------
+@_op("maxpool2d_fwd(Tensor x, Tensor(a!) y, Tensor(b!) argmax, int k, int s, int p) -> ()")
+def _maxpool2d_fwd(x, y, argmax, k, s, p):
+    n, h, w, c = x.shape
+    oh, ow = y.shape[1], y.shape[2]
+    check(_lib.lib().adaptseg_maxpool2d_fwd(n, c, h, w, oh, ow, k, s, p, _p(x), _p(y), _p(argmax), _stream()),
+          "maxpool2d_fwd")
+
+
+@_op("maxpool2d_bwd(Tensor dy, Tensor argmax, Tensor(a!) dx, int k, int s, int p) -> ()")
+def _maxpool2d_bwd(dy, argmax, dx, k, s, p):
+    n, oh, ow, c = dy.shape
+    h, w = dx.shape[1], dx.shape[2]
+    check(_lib.lib().adaptseg_maxpool2d_bwd(n, c, h, w, oh, ow, k, s, p, _p(dy), _p(argmax), _p(dx), _stream()),
+          "maxpool2d_bwd")
+
+
+@_op("upsample_bilinear_fwd(Tensor x, Tensor(a!) y) -> ()")
+def _upsample_bilinear_fwd(x, y):
+    n, h, w, c = x.shape
+    check(_lib.lib().adaptseg_upsample_bilinear_fwd(n, c, h, w, y.shape[1], y.shape[2], _p(x), _p(y), _stream()),
+          "upsample_bilinear_fwd")
+
+
+@_op("upsample_bilinear_bwd(Tensor dy, Tensor(a!) dx, bool accumulate) -> ()")
+def _upsample_bilinear_bwd(dy, dx, accumulate):
+    n, oh, ow, c = dy.shape
+    h, w = dx.shape[1], dx.shape[2]
+    wp, wsz = _ws_args(n * oh * w * c * 4, dy.device)
+    check(_lib.lib().adaptseg_upsample_bilinear_bwd(n, c, h, w, oh, ow, _p(dy), _p(dx),
+                                                    _lib.EPI_ACCUMULATE if accumulate else 0, wp, wsz,
+                                                    _stream()), "upsample_bilinear_bwd")
+
+
+@_op("softmax_fwd(Tensor x, Tensor(a!) y) -> ()")
+def _softmax_fwd(x, y):
+    rows, c = _rc(x)
+    check(_lib.lib().adaptseg_softmax_fwd(rows, c, _p(x), _p(y), _stream()), "softmax_fwd")
+
+
+@_op("softmax_bwd(Tensor y, Tensor dy, Tensor(a!) dx, bool accumulate) -> ()")
+def _softmax_bwd(y, dy, dx, accumulate):
+    rows, c = _rc(y)
+    check(_lib.lib().adaptseg_softmax_bwd(rows, c, _p(y), _p(dy), _p(dx),
+                                          _lib.EPI_ACCUMULATE if accumulate else 0, _stream()), "softmax_bwd")
+
+
+@_op("softmax_ce_fwd(Tensor logits, Tensor labels, int ignore, Tensor? weight, Tensor(a!) out) -> ()")
+def _softmax_ce_fwd(logits, labels, ignore, weight, out):
+    rows, c = _rc(logits)
+    b = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_ce_workspace_size(rows, ctypes.byref(b)), "ce_workspace_size")
+    wp, wsz = _ws_args(b.value, logits.device)
+    check(_lib.lib().adaptseg_softmax_ce_fwd(rows, c, _p(logits), _p(labels), int(ignore), _p(weight), _p(out),
+                                             wp, wsz, _stream()), "softmax_ce_fwd")
+
+
+@_op("softmax_ce_bwd(Tensor logits, Tensor labels, Tensor out, Tensor grad_loss, int ignore, Tensor? weight, "
+     "Tensor(a!) dlogits, bool accumulate) -> ()")
+def _softmax_ce_bwd(logits, labels, out, grad_loss, ignore, weight, dlogits, accumulate):
+    rows, c = _rc(logits)
+    check(_lib.lib().adaptseg_softmax_ce_bwd(rows, c, _p(logits), _p(labels), int(ignore), _p(weight), _p(out),
+                                             _p(grad_loss), _p(dlogits),
+                                             _lib.EPI_ACCUMULATE if accumulate else 0, _stream()),
+          "softmax_ce_bwd")
+
+
+@_op("adv_loss_fwd(Tensor x, float target, int kind, Tensor(a!) loss) -> ()")
+def _adv_loss_fwd(x, target, kind, loss):
+    n = x.numel()
+    b = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_adv_workspace_size(n, ctypes.byref(b)), "adv_workspace_size")
+    wp, wsz = _ws_args(b.value, x.device)
+    check(_lib.lib().adaptseg_adv_loss_fwd(n, _p(x), float(target), int(kind), _p(loss), wp, wsz, _stream()),
+          "adv_loss_fwd")
+
+
+@_op("adv_loss_bwd(Tensor x, float target, int kind, Tensor grad_loss, Tensor(a!) dx, bool accumulate) -> ()")
+def _adv_loss_bwd(x, target, kind, grad_loss, dx, accumulate):
+    check(_lib.lib().adaptseg_adv_loss_bwd(x.numel(), _p(x), float(target), int(kind), _p(grad_loss), _p(dx),
+                                           _lib.EPI_ACCUMULATE if accumulate else 0, _stream()), "adv_loss_bwd")
+
+
+# ---- optimisers and plumbing ----------------------------------------------------------------
+@_op("sgd_step(Tensor(a!) param, Tensor grad, Tensor(b!) momentum_buffer, float lr, float momentum, "
+     "float weight_decay, float grad_scale, int multiplicity, bool first_step) -> ()")
+def _sgd_step(param, grad, momentum_buffer, lr, momentum, weight_decay, grad_scale, multiplicity, first_step):
+    check(_lib.lib().adaptseg_sgd_step(param.numel(), _p(param), _p(grad), _p(momentum_buffer), float(lr),
+                                       float(momentum), float(weight_decay), float(grad_scale), int(multiplicity),
+                                       1 if first_step else 0, _stream()), "sgd_step")
+
+
+@_op("adam_step(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, float lr, "
+     "float beta1, float beta2, float eps, int step, float grad_scale) -> ()")
+def _adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, step, grad_scale):
+    check(_lib.lib().adaptseg_adam_step(param.numel(), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq),
+                                        float(lr), float(beta1), float(beta2), float(eps), int(step),
+                                        float(grad_scale), _stream()), "adam_step")
+
+
+@_op("zero(Tensor(a!) t) -> ()")
+def _zero(t):
+    check(_lib.lib().adaptseg_zero(_p(t), t.numel() * t.element_size(), _stream()), "zero")
+
+
+@_op("to_nhwc(Tensor x, Tensor(a!) out) -> ()")
+def _to_nhwc(x, out):
+    n, c, h, w = x.shape
+    st = (ctypes.c_int64 * 4)(*x.stride())
+    check(_lib.lib().adaptseg_to_nhwc(n, c, h, w, st, _p(x), _p(out), _stream()), "to_nhwc")
+
+
+@_op("axpy(float alpha, Tensor src, Tensor(a!) dst, bool accumulate) -> ()")
+def _axpy(alpha, src, dst, accumulate):
+    check(_lib.lib().adaptseg_axpy(src.numel(), float(alpha), _p(src), _p(dst),
+                                   _lib.EPI_ACCUMULATE if accumulate else 0, _stream()), "axpy")
+
+
+@_op("add_i64(Tensor(a!) t, int v) -> ()")
+def _add_i64(t, v):
+    check(_lib.lib().adaptseg_add_i64(_p(t), t.numel(), int(v), _stream()), "add_i64")
+
+
+# ---- input pipeline and evaluation -----------------------------------------------
+@_op("gta5_preprocess(Tensor images, float[] mean, Tensor(a!) out, Tensor? labels, Tensor? lut, "
+     "Tensor(b!)? labels_out) -> ()")
+def _gta5_preprocess(images, mean, out, labels, lut, labels_out):
+    n, h, w, _ = images.shape
+    oh, ow = out.shape[2], out.shape[3]
+    b = ctypes.c_size_t(0)
+    check(_lib.lib().adaptseg_preprocess_workspace_size(n, h, w, oh, ow, ctypes.byref(b)),
+          "preprocess_workspace_size")
+    wp, wsz = _ws_args(b.value, images.device)
+    check(_lib.lib().adaptseg_gta5_preprocess(
+        n, h, w, oh, ow, _p(images), float(mean[0]), float(mean[1]), float(mean[2]), _p(out), _p(labels),
+        _p(lut) if labels is not None else None, _p(labels_out), wp, wsz, _stream()), "gta5_preprocess")
+
+
+@_op("upsample_argmax(Tensor x, Tensor(a!) out) -> ()")
+def _upsample_argmax(x, out):
+    n, h, w, c = x.shape
+    check(_lib.lib().adaptseg_upsample_argmax(n, c, h, w, out.shape[1], out.shape[2], _p(x), _p(out), _stream()),
+          "upsample_argmax")
+
+
+@_op("confusion_hist(Tensor gt_ids, Tensor lut, Tensor pred, int num_classes, Tensor(a!) hist) -> ()")
+def _confusion_hist(gt_ids, lut, pred, num_classes, hist):
+    check(_lib.lib().adaptseg_confusion_hist(gt_ids.numel(), _p(gt_ids), _p(lut), _p(pred), int(num_classes),
+                                             _p(hist), _stream()), "confusion_hist")
+
+
+class _Overloads:
+    """torch.ops.adaptseg.<name>.default for every op (skips the packet's overload lookup)."""
+
+
+OPS = _Overloads()
+for _n in NAMES:
+    setattr(OPS, _n, getattr(torch.ops.adaptseg, _n).default)

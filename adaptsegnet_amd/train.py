@@ -31,13 +31,11 @@ per-replica DataParallel semantics.
 from __future__ import annotations
 
 import contextlib
-import os
 from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
 
-from . import engine
 from . import functional as F
 from .optim import SGD, Adam, lr_poly
 
@@ -214,15 +212,14 @@ class AdaptSegTrainer:
         optimisers) runs on a HIP stream of priority ``cfg.main_priority`` (-1, high, for
         DeeplabMulti), so the hardware scheduler favours it over the weight-gradient side stream
         that fills the gaps the HBM-bound BN passes leave: +0.9 % c2, +0.2 % c3, ±0 c5, but
-        -1.7 % for DeeplabVGG (c4: no BN, so it runs on the caller's stream; tools/ab_prio*.sh).
-        The caller's stream waits for it at the end.  ``main_priority=None`` or
-        ``ADAPTSEG_EXP_HIPRIO=0`` runs on the caller's stream."""
+        -1.7 % for DeeplabVGG (c4: no BN, so it runs on the caller's stream).  The caller's
+        stream waits for it at the end.  ``main_priority=None`` runs on the caller's stream."""
         prio = self.cfg.main_priority
         if prio == "auto":   # VGG has no BN passes for the side stream to fill: -1.7 % with it
             prio = None if getattr(self.model, "single_output", False) else -1
         dev = next(self.model.parameters()).device
-        if prio is None or os.environ.get("ADAPTSEG_EXP_HIPRIO") == "0" or dev.type != "cuda":
-            return self._step(i_iter, batches)
+        if prio is None or dev.type != "cuda":
+            return self._step_body(i_iter, batches)
         batches = list(batches)
         key = (dev.index, prio)
         hp = AdaptSegTrainer._hp_streams.get(key)
@@ -231,15 +228,9 @@ class AdaptSegTrainer:
         cur = torch.cuda.current_stream(dev)
         hp.wait_stream(cur)
         with torch.cuda.stream(hp):
-            L = self._step(i_iter, batches)
+            L = self._step_body(i_iter, batches)
         cur.wait_stream(hp)
         return L
-
-    def _step(self, i_iter, batches):
-        if os.environ.get("ADAPTSEG_EXP_DEFERJOIN") == "1":
-            with engine.deferred_wgrad_join():
-                return self._step_body(i_iter, batches)
-        return self._step_body(i_iter, batches)
 
     def _step_body(self, i_iter, batches):
         """batches: iterable of ``iter_size`` tuples (images, labels, images_target).
@@ -260,8 +251,7 @@ class AdaptSegTrainer:
         batches = list(batches)
         self._pending = []
         for idx, batch in enumerate(batches):
-            g_done = (lambda: (engine.join_deferred(), self._start_sync((self.model,)))) \
-                if idx == len(batches) - 1 else None
+            g_done = (lambda: self._start_sync((self.model,))) if idx == len(batches) - 1 else None
             if c.level == "source-only":
                 self._sub_source_only(batch[0], batch[1], inv, L, g_done)
                 continue
@@ -270,7 +260,6 @@ class AdaptSegTrainer:
                 self._sub_single(images, labels, images_t, inv, tsize, L, g_done)
             else:
                 self._sub_multi(images, labels, images_t, inv, tsize, L, g_done)
-        engine.join_deferred()   # weight gradients complete before the collectives / optimisers
         if not batches:
             self._start_sync((self.model,))
         self._start_sync((self.D1, self.D2))

@@ -4,7 +4,8 @@ Reference semantics (utils/loss.py:14-36): pixels with target < 0 or target ==
 ignore_label are dropped, the rest are averaged (``size_average=True``) or weighted by
 ``weight[target]``; shape asserts as in the reference.  The reference's ``:31-32`` zero
 branch is unreachable (it tests ``target.data.dim()`` after masking, which is always 1), so
-an all-ignored batch gives NaN there and here.  ``size_average=False`` returns the sum.
+an all-ignored batch gives NaN there and here.  ``size_average=False`` returns the sum
+(``F.cross_entropy(..., size_average=False)``, reference :35; 0 for an all-ignored batch).
 """
 from __future__ import annotations
 
@@ -27,7 +28,5 @@ class CrossEntropy2d(nn.Module):
         assert predict.size(0) == target.size(0), "{0} vs {1} ".format(predict.size(0), target.size(0))
         assert predict.size(2) == target.size(1), "{0} vs {1} ".format(predict.size(2), target.size(1))
         assert predict.size(3) == target.size(2), "{0} vs {1} ".format(predict.size(3), target.size(2))
-        loss = cross_entropy2d(predict, target.long(), self.ignore_label, weight)
-        if not self.size_average:
-            raise NotImplementedError("size_average=False (sum) is not on the adversarial hot path")
-        return loss
+        return cross_entropy2d(predict, target.long(), self.ignore_label, weight,
+                               reduction="mean" if self.size_average else "sum")

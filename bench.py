@@ -48,15 +48,19 @@ CONFIGS = {
 }
 
 
-def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize):
-    """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector."""
+def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None):
+    """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector.  ``products``
+    (a set), when given, also collects every (op, selector, split-K?) the step launches
+    (host-side planning only: tests/test_conv_coverage.py runs it without a GPU)."""
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd import engine
     inv = {}
 
     def add(geom, n, h, w, op, strides=None, count=1):
-        kid, _ = K.conv_kernel_id(geom, n, h, w, op, strides)
+        kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides)
         inv[kid] = inv.get(kid, 0.0) + count * geom.flops(n, h, w)
+        if products is not None:
+            products.add((op, kid, sp > 1))
 
     def vgg_pass(wh):
         w, h = wh

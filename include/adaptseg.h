@@ -101,6 +101,10 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
    over y is skipped otherwise (model/deeplab_multi.py:83-103: every Bottleneck conv feeds a
    BatchNorm). */
 int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes);
+/* The row-tile count adaptseg_conv2d_fwd_bnstats will produce for `d` (0: no fused
+   statistics for this geometry), assuming 16-byte aligned operands: lets a caller size and
+   plan the BatchNorm that follows before launching (host-side, no GPU). */
+int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles);
 int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                                 float *y, float *stats, size_t stats_bytes, int *ntiles, void *ws,
                                 size_t ws_bytes, adaptseg_stream_t stream);
@@ -109,20 +113,6 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream);
-
-/* Data gradient dx of a conv whose input is the output of a train-mode BatchNorm+ReLU
-   (model/deeplab_multi.py:65-98, bn1/bn2 of every Bottleneck), plus the BN backward's
-   reduction straight from the accumulators: per row tile, sum g and sum g*(bn_x - mean) with
-   g = dx * [(bn_x-mean)*invstd*weight + bias > 0], into partial = [2][c][ntiles] for
-   adaptseg_bn_bwd_tiles.  *ntiles = 0 when the chosen kernel cannot fuse them (split-K,
-   stride-2 parity path, unaligned operands, tap-GEMM path): dx is still computed and the caller
-   runs adaptseg_bn_bwd.  No epilogue flags. */
-int adaptseg_conv2d_bnsums_size(const adaptseg_conv_desc *d, size_t *bytes);
-int adaptseg_conv2d_bwd_data_bnsums(const adaptseg_conv_desc *d, const float *dy, const float *const *w, float *dx,
-                                    const float *bn_x, const float *bn_mean, const float *bn_invstd,
-                                    const float *bn_weight, const float *bn_bias, float *partial,
-                                    size_t partial_bytes, int *ntiles, void *ws, size_t ws_bytes,
-                                    adaptseg_stream_t stream);
 
 /* dw[seg][k,kh,kw,c] (+)= sum_{n,oh,ow} dy * x_gathered; db[seg][k] (+)= sum dy.
    db may be NULL.  Only ADAPTSEG_EPI_ACCUMULATE is honoured. */
@@ -179,14 +169,6 @@ int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y,
                            const float *weight, const float *bias, const float *save_mean,
                            const float *save_invstd, float *dx, float *dres, int act, float *dweight,
                            float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
-
-/* adaptseg_bn_bwd (train mode, ReLU mask recomputed from x) from the row-tile sums of
-   adaptseg_conv2d_bwd_data_bnsums: a deterministic fp64 finalize into coef [2][c] (caller-
-   owned, 2*c floats), then the same apply pass.  dx may alias dy. */
-int adaptseg_bn_bwd_tiles(int64_t rows, int c, const float *partial, int ntiles, const float *dy,
-                          const float *x, const float *weight, const float *bias, const float *save_mean,
-                          const float *save_invstd, float *coef, float *dx, float *dres,
-                          adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Evaluation: evaluate_cityscapes.py:153-169 (interp to 1024x2048 + argmax) and          */

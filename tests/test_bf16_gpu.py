@@ -8,6 +8,9 @@ path).  Against the UNROUNDED fp64 conv the error is the bf16 input rounding its
 (~2^-9 relative per operand), checked loosely (<= 2e-2) to show the result is a conv at all.
 """
 
+import os
+import sys
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -16,19 +19,8 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 
-# (n, cin, h, w, cout, k, stride, pads, dils, bias) — shapes the bf16 kernel covers
-BF16_CASES = [
-    (2, 64, 17, 23, 256, 1, 1, (0,), (1,), False),       # 1x1, M and N tails
-    (2, 256, 17, 23, 128, 1, 2, (0,), (1,), False),      # stride-2 1x1 (dgrad parity classes)
-    (2, 64, 15, 21, 64, 3, 1, (1,), (1,), False),        # 3x3, N = 64 < tile
-    (2, 128, 13, 11, 128, 3, 1, (2,), (2,), False),      # atrous d2
-    (1, 256, 9, 12, 256, 3, 1, (4,), (4,), False),       # atrous d4
-    (2, 64, 16, 20, 128, 4, 2, (1,), (1,), True),        # D conv2 (4x4/2, bias)
-    (2, 128, 7, 9, 64, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP segments
-    (1, 2048, 3, 5, 64, 1, 1, (0,), (1,), False),        # split-K (M = 15, K = 2048)
-    (2, 64, 31, 33, 192, 3, 2, (1,), (1,), False),       # stride-2 3x3, odd sizes
-    (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),         # wgrad, many K splits
-]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_cases import BF16_CASES  # noqa: E402  (n, cin, h, w, cout, k, stride, pads, dils, bias)
 
 
 def K():

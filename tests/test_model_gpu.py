@@ -18,6 +18,9 @@ from oracle import reference_torch as R
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+# the three adversarial objectives of BASELINE's configs: c2 (single-level BCE), c3
+# (multi-level BCE on two discriminators), c5 (multi-level LS-GAN)
+LEVEL_GAN = [("single-level", "Vanilla"), ("multi-level", "Vanilla"), ("multi-level", "LS")]
 
 
 def _sd_torch(sd):
@@ -174,7 +177,7 @@ def _run_hip(level, gan, cfg, data, iters, bn_train):
     return m, d1, d2, got
 
 
-@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+@pytest.mark.parametrize("level,gan", LEVEL_GAN)
 def test_adversarial_step_eval_bn(data, level, gan):
     """Six full iterations with eval-mode BN (well conditioned): every loss of every iteration
     within 1e-4 rel of the fp64 oracle; generator/discriminator parameter updates within 2x
@@ -208,7 +211,7 @@ def test_adversarial_step_eval_bn(data, level, gan):
         assert f <= 2 * f32 + 1e-3, (dname, f, f32)
 
 
-@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+@pytest.mark.parametrize("level,gan", LEVEL_GAN)
 def test_adversarial_step_train_bn(data, level, gan):
     """Two iterations with train-mode BN (the training semantics).  Iteration-0 losses are
     tight (1e-3 rel).  After one update the trajectory is chaotic at random init (SURVEY.md
@@ -240,7 +243,7 @@ def test_adversarial_step_train_bn(data, level, gan):
                            torch.from_numpy(g0["layer5.conv2d_list.0.weight"]).float())
 
 
-@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+@pytest.mark.parametrize("level,gan", LEVEL_GAN)
 def test_domain_overlap_is_bit_identical(data, level, gan):
     """StepConfig.overlap_domains (target-domain pass on a second stream, overlapping the
     source backward) must not change a single bit of the losses or parameters."""
@@ -266,7 +269,7 @@ def test_domain_overlap_is_bit_identical(data, level, gan):
         assert torch.equal(d0[k], d1_[k]), k
 
 
-@pytest.mark.parametrize("level,gan", [("single-level", "Vanilla"), ("multi-level", "LS")])
+@pytest.mark.parametrize("level,gan", LEVEL_GAN)
 def test_iter_size_two_accumulates_sub_batches(data, level, gan):
     """iter_size = 2 (train:569-683 sub-iteration loop): two sub-batches per step, each loss
     scaled by 1/iter_size, gradients accumulated before one optimiser step.  Eval-mode BN, 2

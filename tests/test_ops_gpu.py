@@ -5,6 +5,9 @@ chain), the oracle in fp64.  Convolutions: max|err| <= 2e-5 * max|ref| (K up to 
 pointwise / reductions: <= 1e-5 relative; integer-exact where the op is a selection
 (max-pool argmax routing).
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -38,34 +41,8 @@ def w_cl(w):  # [co,ci,kh,kw] cpu -> device [co,kh,kw,ci] contiguous
     return w.permute(0, 2, 3, 1).contiguous().float().to(DEV)
 
 
-CONV_CASES = [
-    # (n, cin, h, w, cout, k, stride, pads, dils, bias)
-    (2, 64, 17, 23, 256, 1, 1, (0,), (1,), False),        # bottleneck conv1/conv3 (1x1)
-    (2, 256, 17, 23, 128, 1, 2, (0,), (1,), False),       # layer2 stride-2 1x1
-    (2, 64, 15, 21, 64, 3, 1, (1,), (1,), False),         # layer1 3x3
-    (2, 128, 13, 11, 128, 3, 1, (2,), (2,), False),       # layer3 atrous d2
-    (1, 256, 9, 12, 256, 3, 1, (4,), (4,), False),        # layer4 atrous d4
-    (2, 3, 37, 45, 64, 7, 2, (3,), (1,), False),          # stem 7x7/2
-    (2, 19, 32, 40, 64, 4, 2, (1,), (1,), True),          # D conv1 (Cin 19)
-    (2, 64, 16, 20, 128, 4, 2, (1,), (1,), True),         # D conv2
-    (2, 128, 6, 8, 1, 4, 2, (1,), (1,), True),            # D classifier (Cout 1)
-    (2, 64, 7, 9, 19, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP, dil > spatial
-    (1, 2048, 3, 5, 7, 1, 1, (0,), (1,), False),          # split-K path (M=15, K=2048)
-    (2, 32, 15, 17, 64, 3, 2, (1,), (1,), False),         # stride-2 3x3, odd sizes (parity classes)
-    (1, 64, 9, 11, 32, 4, 2, (1,), (1,), True),           # stride-2 4x4, odd sizes
-    (3, 64, 20, 24, 64, 3, 1, (1,), (1,), False),         # N = 64 tile (256x64)
-    (2, 96, 12, 10, 96, 1, 2, (0,), (1,), False),         # 1x1 stride 2, empty parity classes
-    (2, 64, 40, 48, 64, 1, 1, (0,), (1,), True),          # wgrad 64x64 tile, bias Cout 64
-    (2, 64, 30, 34, 256, 1, 1, (0,), (1,), False),        # wgrad 256x64 tile (M'=256, N'=64)
-    (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),          # wgrad ~192 K-splits (16-group reduce)
-    (1, 32, 8, 10, 320, 1, 1, (0,), (1,), True),          # bias grad with Cout > 256
-    (2, 64, 16, 24, 2, 3, 1, (1,), (1,), True),           # thin: the warper's output conv (Cout 2)
-    (2, 32, 10, 14, 3, 3, 1, (2,), (2,), False),          # thin: Cout 3, dilated
-    (1, 16, 9, 7, 4, 1, 1, (0,), (1,), True),             # thin: Cout 4, 1x1
-    (2, 256, 17, 23, 64, 1, 1, (0,), (1,), False),        # 1x1 dgrad on the occupancy-3 BK16 tile, ragged M
-    (2, 100, 13, 9, 48, 1, 1, (0,), (1,), False),         # ... ragged N (Cin 100), K = 48 (BK16 but not BK32)
-    (1, 1024, 3, 5, 256, 1, 1, (0,), (1,), False),        # ... split-K (M = 15: one row tile)
-]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_cases import CONV_CASES, LARGE_CASES  # noqa: E402
 
 
 def test_thin_conv_selection_and_epilogues():
@@ -430,38 +407,183 @@ def test_to_nhwc_and_axpy():
     assert torch.allclose(c, b + 0.5 * a)
 
 
-@pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1, 1), (4, 64, 128, 136, 256, 3, 2),
-                                   (4, 128, 96, 88, 128, 3, 1), (1, 64, 5, 7, 256, 1, 1),
-                                   (2, 128, 20, 18, 48, 1, 1)])
-@pytest.mark.parametrize("math", ["f32", "bf16"])
-def test_conv_dgrad_fused_bn_backward_sums(shape, math):
-    """conv_dgrad_bnsums + bn_bwd_tiles (BN backward reduction fused into the data-gradient
-    epilogue) == conv_dgrad + bn_bwd with the ReLU mask recomputed from x; the last shape is
-    split along K on the fp32 path, which cannot fuse and must report ntiles = 0.  Tolerance 1e-5 rel (the
-    fused path sums the same terms in row-tile order)."""
+@pytest.mark.parametrize("case", LARGE_CASES, ids=[f"L{i}" for i in range(len(LARGE_CASES))])
+def test_conv_large_grid_epilogues(case):
+    """Grids of >= 257 output tiles (the c2 / c3 / c5 layer sizes): forward and data gradient
+    store from the in-kernel epilogue (no K split), so every epilogue flag the engine uses is
+    checked there against fp64 torch:
+      fwd   plain, EPI_RELU + EPI_RESIDUAL, EPI_ACCUMULATE, EPI_LEAKY (D convs, bias)
+      dgrad plain, EPI_RESIDUAL with out == res (identity shortcut, engine.block_backward),
+            EPI_ACCUMULATE (downsample + conv1, ASPP layer5 + layer6), aux RELU_GRAD (VGG),
+            aux LEAKY_GRAD (D)
+      wgrad accumulate (the gradient arena)."""
     k = K()
-    n, cin, h, w, cout, ks, dil = shape
-    k.set_conv_math(k.MATH_BF16 if math == "bf16" else k.MATH_F32)
-    try:
-        g = torch.Generator().manual_seed(17)
-        geom = k.ConvGeom(cin, cout, ks, ks, 1, ((ks // 2) * dil,), (dil,))
-        dy = nhwc(torch.randn(n, cout, h, w, generator=g, dtype=torch.float64))
-        wt = w_cl(torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.05)
-        bx = nhwc(torch.randn(n, cin, h, w, generator=g, dtype=torch.float64) * 2 + 0.3)
-        bw = (torch.rand(cin, generator=g) + 0.5).float().to(DEV)
-        bb = (torch.randn(cin, generator=g) * 0.2).float().to(DEV)
-        rm = torch.zeros(cin, device=DEV)
-        rv = torch.ones(cin, device=DEV)
-        _, mean, invstd = k.bn_fwd_train(bx, bw, bb, rm, rv, 0.1, 1e-5, relu=True)
-        dx_ref = k.conv_dgrad(geom, dy, n, h, w, [wt])
-        ref = k.bn_bwd(dx_ref.clone(), None, bx, bw, mean, invstd, relu=True, bias=bb)
-        dx, sums = k.conv_dgrad_bnsums(geom, dy, n, h, w, [wt], bx, mean, invstd, bw, bb)
-        assert rel(dx, dx_ref) == 0.0
-        if shape[0] == 1 and math == "f32":
-            assert sums is None  # K split across blocks: no per-tile sums
-            return
-        assert sums is not None
-        got = k.bn_bwd_tiles(dx, bx, bw, bb, mean, invstd, sums, dx=dx)
-        assert rel(got, ref) < 1e-5
-    finally:
-        k.set_conv_math(k.MATH_F32)
+    n, cin, h, w, cout, ks, stride, pads, dils, bias = case
+    geom = k.ConvGeom(cin, cout, ks, ks, stride, pads, dils)
+    for op in (0, 1):
+        sel, sp = k.conv_kernel_id(geom, n, h, w, op)
+        assert sp == 1, (op, sel, sp)   # the unsplit large-grid path is what this test is for
+    g = torch.Generator().manual_seed(4242 + LARGE_CASES.index(case))
+    nseg = len(pads)
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    ws = [torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * (1.0 / (cin * ks * ks) ** 0.5)
+          for _ in range(nseg)]
+    bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in range(nseg)] if bias else None
+    xr = x.clone().requires_grad_(True)
+    wr = [t.clone().requires_grad_(True) for t in ws]
+    ref = _ref_conv(xr, wr, bs, stride, pads, dils)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gy)
+    ref = ref.detach()
+    xd, gyd = nhwc(x), nhwc(gy)
+    wd = [w_cl(t) for t in ws]
+    bd = [t.float().to(DEV) for t in bs] if bias else None
+
+    # forward
+    assert rel(nchw(k.conv_fwd(geom, xd, n, h, w, wd, bd)), ref) < 2e-5
+    xc = x.float().to(DEV).contiguous()
+    assert rel(nchw(k.conv_fwd(geom, xc, n, h, w, wd, bd, strides=tuple(xc.stride()))), ref) < 2e-5
+    res = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    y = k.conv_fwd(geom, xd, n, h, w, wd, bd, res=nhwc(res), flags=k.EPI_RELU)
+    assert rel(nchw(y), F.relu(ref + res)) < 2e-5
+    y = nhwc(res)
+    k.conv_fwd(geom, xd, n, h, w, wd, bd, out=y, flags=k.EPI_ACCUMULATE)
+    assert rel(nchw(y), ref + res) < 2e-5
+    y = k.conv_fwd(geom, xd, n, h, w, wd, bd, flags=k.EPI_LEAKY)
+    assert rel(nchw(y), F.leaky_relu(ref, 0.2)) < 2e-5
+    if nseg == 1 and not bias:   # forward with fused BN statistics (every Bottleneck conv)
+        y, tiles = k.conv_fwd_bnstats(geom, xd, n, h, w, wd)
+        assert tiles is not None and rel(nchw(y), ref) < 2e-5
+
+    # data gradient
+    dref = xr.grad
+    assert rel(nchw(k.conv_dgrad(geom, gyd, n, h, w, wd)), dref) < 2e-5
+    prev = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    out = nhwc(prev)
+    k.conv_dgrad(geom, gyd, n, h, w, wd, out=out, res=out)
+    assert rel(nchw(out), dref + prev) < 2e-5
+    out = nhwc(prev)
+    k.conv_dgrad(geom, gyd, n, h, w, wd, out=out, flags=k.EPI_ACCUMULATE)
+    assert rel(nchw(out), dref + prev) < 2e-5
+    dx = k.conv_dgrad(geom, gyd, n, h, w, wd, aux=nhwc(prev), flags=k.EPI_RELU_GRAD)
+    assert rel(nchw(dx), dref * (prev > 0)) < 2e-5
+    dx = k.conv_dgrad(geom, gyd, n, h, w, wd, aux=nhwc(prev))
+    assert rel(nchw(dx), torch.where(prev > 0, dref, 0.2 * dref)) < 2e-5
+
+    # weight gradient, accumulated into a non-zero arena slot
+    dws = [torch.ones_like(t) for t in wd]
+    k.conv_wgrad(geom, gyd, xd, n, h, w, dws, accumulate=True)
+    for i in range(nseg):
+        assert rel(dws[i].permute(0, 3, 1, 2).cpu() - 1.0, wr[i].grad) < 2e-5
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1), (2, 256, 96, 96, 256, 3), (2, 128, 20, 18, 48, 1)])
+def test_conv_dgrad_into_bn_relu_backward(shape):
+    """The Bottleneck backward chain conv2 / conv3 data gradient -> train-mode BN+ReLU backward
+    with the ReLU mask recomputed from the BN input (engine.block_backward), in place, vs
+    fp64 torch autograd of conv(relu(bn(x))).  The first two shapes are unsplit large grids
+    (in-kernel epilogue), the last is split along K."""
+    k = K()
+    n, cin, h, w, cout, ks = shape
+    g = torch.Generator().manual_seed(17)
+    pad = ks // 2 * (2 if ks == 3 else 1)
+    geom = k.ConvGeom(cin, cout, ks, ks, 1, (pad,), (2 if ks == 3 else 1,))
+    bx = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64) * 2 + 0.3
+    bw = torch.rand(cin, generator=g, dtype=torch.float64) + 0.5
+    bb = torch.randn(cin, generator=g, dtype=torch.float64) * 0.2
+    wt = torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.05
+    xr = bx.clone().requires_grad_(True)
+    a = F.relu(F.batch_norm(xr, None, None, bw, bb, True, 0.1, 1e-5))
+    y = F.conv2d(a, wt, None, 1, geom.pads[0], geom.dils[0])
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    bxd = nhwc(bx)
+    bwd, bbd = bw.float().to(DEV), bb.float().to(DEV)
+    _, mean, invstd = k.bn_fwd_train(bxd, bwd, bbd, torch.zeros(cin, device=DEV), torch.ones(cin, device=DEV),
+                                     0.1, 1e-5, relu=True)
+    dx = k.conv_dgrad(geom, nhwc(dy), n, h, w, [w_cl(wt)])
+    k.bn_bwd(dx, None, bxd, bwd, mean, invstd, relu=True, dx=dx, bias=bbd)
+    assert rel(nchw(dx), xr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("size_average", [True, False])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_crossentropy2d_module(size_average, weighted):
+    """utils/loss.py CrossEntropy2d drop-in: mean (size_average=True) and sum reductions, with
+    and without class weights, value and logits gradient vs F.cross_entropy in fp64 on the
+    kept pixels (target >= 0 and != 255, reference utils/loss.py:29-35)."""
+    from adaptsegnet_amd.utils.loss import CrossEntropy2d
+    g = torch.Generator().manual_seed(31)
+    n, c, h, w = 2, 19, 21, 27
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64) * 2
+    lab = torch.randint(0, c, (n, h, w), generator=g)
+    lab[torch.rand(n, h, w, generator=g) < 0.1] = 255
+    lab[0, 0, :3] = -1
+    cw = torch.rand(c, generator=g, dtype=torch.float64) + 0.5 if weighted else None
+    xr = x.clone().requires_grad_(True)
+    keep = (lab >= 0) & (lab != 255)
+    ref = F.cross_entropy(xr.permute(0, 2, 3, 1)[keep], lab[keep], weight=cw,
+                          reduction="mean" if size_average else "sum")
+    ref.backward(torch.tensor(0.7, dtype=torch.float64))
+    xd = x.float().to(DEV).requires_grad_(True)
+    loss = CrossEntropy2d(size_average=size_average)(xd, lab.to(DEV),
+                                                     None if cw is None else cw.float().to(DEV))
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    loss.backward(torch.tensor(0.7, device=DEV))
+    assert rel(xd.grad, xr.grad) < 1e-5
+    if not size_average:   # an all-ignored batch sums to 0 (F.cross_entropy on no pixels)
+        empty = CrossEntropy2d(size_average=False)(xd.detach(), torch.full_like(lab, 255).to(DEV))
+        assert empty.item() == 0.0
+
+
+def test_custom_ops_opcheck():
+    """torch.library.opcheck (schema mutation annotations, fake kernels, autograd registration,
+    AOT dispatch) on small cases of the hot-path ops of torch.ops.adaptseg."""
+    g = torch.Generator().manual_seed(3)
+    r = lambda *s: torch.randn(*s, generator=g).to(DEV)  # noqa: E731
+    n, h, w, cin, cout = 2, 9, 11, 16, 32
+    x = r(n, h, w, cin)
+    wt = r(cout, cin, 3, 3).contiguous(memory_format=torch.channels_last)
+    y = torch.empty(n, h, w, cout, device=DEV)
+    ops = torch.ops.adaptseg
+    cases = [
+        (ops.conv2d_fwd.default, (x, [wt], [None], None, y, [n, cin, h, w], [h * w * cin, 1, w * cin, cin],
+                                  [cout, cin, 3, 3], 1, [1], [1], 0)),
+        (ops.conv2d_bwd_data.default, (r(n, h, w, cout), [wt], None, None, torch.empty_like(x), [n, cin, h, w],
+                                       [cout, cin, 3, 3], 1, [1], [1], 0)),
+        (ops.conv2d_bwd_weight.default, (r(n, h, w, cout), x, [torch.zeros_like(wt)], [], [n, cin, h, w],
+                                         [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1, [1], [1], 2)),
+        (ops.bn_fwd_train.default, (r(n, h, w, cout), r(cout), r(cout), torch.zeros(cout, device=DEV),
+                                    torch.ones(cout, device=DEV), None, torch.empty(n, h, w, cout, device=DEV),
+                                    torch.empty(cout, device=DEV), torch.empty(cout, device=DEV), 0.1, 1e-5, 1)),
+        (ops.upsample_bilinear_fwd.default, (r(n, 4, 5, 19), torch.empty(n, 13, 17, 19, device=DEV))),
+        (ops.softmax_fwd.default, (r(n, h, w, 19), torch.empty(n, h, w, 19, device=DEV))),
+        (ops.softmax_ce_fwd.default, (r(n, h, w, 19), torch.randint(0, 19, (n, h, w), generator=g).to(DEV), 255,
+                                      None, torch.empty(2, device=DEV))),
+        (ops.adv_loss_fwd.default, (r(n, 1, 3, 4), 1.0, 0, torch.empty(1, device=DEV))),
+    ]
+    for op, args in cases:
+        res = torch.library.opcheck(op, args)
+        assert all(v == "SUCCESS" for v in res.values()), (op, res)
+
+
+def test_torch_ops_conv_and_ce_vs_oracle():
+    """The ops called through torch.ops.adaptseg directly (what the modules route through) vs
+    fp64 torch: an atrous 3x3 conv forward and the ignore-index cross entropy."""
+    g = torch.Generator().manual_seed(5)
+    n, cin, h, w, cout = 2, 64, 21, 27, 96
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    ref = F.conv2d(x, wt, None, 1, 2, 2)
+    y = torch.empty(n, h, w, cout, device=DEV)
+    torch.ops.adaptseg.conv2d_fwd(nhwc(x), [wt.float().to(DEV).contiguous(memory_format=torch.channels_last)], [],
+                                  None, y, [n, cin, h, w], [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1,
+                                  [2], [2], 0)
+    assert rel(nchw(y), ref) < 2e-5
+    logits = torch.randn(n, 19, h, w, generator=g, dtype=torch.float64) * 3
+    lab = torch.randint(0, 19, (n, h, w), generator=g)
+    lab[torch.rand(n, h, w, generator=g) < 0.1] = 255
+    out = torch.empty(2, device=DEV)
+    torch.ops.adaptseg.softmax_ce_fwd(nhwc(logits), lab.to(DEV), 255, None, out)
+    lref = F.cross_entropy(logits, lab, ignore_index=255)
+    assert abs(out[0].item() - lref.item()) < 1e-5 * lref.item()

@@ -129,3 +129,27 @@ def test_two_steps_match_reference(gold, inputs, level, gan):
     for k, t in D2.items():
         np.testing.assert_allclose(t.detach().norm().item(), float(gold[pre + "D2/norm/" + k]),
                                    rtol=1e-9, err_msg=k)
+
+
+def test_reference_trajectory_fixture_and_oracle_iteration0():
+    """tests/golden/trajectory_goldens.npz (gen_trajectory.py: the reference's own modules,
+    fp32, full 1024x512 geometry) pins the bench's climbing loss_seg2 as reference behaviour:
+    with train-mode BN it climbs from ~6 past 20 within 5 iterations on one fixed batch, with
+    eval-mode BN it stays near chance (ln 19 = 2.94).  The oracle's first full-size iteration
+    reproduces the reference's (same stock CPU ops, same thread count)."""
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "trajectory_goldens.npz"))
+    tr, ev = gold["c2_train/threads8"], gold["c2_eval/threads8"]
+    assert tr[0, 0] < 7 and tr[-1, 0] > 20          # loss_seg2 climbs (train-mode BN)
+    assert np.all(np.abs(ev[:, 0] - np.log(19)) < 0.3)
+    assert gold["c3_train/threads8"][-1, 1] > 20
+    torch.set_num_threads(8)
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
+    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
+    cfg = dict(level="single-level", gan="Vanilla", input_size=(1024, 512), input_size_target=(1024, 512))
+    opts = R.make_optimizers(G, None, D2, R.DEFAULT_CFG | cfg)
+    xs = torch.from_numpy(R.det_images((1, 3, 512, 1024), 11)).float()
+    lab = torch.from_numpy(R.det_labels((1, 512, 1024), 12))
+    xt = torch.from_numpy(R.det_images((1, 3, 512, 1024), 13)).float()
+    got = R.oracle_step(G, None, D2, opts, cfg, 0, [(xs, lab, xt)])
+    for j, k in enumerate(["loss_seg2", "loss_adv_target2", "loss_D2"]):
+        assert abs(got[k] - tr[0, j]) <= 1e-5 * abs(tr[0, j]), (k, got[k], tr[0, j])
