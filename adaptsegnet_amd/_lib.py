@@ -23,7 +23,7 @@ EPI_RESIDUAL = 8
 EPI_RELU = 16
 EPI_RELU_GRAD = 32
 CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT = 0, 1, 2
-MATH_F32, MATH_BF16, MATH_BF16_WIDE = 0, 1, 2
+MATH_F32, MATH_BF16, MATH_BF16_WIDE, MATH_F32X3 = 0, 1, 2, 3
 
 
 class AdaptSegLibraryError(RuntimeError):

@@ -224,9 +224,10 @@ struct TimingState {
 };
 static TimingState g_timing;
 
-// Process-wide conv math (adaptseg_conv_set_math): 0 = fp32 MFMA, 1 = bf16 MFMA.  Global, not
-// thread-local: autograd runs backward on its own worker thread.
-static std::atomic<int> g_conv_math{0};
+// Process-wide conv math (adaptseg_conv_set_math), default F32X3 (fp32-accurate on the bf16
+// MFMA, conv_x3.hpp); F32 = the fp32-input MFMA kernels, BF16 = bf16 operands (config c5).
+// Global, not thread-local: autograd runs backward on its own worker thread.
+static std::atomic<int> g_conv_math{ADAPTSEG_MATH_F32X3};
 int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 
 void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
@@ -319,10 +320,11 @@ double conv_flops(const adaptseg_conv_desc *d) {
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  if (!pl.fast) pl.s2 = pl.bf16 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
-  const int bm = pl.bf16 ? 128 : kCfgBM[pl.cfg], bn = pl.bf16 ? pl.bf16_bn : kCfgBN[pl.cfg];
-  pl.bk = pl.bf16 ? 64 : pl.fast ? fast_bk(pl.cfg) : BK;
+  const int bm = (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
+  const int bn = pl.bf16 ? pl.bf16_bn : pl.x3 ? 128 : kCfgBN[pl.cfg];
+  pl.bk = pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
     p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
@@ -358,6 +360,7 @@ void set_splits(Plan &pl) {
   p.ktiles_per_split = per;
   pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
   if (pl.bf16) pl.slab_bytes += (bf16_wpack_bytes(pl) + 255) / 256 * 256;
+  if (pl.x3) pl.slab_bytes += (x3_wpack_bytes(pl) + 255) / 256 * 256;
 }
 
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
@@ -440,11 +443,20 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   }
   // bf16 conv math: the vector FAST cases whose K tiles of 64 stay inside one tap
   pl.bf16 = false;
-  if (conv_math() != ADAPTSEG_MATH_F32 && pl.fast && !pl.ae && !pl.be) {
+  const bool bf16_math = conv_math() == ADAPTSEG_MATH_BF16 || conv_math() == ADAPTSEG_MATH_BF16_WIDE;
+  if (bf16_math && pl.fast && !pl.ae && !pl.be) {
     if (op == ADAPTSEG_CONV_FWD) pl.bf16 = d->c % 64 == 0;
     else if (op == ADAPTSEG_CONV_BWD_DATA) pl.bf16 = d->k % 64 == 0;
     else pl.bf16 = true;
   }
+  // F32X3 conv math: the vector FAST cases whose 16-deep K tiles stay inside one tap
+  pl.x3 = false;
+  if (conv_math() == ADAPTSEG_MATH_F32X3 && pl.fast && !pl.ae && !pl.be) {
+    if (op == ADAPTSEG_CONV_FWD) pl.x3 = d->c % kX3BK == 0;
+    else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3 = d->k % kX3BK == 0;
+    else pl.x3 = true;
+  }
+  if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
     pl.cfg = 0;
     // 128x256 (8 waves) halves the refetch of the gathered A operand but measured no faster
@@ -466,6 +478,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 
 int kernel_id(const Plan &pl, int mode) {
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
+  if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)
   if (pl.fast) return 100 * mode + 10 * pl.cfg + 4 + (pl.s2 ? 4 : 0) + (pl.ae ? 2 : 0) + (pl.be ? 1 : 0);
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
@@ -473,7 +486,7 @@ int kernel_id(const Plan &pl, int mode) {
 
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
-  if (pl.p.splits > 1 && !pl.bf16) {
+  if (pl.p.splits > 1 && !pl.bf16 && !pl.x3) {
     if (!ws || ws_bytes < pl.slab_bytes) {
       set_error("conv: workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
@@ -482,15 +495,15 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   }
   hipError_t e;
   int slot;
-  if (pl.bf16) {  // [bf16 weight pack][slabs]
-    const size_t wb = (bf16_wpack_bytes(pl) + 255) / 256 * 256;
+  if (pl.bf16 || pl.x3) {  // [bf16 weight pack(s)][slabs]
+    const size_t wb = ((pl.x3 ? x3_wpack_bytes(pl) : bf16_wpack_bytes(pl)) + 255) / 256 * 256;
     if (!ws || ws_bytes < pl.slab_bytes) {
-      set_error("conv (bf16): workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
+      set_error("conv (%s): workspace %zu < required %zu", pl.x3 ? "f32x3" : "bf16", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
     }
     if (pl.p.splits > 1) pl.p.out = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + wb);
     timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
-    e = launch_bf16(pl, ws, s);
+    e = pl.x3 ? launch_x3(pl, ws, s) : launch_bf16(pl, ws, s);
     timing_end(slot, s);
     ws = reinterpret_cast<char *>(ws) + wb;  // the reduce below reads the slabs
   } else {
@@ -764,7 +777,8 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
 }
 
 int adaptseg_conv_set_math(int math) {
-  AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16 || math == ADAPTSEG_MATH_BF16_WIDE,
+  AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16 || math == ADAPTSEG_MATH_BF16_WIDE ||
+                   math == ADAPTSEG_MATH_F32X3,
                "conv_set_math: bad math %d", math);
   g_conv_math.store(math);
   return ADAPTSEG_OK;

@@ -31,6 +31,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int kMaxTaps = 64;
 constexpr int BK = 16;
+constexpr int kX3BK = 16;  // K step of the F32X3 kernel (conv_x3.hpp)
 
 struct ConvParams {
   int M, N, K;                 // GEMM extents
@@ -1247,6 +1248,7 @@ struct Plan {
   bool fast;
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
   bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
+  bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
@@ -1291,6 +1293,9 @@ hipError_t launch_fwd(const Plan &pl, hipStream_t s);
 int conv_math();
 size_t bf16_wpack_bytes(const Plan &pl);
 hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s);
+// F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)
+size_t x3_wpack_bytes(const Plan &pl);
+hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s);
 hipError_t launch_dgrad(const Plan &pl, hipStream_t s);
 hipError_t launch_wgrad(const Plan &pl, hipStream_t s);
 

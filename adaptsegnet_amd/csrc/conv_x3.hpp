@@ -1,0 +1,388 @@
+// fp32 convolution on the bf16 matrix cores: "F32X3" conv math (adaptseg_conv_set_math).
+//
+// gfx950 runs fp32-input MFMA (v_mfma_f32_32x32x2_f32) at 1/16 of the bf16 MFMA rate.  Every
+// fp32 operand v splits EXACTLY into three bf16 terms, v = v0 + v1 + v2 (round-to-nearest-even
+// each: v0 = bf16(v), v1 = bf16(v - v0), v2 = v - v0 - v1; 3 x 8 significant bits cover fp32's
+// 24, and bf16 has fp32's exponent range), so
+//     a * b = sum_{i+j<=2} a_i b_j  +  (a1 b2 + a2 b1 + a2 b2)
+// where the dropped terms are below 2^-23 |a b| — the size of one fp32 rounding.  The six kept
+// products a0b0, a0b1, a1b0, a0b2, a1b1, a2b0 are exact in the bf16 MFMA (8 x 8 bit
+// significands) and accumulate in fp32, so the conv keeps fp32 accuracy (the fp64-oracle parity
+// tests hold it to the same 2e-5 * max|ref| as the fp32 MFMA path) at 6 bf16 MFMAs per 16-deep
+// K step instead of 8 fp32 MFMAs of 4x the cycles: 768 vs 2048 MFMA cycles per 64x64 wave tile.
+//
+// Two accumulators per output tile: a0*b0 into acc, the five cross terms (2^-8 and 2^-16 of it)
+// into accs, summed once in the epilogue (one fp32 RNE add).  The bf16 MFMA's internal sum does
+// not round to nearest: products far below the largest addend (accumulator included) lose their
+// low bits, a downward bias of a few hundredths of an ulp per instruction (measured: mean -0.028
+// ulp, 14398 results below vs 8734 above round-to-nearest of 204800, tools/dbg/mfma_round.hip).
+// Fed into one accumulator, the small cross terms always sit ~2^8 below it and the bias piles up
+// over K to ~-1e-8 * max|y| (systematic, unlike fp32 MFMA's +-1e-10); in their own accumulator
+// they are the largest addends and the residual bias drops to the fp32 MFMA's level (measured on
+// a 256->256 3x3 conv: mean signed error <= 2e-10 * max|y|, rms 2e-8 vs fp32 MFMA's 5.5e-8).
+// The cost is 64 more accumulator VGPRs (occupancy 3 -> 2), which the measured per-product
+// throughput does not show (conv step 141 -> 143 TF/s fp32-equivalent).
+//
+// Same products, gathers, tile order, split-K and epilogue as igemm_fast_kernel; the operand path
+// is the bf16 kernel's (conv_bf16.hpp) with three LDS images per operand:
+//   * activations are gathered in fp32 and split into their three bf16 images while staged;
+//   * FWD / DGRAD weights are split once per call into three bf16 images packed in the exact
+//     byte order of the LDS tiles ([column tile][K step][term][128 x 16, swizzled], zero rows past
+//     N), so staging B is a contiguous 12 KB copy per K step (conv_wpack_x3_kernel);
+//   * K-contiguous activation rows are gathered 64 B (16 fp32) per row by four lanes, so one
+//     load instruction covers 16 whole rows;
+//   * K-contiguous images are 32-B rows (16 k) with the 16-B chunk XOR-swizzled by row bit 3
+//     (conflict-free ds_read_b128 fragments); M/N-contiguous images (weight gradient) are the
+//     bf16 kernel's 256-B k-rows read with ds_read_b64_tr_b16.
+// Block tile 128x128x16, 4 waves (2x2), each wave 64x64 = 2x2 MFMA tiles (x2 accumulators); 48 KB of LDS.
+#pragma once
+#include "conv_bf16.hpp"
+
+namespace adaptseg {
+
+constexpr int kX3Img = 128 * kX3BK * 2;  // bytes of one bf16 operand image (128 x 16)
+
+__device__ __forceinline__ int kc16_off(int r, int ch) { return r * 32 + ((ch ^ ((r >> 3) & 1)) << 4); }
+
+__device__ __forceinline__ bf16x8 kc16_frag(const char *img, int r0, int lane) {
+  return as_bf16x8(*reinterpret_cast<const uint4 *>(img + kc16_off(r0 + (lane & 31), lane >> 5)));
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float floatx2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// (a, b) -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32) and the two values it rounds to
+__device__ __forceinline__ uint32_t rne2(float a, float b, float &ra, float &rb) {
+  const floatx2v f = {a, b};
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
+  ra = __uint_as_float(u << 16);
+  rb = __uint_as_float(u & 0xffff0000u);
+  return u;
+}
+
+// v = hi + mid + lo exactly (each term RNE to bf16), for a pair of values: packed bf16 pairs
+__device__ __forceinline__ void split3_2(float a, float b, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
+  float ha, hb, ma, mb;
+  hi = rne2(a, b, ha, hb);
+  a -= ha;
+  b -= hb;
+  mid = rne2(a, b, ma, mb);
+  const floatx2v r = {a - ma, b - mb};
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+}
+
+// four elements -> three packed 4 x bf16
+__device__ __forceinline__ void split3(float4 v, uint2 &hi, uint2 &mid, uint2 &lo) {
+  split3_2(v.x, v.y, hi.x, mid.x, lo.x);
+  split3_2(v.z, v.w, hi.y, mid.y, lo.y);
+}
+
+template <int MODE, bool S2>
+__global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  constexpr int BM = 128, BN = 128, BK = kX3BK, NT = 256;
+  constexpr int WAVES_M = 2, WAVES_N = 2, TM = 2, TN = 2;
+  constexpr bool MC = MODE == MODE_WGRAD;   // both operands M/N-contiguous (k = output pixel)
+  constexpr int IMG = kX3Img;
+  constexpr int STAGE = 6 * IMG;            // A hi/mid/lo, B hi/mid/lo
+
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int ntn = (p.N + BN - 1) / BN;
+  int tile, split;
+  xcd_tile_split(tile, split);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int bm = tm * BM, bn = tn * BN;
+  const SegRegs sr = seg_regs(p);
+
+  int M = p.M, K = p.K, Hc = p.h, Wc = p.w, py = 0, px = 0, kh0 = 0, kw0 = 0, nkw = p.kw_;
+  if constexpr (S2) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (p.h - py + 1) >> 1;
+    Wc = (p.w - px + 1) >> 1;
+    kh0 = (py + p.pad_[0]) & 1;
+    kw0 = (px + p.pad_[0]) & 1;
+    const int nkh = (p.kh_ - kh0 + 1) >> 1;
+    nkw = (p.kw_ - kw0 + 1) >> 1;
+    M = p.n * Hc * Wc;
+    K = nkh * nkw * p.k;
+    if (bm >= M) return;
+  }
+  const int nkt = (K + BK - 1) / BK;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
+  const int ktot = p.ntaps * (MODE == MODE_FWD ? p.c : p.k);  // packed weight row length
+
+  // ---- per-slot constants ----
+  // K-contiguous A: slot i = row (tid>>2) + 64*i, float4 (tid&3) of its 16 k.
+  // M/N-contiguous: slot q = tid + 256*i: k-row q>>5, columns 4*(q&31) .. +3.
+  constexpr int NQ = 2;
+  int a_pix[NQ], a_y[NQ], a_x[NQ];
+  bool a_ok[NQ];
+  int b_off[NQ], b_dy[NQ], b_dx[NQ];
+  bool b_ok[NQ];
+  const int sj = tid & 3;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    if constexpr (!MC) {
+      const int m = bm + (tid >> 2) + 64 * i;
+      a_ok[i] = m < M;
+      const int mm = min(m, M - 1);
+      if constexpr (S2) {
+        const int j = mm % Wc, t2 = mm / Wc;
+        const int ii = t2 % Hc, b = t2 / Hc;
+        a_y[i] = ii;
+        a_x[i] = j;
+        a_pix[i] = ((b * p.oh + ii) * p.ow + j) * p.k + 4 * sj;
+      } else if constexpr (MODE == MODE_FWD) {
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        a_y[i] = oh * p.stride;
+        a_x[i] = ow * p.stride;
+        a_pix[i] = (int)b * p.sxn + a_y[i] * p.sxh + a_x[i] * p.sxw + 4 * sj;
+      } else {
+        uint32_t t = fdiv((uint32_t)mm, p.fd_w);
+        const int iw = mm - (int)t * p.w;
+        uint32_t b = fdiv(t, p.fd_hw);
+        const int ih = (int)t - (int)b * p.h;
+        a_y[i] = ih;
+        a_x[i] = iw;
+        a_pix[i] = (((int)b * p.oh + ih) * p.ow + iw) * p.k + 4 * sj;
+      }
+    } else {
+      const int q = tid + NT * i;
+      const int col = 4 * (q & 31);
+      a_ok[i] = bm + col < p.M;                    // Cout % 4 == 0
+      a_pix[i] = a_ok[i] ? bm + col : 0;
+      const int n = bn + col;
+      b_ok[i] = n < p.N;
+      const int nn = b_ok[i] ? n : 0;
+      const int tap = (int)fdiv((uint32_t)nn, p.fd_c);
+      int seg, t;
+      seg_geom(p, sr, tap, seg, t, b_dy[i], b_dx[i]);
+      b_off[i] = nn - tap * p.c;                   // input channel of the column
+    }
+  }
+  // packed B tiles of this column tile: [K step][term][4 KB]
+  const char *wtile = reinterpret_cast<const char *>(wb) + (size_t)tn * ktot / BK * 3 * IMG + 16 * tid;
+
+  float4 ra[NQ];           // A: one float4 per slot
+  float4 rbf[MC ? NQ : 1]; // MC: B float4 per slot
+  u32x4 rbh[MC ? 1 : 3];   // K-contiguous B: this thread's 16 B of each packed term image
+  bool ma[NQ], mb[NQ];
+
+  auto load_tile = [&](int kt) {
+    const int kbase = kt * BK;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
+      int seg, t, dy, dx;
+      seg_geom(p, sr, tap, seg, t, dy, dx);
+      dy = uni(dy);
+      dx = uni(dx);
+      const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const bool v = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h && (unsigned)(a_x[i] + dx) < (unsigned)p.w;
+        ma[i] = v;
+        ra[i] = ld4(p.x + (v ? a_pix[i] + soff : 0));
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const u32x4 *>(wtile + (size_t)(kt * 3 + s) * IMG);
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
+      const int co0 = kbase - tap * p.k;
+      int dy, dx, wk;
+      if constexpr (S2) {
+        const int u = tap / nkw, v = tap - u * nkw;
+        const int kh = kh0 + 2 * u, kw = kw0 + 2 * v;
+        dy = uni(-((py + p.pad_[0] - kh) >> 1));
+        dx = uni(-((px + p.pad_[0] - kw) >> 1));
+        wk = uni((kh * p.kw_ + kw) * p.k + co0);   // packed row offset of (tap, co0)
+      } else {
+        int seg, t;
+        seg_geom(p, sr, tap, seg, t, dy, dx);
+        dy = uni(dy);
+        dx = uni(dx);
+        wk = kbase;
+      }
+      const int soff = uni(co0 - (dy * p.ow + dx) * p.k);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const bool v = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh && (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
+        ma[i] = v;
+        ra[i] = ld4(p.dy + (v ? a_pix[i] + soff : 0));
+      }
+      const int wkt = wk / BK;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const u32x4 *>(wtile + (size_t)(wkt * 3 + s) * IMG);
+    } else {  // WGRAD: k = output pixel
+      const int krow0 = tid >> 5;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int m = kbase + krow0 + (NT / 32) * i;
+        const bool rv = m < K;
+        ma[i] = rv && a_ok[i];
+        ra[i] = ld4(p.dy + (size_t)(rv ? m : 0) * p.k + a_pix[i]);
+        const int mm = min(m, K - 1);
+        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+        const int ow = mm - (int)t * p.ow;
+        uint32_t b = fdiv(t, p.fd_oh);
+        const int oh = (int)t - (int)b * p.oh;
+        const int iy = oh * p.stride + b_dy[i], ix = ow * p.stride + b_dx[i];
+        const bool v = b_ok[i] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+        mb[i] = v;
+        rbf[i] = ld4(p.x + (v ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char *As = lds + buf * STAGE;
+    char *Bs = As + 3 * IMG;
+    const uint2 z2 = make_uint2(0, 0);
+    if constexpr (!MC) {
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int o = kc16_off((tid >> 2) + 64 * i, sj >> 1) + 8 * (sj & 1);
+        uint2 h, m, l;
+        split3(ra[i], h, m, l);
+        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? h : z2;
+        *reinterpret_cast<uint2 *>(As + IMG + o) = ma[i] ? m : z2;
+        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) *reinterpret_cast<u32x4 *>(Bs + s * IMG + 16 * tid) = rbh[s];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int q = tid + NT * i;
+        const int kr = q >> 5, col = 4 * (q & 31);
+        const int o = mc_off(kr, col >> 3) + 8 * ((col >> 2) & 1);
+        uint2 h, m, l;
+        split3(ra[i], h, m, l);
+        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? h : z2;
+        *reinterpret_cast<uint2 *>(As + IMG + o) = ma[i] ? m : z2;
+        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
+        split3(rbf[i], h, m, l);
+        *reinterpret_cast<uint2 *>(Bs + o) = mb[i] ? h : z2;
+        *reinterpret_cast<uint2 *>(Bs + IMG + o) = mb[i] ? m : z2;
+        *reinterpret_cast<uint2 *>(Bs + 2 * IMG + o) = mb[i] ? l : z2;
+      }
+    }
+  };
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // a0*b0 accumulates in acc, the five smaller cross terms in accs (see header comment)
+  floatx16 accs[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accs[i][j][r] = 0.f;
+
+  int cur = 0;
+  // One 16-deep K step from LDS buffer `cur`: the six split products of every 32x32 tile,
+  // term-major so consecutive MFMAs write different accumulators.
+  auto compute = [&]() {
+    const char *As = lds + cur * STAGE;
+    const char *Bs = As + 3 * IMG;
+    bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[s][i] = MC ? mc_frag(As + s * IMG, wm * 64 + i * 32, 0, lane) : kc16_frag(As + s * IMG, wm * 64 + i * 32, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[s][j] = MC ? mc_frag(Bs + s * IMG, wn * 64 + j * 32, 0, lane) : kc16_frag(Bs + s * IMG, wn * 64 + j * 32, lane);
+    }
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
+    constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+          else accs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[TA[u]][i], b[TB[u]][j], accs[i][j], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      compute();
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += accs[i][j];
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+                                                      reinterpret_cast<float *>(lds));
+}
+
+// Weight pack: the three bf16 terms of every weight of the GEMM's B operand (FWD: row n = Cout,
+// k = (seg, tap, ci); DGRAD: row n = Cin, k = (tap, co)) at the byte the kernel's LDS tile
+// wants: [n / 128][k / 16][term][kc16 image of 128 rows x 16 k]; rows >= N are zeros.
+// One thread per (row, k) of the padded operand, the source's contiguous axis fastest.
+template <int MODE>
+__global__ void conv_wpack_x3_kernel(const ConvParams p, char *out, int rows_pad, int ktot) {
+  const int64_t total = (int64_t)rows_pad * ktot;
+  const int nkt = ktot / kX3BK;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int n, k;
+    float v = 0.f;
+    if constexpr (MODE == MODE_FWD) {  // W[co][seg*kseg + tk]: k fastest
+      n = (int)(i / ktot);
+      k = (int)(i - (int64_t)n * ktot);
+      if (n < p.k) {
+        const int seg = k / p.kseg;
+        v = seg_ptr(p, seg)[(size_t)n * p.kseg + (k - seg * p.kseg)];
+      }
+    } else {  // W_seg(tap)[co][t][ci]: ci (the row) fastest
+      k = (int)(i / rows_pad);
+      n = (int)(i - (int64_t)k * rows_pad);
+      if (n < p.c) {
+        const int tap = k / p.k, co = k - tap * p.k;
+        const int seg = tap / p.taps_per_seg, t = tap - seg * p.taps_per_seg;
+        v = seg_ptr(p, seg)[((size_t)co * p.taps_per_seg + t) * p.c + n];
+      }
+    }
+    const int r = n & 127, kk = k & (kX3BK - 1);
+    char *dst = out + ((size_t)(n >> 7) * nkt + (k >> 4)) * 3 * kX3Img + kc16_off(r, kk >> 3) + 2 * (kk & 7);
+    const __bf16 h = (__bf16)v;
+    const float r1 = v - (float)h;
+    const __bf16 m = (__bf16)r1;
+    *reinterpret_cast<__bf16 *>(dst) = h;
+    *reinterpret_cast<__bf16 *>(dst + kX3Img) = m;
+    *reinterpret_cast<__bf16 *>(dst + 2 * kX3Img) = (__bf16)(r1 - (float)m);
+  }
+}
+
+}  // namespace adaptseg

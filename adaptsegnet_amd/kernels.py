@@ -17,11 +17,11 @@ import torch
 from . import _lib
 from . import ops as _ops
 from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
-                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_BF16_WIDE, MATH_F32,
+                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_BF16_WIDE, MATH_F32, MATH_F32X3,
                    ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "MATH_BF16_WIDE", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "MATH_BF16_WIDE", "MATH_F32X3", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
@@ -71,8 +71,9 @@ class ConvGeom:
 
 
 def set_conv_math(math: int) -> None:
-    """Process-wide conv arithmetic: MATH_F32 (fp32 MFMA, default) or MATH_BF16 (operands
-    rounded to bf16, fp32 accumulate: BASELINE config c5).  Workspace sizes depend on it,
+    """Process-wide conv arithmetic: MATH_F32X3 (default: fp32 through exact three-term bf16
+    splits on the bf16 MFMA, fp32-accurate, conv_x3.hpp), MATH_F32 (the fp32-input MFMA
+    kernels) or MATH_BF16 (operands rounded to bf16, fp32 accumulate: BASELINE config c5).  Workspace sizes depend on it,
     so the descriptor cache is keyed on it."""
     _ops.set_math(math)
 

@@ -35,7 +35,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, MATH_F32, ConvDesc, check
+from ._lib import CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, MATH_F32X3, ConvDesc, check
 
 LIB = torch.library.Library("adaptseg", "DEF")
 
@@ -78,7 +78,7 @@ def _ws_args(nbytes: int, device):
 # Conv descriptors (host planning only: no GPU needed)
 # ---------------------------------------------------------------------------------------
 _DESC_CACHE: dict = {}
-_CONV_MATH = [MATH_F32]
+_CONV_MATH = [MATH_F32X3]   # the library's default (adaptseg_conv_get_math)
 
 
 def conv_desc(n, c, h, w, strides, cout, kh, kw, stride, pads, dils):

@@ -11,9 +11,15 @@ batch 4 per GPU, source and target 1024x512, Vanilla GAN, fp32 (the reference's 
 ``value`` = (source, target) pairs per second over all ranks (weak scaling: batch per GPU
 is fixed).  Rank 0 prints ONE JSON line.
 
+Conv math: the fp32 configs run F32X3 by default (fp32-accurate convs on the bf16 MFMA through
+exact three-term bf16 operand splits, six bf16 products per fp32 product; conv_x3.hpp),
+``--conv-math f32`` the fp32-input MFMA kernels; c5 runs bf16 operands.
+
 roofline: the dominant implicit-GEMM conv kernel symbol (most algorithmic FLOPs per step)
 is bracketed by hipEvents inside the library during the timed steps; achieved = its
-algorithmic FLOPs / its summed launch time, against the fp32 MFMA peak (157.3 TFLOP/s).
+algorithmic FLOPs / its summed launch time, against that kernel's MFMA ceiling: the fp32 MFMA
+peak (157.3 TFLOP/s) for the fp32-input kernels, the bf16 dense peak / 6 (419.4 TFLOP/s of
+fp32 products) for F32X3, the bf16 dense peak (2516.6) for bf16.
 cpu_baseline: the oracle (stock-PyTorch CPU restatement of the reference step, the
 reference's own arithmetic) timed on this host for ONE single-level step at batch 1.
 """
@@ -143,8 +149,19 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
         8: (128, 128, 2, 2, 16)}
 
 
+def kernel_peak(sel):
+    """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
+    if sel % 100 >= 95:
+        return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
+    if sel % 100 >= 90:
+        return BF16_MFMA_PEAK_TFLOPS, "bf16"
+    return FP32_MFMA_PEAK_TFLOPS, "fp32-input MFMA"
+
+
 def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
+    if sel % 100 >= 95:
+        return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
     if cfg == 9:
         return f"igemm_bf16_kernel<{op}, {'true' if var & 1 else 'false'}, {256 if var & 2 else 128}>"
     bm, bn, wm, wn, bk = _CFG[cfg]
@@ -208,6 +225,9 @@ def main():
                     help="c2 (default, BASELINE metric at N=1), c3 multi-level, c4 DeeplabVGG, "
                          "c5 multi-level LS bf16 batch 4")
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
+    ap.add_argument("--conv-math", default="f32x3", choices=("f32x3", "f32"),
+                    help="conv arithmetic of the fp32 configs: f32x3 (default, fp32-accurate on the "
+                         "bf16 MFMA) or f32 (the fp32-input MFMA kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--overlap", action="store_true",
@@ -240,8 +260,8 @@ def main():
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
 
     level, gan, batch, src_wh, tgt_wh, gen, math = CONFIGS[args.config]
-    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32)
-    peak = BF16_MFMA_PEAK_TFLOPS if math == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    conv_math = "bf16" if math == "bf16" else args.conv_math
+    K.set_conv_math({"bf16": K.MATH_BF16, "f32x3": K.MATH_F32X3, "f32": K.MATH_F32}[conv_math])
     if args.batch:
         batch = args.batch
     torch.manual_seed(1338 + rank)
@@ -273,10 +293,9 @@ def main():
 
     inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize)
     step_flops = sum(inv.values())
-    # the roofline kernel: the symbol with the most algorithmic FLOPs per step (with bf16 math,
-    # among the bf16 kernels, which the peak below refers to)
-    cand = {k: v for k, v in inv.items() if math != "bf16" or k // 10 % 10 == 9}
-    dom = max(cand, key=cand.get)
+    # the roofline kernel: the symbol with the most algorithmic FLOPs per step
+    dom = max(inv, key=inv.get)
+    peak, family = kernel_peak(dom)
     hbm = []
     if not args.no_roofline:
         # HBM-bound kernels (interp / loss / BN passes): hipEvent pairs around each of their
@@ -334,6 +353,7 @@ def main():
                    "global_batch": batch * world, "parallelism": f"dp{world}",
                    "step_conv_tflop": step_flops / 1e12,
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
+                   "conv_math": conv_math,
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    "losses_last_step": losses},
@@ -344,6 +364,8 @@ def main():
         traffic, tsrc = pmc_traffic(args.config, dom)
         out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak,
                            "unit": "TFLOP/s", "frac": ach / peak, "traffic": traffic,
+                           "kernel_family": family,
+                           "frac_of_fp32_mfma_peak": ach / FP32_MFMA_PEAK_TFLOPS,
                            "traffic_unit": "bytes/launch (L2 memory-side FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": tsrc,
                            "algorithmic_flop_per_launch": k_flops / k_launches,

@@ -79,7 +79,9 @@ enum adaptseg_conv_flags {
 enum adaptseg_conv_math {
   ADAPTSEG_MATH_F32 = 0,
   ADAPTSEG_MATH_BF16 = 1,
-  ADAPTSEG_MATH_BF16_WIDE = 2  /* BF16 with 128x256 tiles for fwd / data-grad products with N >= 256 */
+  ADAPTSEG_MATH_BF16_WIDE = 2, /* BF16 with 128x256 tiles for fwd / data-grad products with N >= 256 */
+  ADAPTSEG_MATH_F32X3 = 3      /* fp32 on the bf16 MFMA: exact 3-term bf16 splits of both operands,
+                                  the 6 products above 2^-23 relative (fp32-accurate; conv_x3.hpp) */
 };
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);

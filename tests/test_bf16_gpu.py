@@ -33,7 +33,7 @@ def bf16_math():
     k = K()
     k.set_conv_math(k.MATH_BF16)
     yield k
-    k.set_conv_math(k.MATH_F32)
+    k.set_conv_math(k.MATH_F32X3)   # the library default
 
 
 @pytest.fixture(params=["bf16", "bf16_wide"])
@@ -42,7 +42,7 @@ def bf16_any(request):
     k = K()
     k.set_conv_math(k.MATH_BF16 if request.param == "bf16" else k.MATH_BF16_WIDE)
     yield k
-    k.set_conv_math(k.MATH_F32)
+    k.set_conv_math(k.MATH_F32X3)   # the library default
 
 
 def bf(t):
@@ -141,10 +141,10 @@ def test_bf16_fused_bn_statistics(bf16_math):
 
 def test_bf16_math_is_process_wide_and_default_off():
     k = K()
-    assert k.get_conv_math() == k.MATH_F32
+    assert k.get_conv_math() == k.MATH_F32X3
     geom = k.ConvGeom(64, 64, 3, 3, 1, (1,), (1,))
     kid, _ = k.conv_kernel_id(geom, 2, 16, 16, 0)
-    assert kid // 10 % 10 != 9
+    assert kid % 100 in (95, 96)   # the F32X3 kernel, not the bf16-operand one (90..93)
     with pytest.raises(RuntimeError):
         k.set_conv_math(7)
 

@@ -26,8 +26,32 @@ def test_version_and_error_paths_without_gpu():
     assert b"bad" in L.adaptseg_last_error()
 
 
+def test_default_conv_math_selects_f32x3():
+    """The library's default conv math is F32X3: the vector products of the step run on the
+    split-bf16 kernel (selector 100*op + 95, +1 for the stride-2 parity path); thin and
+    per-element products keep their fp32 kernels."""
+    from adaptsegnet_amd import kernels as K
+    assert K.get_conv_math() == K.MATH_F32X3
+    g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
+    assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [95, 195, 295]
+    s2 = K.ConvGeom(256, 128, 1, 1, 2, (0,), (1,))
+    assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 196
+    stem = K.ConvGeom(3, 64, 7, 7, 2, (3,), (1,))
+    assert K.conv_kernel_id(stem, 4, 512, 1024, 0, (3 * 512 * 1024, 512 * 1024, 1024, 1))[0] % 100 < 90
+    d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))
+    assert K.conv_kernel_id(d5, 4, 32, 64, 0)[0] == 80
+
+
 def test_workspace_and_kernel_selection_on_host():
     from adaptsegnet_amd import kernels as K
+    K.set_conv_math(K.MATH_F32)
+    try:
+        _fp32_kernel_selection(K)
+    finally:
+        K.set_conv_math(K.MATH_F32X3)
+
+
+def _fp32_kernel_selection(K):
     g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
     kid, splits = K.conv_kernel_id(g, 4, 64, 128, 0)
     assert kid == 84 and splits == 1          # fwd, 128x128 BK16 occupancy-3 tile (cfg 8), FAST, no K split

@@ -28,7 +28,7 @@ def _step_products(config):
     tsize = src if level == "single-level" else tgt
     prods = set()
     prev = K.get_conv_math()
-    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32)
+    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32X3 if math == "f32x3" else K.MATH_F32)
     try:
         bench.conv_inventory(model, D, level, batch, src, tgt, tsize, products=prods)
     finally:
@@ -48,8 +48,8 @@ def test_every_step_conv_variant_is_oracle_checked(config):
         # fp32 kernels, which the fp32 cases cover under bf16 math as well
         for c in CONV_CASES + LARGE_CASES:
             covered |= case_products(K, c, K.MATH_BF16)
-    else:
+    else:   # the fp32 cases run under both fp32 conv maths (tests/test_ops_gpu.py::conv_math)
         for c in CONV_CASES + LARGE_CASES:
-            covered |= case_products(K, c, K.MATH_F32)
+            covered |= case_products(K, c, K.MATH_F32) | case_products(K, c, K.MATH_F32X3)
     missing = sorted(prods - covered)
     assert not missing, f"{config}: step conv products without an fp64 parity case: {missing}"

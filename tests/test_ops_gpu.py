@@ -86,8 +86,18 @@ def _ref_conv(x, ws, bs, stride, pads, dils):
     return out
 
 
+@pytest.fixture(params=["f32", "f32x3"])
+def conv_math(request):
+    """The two fp32 conv maths: exact fp32 MFMA and F32X3 (fp32 through exact 3-term bf16
+    splits on the bf16 MFMA, conv_x3.hpp) — both held to the same fp64 tolerance."""
+    k = K()
+    k.set_conv_math(k.MATH_F32 if request.param == "f32" else k.MATH_F32X3)
+    yield request.param
+    k.set_conv_math(k.MATH_F32X3)   # the library default
+
+
 @pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{i}" for i in range(len(CONV_CASES))])
-def test_conv_fwd_dgrad_wgrad(case):
+def test_conv_fwd_dgrad_wgrad(case, conv_math):
     k = K()
     n, cin, h, w, cout, ks, stride, pads, dils, bias = case
     g = torch.Generator().manual_seed(hash(case) % (2 ** 31))
@@ -169,7 +179,7 @@ def test_aspp_tap_gemm_epilogues(rates):
     bs = [torch.randn(cout, generator=g, dtype=torch.float64) for _ in rates]
     geom = k.ConvGeom(cin, cout, 3, 3, 1, rates, rates)
     sel, _ = k.conv_kernel_id(geom, n, h, w, 0)
-    assert sel % 100 // 10 in (0, 8), sel  # a 128x128 tile of the dense 1x1 GEMM, not 256x32
+    assert sel % 100 // 10 in (0, 8, 9), sel  # a 128x128 tile of the dense 1x1 GEMM, not 256x32
     ref = _ref_conv(x, ws, bs, 1, rates, rates)
     res = torch.randn(ref.shape, generator=g, dtype=torch.float64)
     wd, bd = [w_cl(t) for t in ws], [t.float().to(DEV) for t in bs]
@@ -408,7 +418,7 @@ def test_to_nhwc_and_axpy():
 
 
 @pytest.mark.parametrize("case", LARGE_CASES, ids=[f"L{i}" for i in range(len(LARGE_CASES))])
-def test_conv_large_grid_epilogues(case):
+def test_conv_large_grid_epilogues(case, conv_math):
     """Grids of >= 257 output tiles (the c2 / c3 / c5 layer sizes): forward and data gradient
     store from the in-kernel epilogue (no K split), so every epilogue flag the engine uses is
     checked there against fp64 torch:
@@ -478,7 +488,7 @@ def test_conv_large_grid_epilogues(case):
 
 
 @pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1), (2, 256, 96, 96, 256, 3), (2, 128, 20, 18, 48, 1)])
-def test_conv_dgrad_into_bn_relu_backward(shape):
+def test_conv_dgrad_into_bn_relu_backward(shape, conv_math):
     """The Bottleneck backward chain conv2 / conv3 data gradient -> train-mode BN+ReLU backward
     with the ReLU mask recomputed from the BN input (engine.block_backward), in place, vs
     fp64 torch autograd of conv(relu(bn(x))).  The first two shapes are unsplit large grids
@@ -587,3 +597,43 @@ def test_torch_ops_conv_and_ce_vs_oracle():
     torch.ops.adaptseg.softmax_ce_fwd(nhwc(logits), lab.to(DEV), 255, None, out)
     lref = F.cross_entropy(logits, lab, ignore_index=255)
     assert abs(out[0].item() - lref.item()) < 1e-5 * lref.item()
+
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_f32x3_accuracy_matches_fp32_mfma(op):
+    """F32X3 is fp32-accurate: on a layer3-shaped atrous conv (K = 2304) and a wide 1x1 (K =
+    1024) its max error vs fp64 stays within 1.5x that of the exact fp32-MFMA kernel (the dropped
+    split terms are below one fp32 rounding per product), and the F32X3 kernel is the one
+    selected (selector 100*op + 95)."""
+    k = K()
+    g = torch.Generator().manual_seed(77)
+    errs = {}
+    for n, cin, h, w, cout, ks, dil in ((2, 256, 48, 64, 256, 3, 2), (2, 1024, 32, 48, 256, 1, 1)):
+        geom = k.ConvGeom(cin, cout, ks, ks, 1, ((ks // 2) * dil,), (dil,))
+        x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+        wt = torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) / (cin * ks * ks) ** 0.5
+        gy = torch.randn(n, cout, h, w, generator=g, dtype=torch.float64)
+        if op == 0:
+            ref = F.conv2d(x, wt, None, 1, geom.pads[0], dil)
+        elif op == 1:
+            ref = torch.nn.grad.conv2d_input(x.shape, wt, gy, 1, geom.pads[0], dil)
+        else:
+            ref = torch.nn.grad.conv2d_weight(x, wt.shape, gy, 1, geom.pads[0], dil)
+        for math in ("f32", "f32x3"):
+            k.set_conv_math(k.MATH_F32 if math == "f32" else k.MATH_F32X3)
+            try:
+                sel, _ = k.conv_kernel_id(geom, n, h, w, op)
+                assert (sel % 100 >= 95) == (math == "f32x3"), (math, sel)
+                if op == 0:
+                    out = nchw(k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)]))
+                elif op == 1:
+                    out = nchw(k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)]))
+                else:
+                    dw = torch.zeros(cout, ks, ks, cin, device=DEV)
+                    k.conv_wgrad(geom, nhwc(gy), nhwc(x), n, h, w, [dw], accumulate=False)
+                    out = dw.permute(0, 3, 1, 2).double().cpu()
+            finally:
+                k.set_conv_math(k.MATH_F32X3)   # the library default
+            errs[math] = rel(out, ref)
+        print(f"op {op} K={cin * ks * ks}: max rel err f32 {errs['f32']:.3e}  f32x3 {errs['f32x3']:.3e}")
+        assert errs["f32x3"] <= 1.5 * errs["f32"] + 1e-7, errs
