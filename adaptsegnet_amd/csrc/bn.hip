@@ -437,16 +437,21 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
   hipStream_t s = as_stream(stream);
   ReducePlan r = reduce_plan(rows, c);
   float *partial = reinterpret_cast<float *>(ws);
+  int slot;  // x in
+  timing_begin(kTBnReduceStats, s, 4.0 * rows * c, &slot);
   bn_reduce_kernel<0><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
                                                                 nullptr, nullptr, nullptr, 0, r.per, partial);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_reduce<stats>");
   bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
                                                                    save_invstd, running_mean, running_var,
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
   const ApplyPlan ap = apply_plan(rows, c);
+  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
                                                                  weight, bias, res, y, relu);
+  timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
 }
@@ -500,6 +505,7 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   const int rmode = relu == 0 ? 0 : relu == 1 ? (y ? 1 : 2) : (y ? 3 : 4);
   hipStream_t s = as_stream(stream);
   float *coef = nullptr;
+  int slot;
   if (train) {
     size_t need = bn_ws_bytes(rows, c);
     if (!ws || ws_bytes < need) {
@@ -509,15 +515,18 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
     ReducePlan r = reduce_plan(rows, c);
     float *partial = reinterpret_cast<float *>(ws);
     coef = partial + (size_t)r.splits * 2 * c;
+    // dy, x (+ y for the mask from y) in
+    timing_begin(kTBnReduceBwd, s, 4.0 * rows * c * (2 + ((rmode == 1 || rmode == 3) ? 1 : 0)), &slot);
     bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
                                                                   save_invstd, weight, bias, rmode, r.per,
                                                                   partial);
+    timing_end(slot, s);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
                                                                    coef, dweight, dbias);
     AS_CHECK_LAUNCH("bn_bwd_final");
   }
-  int slot;  // dy, x (train), y (mask from y) in; dx, dres out
+  // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
                4.0 * rows * c * (2 + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)),
                &slot);

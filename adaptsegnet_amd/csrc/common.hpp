@@ -76,7 +76,8 @@ constexpr int kTimingMemBase = 1000;
 enum TimingMemId {
   kTUpsampleFwd = 1000, kTUpsampleBwd = 1001, kTSoftmaxFwd = 1002, kTSoftmaxBwd = 1003,
   kTCeFwd = 1004, kTCeBwd = 1005, kTBnApply = 1006, kTBnBwdApply = 1007,
-  kTUp2Fwd = 1008, kTUp2Bwd = 1009, kTWarpFwd = 1010, kTWarpDflow = 1011, kTWarpScatter = 1012
+  kTUp2Fwd = 1008, kTUp2Bwd = 1009, kTWarpFwd = 1010, kTWarpDflow = 1011, kTWarpScatter = 1012,
+  kTBnReduceStats = 1013, kTBnReduceBwd = 1014, kTSplitkReduce = 1015
 };
 void timing_begin(int kernel_id, hipStream_t s, double units, int *slot);
 void timing_end(int slot, hipStream_t s);

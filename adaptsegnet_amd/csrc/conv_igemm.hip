@@ -532,6 +532,11 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
       if (mode == MODE_FWD)
         for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
     }
+    int slot;  // the slabs + read-modify-write operands in, the output out
+    const int extra = (q.flags & ADAPTSEG_EPI_ACCUMULATE ? 1 : 0) +
+                      (mode != MODE_WGRAD && (q.flags & ADAPTSEG_EPI_RESIDUAL) ? 1 : 0) +
+                      (mode != MODE_WGRAD && (q.flags & kEpiActGrad) ? 1 : 0);
+    timing_begin(kTSplitkReduce, s, 4.0 * (double)total * (q.splits + 1 + extra), &slot);
     if (vec) {
       const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
       const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
@@ -544,6 +549,7 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
       int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
       splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
     }
+    timing_end(slot, s);
     AS_CHECK_LAUNCH("splitk_reduce");
   }
   return ADAPTSEG_OK;

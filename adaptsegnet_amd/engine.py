@@ -283,22 +283,36 @@ class _DeeplabMultiFn(torch.autograd.Function):
                 idx += model._pidx["layer5"]
             model._arena.claim(idx)
         ws = WgradStream(ctx.x.device) if need_w else None
+        hook = model._grad_hook if need_w else None
+
+        def done(ordinal):
+            # a backward unit's weight gradients are queued (on the side stream): the
+            # data-parallel hook may start all-reducing the gradient buckets now complete
+            if hook is not None:
+                hook(ordinal, ws.side)
+
+        # unit ordinals follow DeeplabMulti._bwd_units
+        n4 = len(model.layer4)
         gp3 = None
         if g2_up is not None:
             gx2 = K.upsample_bwd(K.nhwc_view(g2_up), h3, w3)
             gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w, ws=ws)
+            done(0)
             del gx2
             ctx.q = None
-            for i in reversed(range(len(model.layer4))):
+            for i in reversed(range(n4)):
                 gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w, ws)
+                done(n4 - i)
                 ctx.recs4[i] = None
             gp3 = gq
         if g1_up is not None:
             gx1 = K.upsample_bwd(K.nhwc_view(g1_up), h3, w3)
             gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3, ws=ws)
+            done(n4 + 1)
             del gx1
         ctx.p3 = None
         if gp3 is None:
+            done(None)
             if ws is not None:
                 ws.join()
             return None, None, None, None, None, None
@@ -306,6 +320,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
         g = gp3
         for i in reversed(range(len(blocks))):
             g = block_backward(blocks[i], ctx.recs[i], g, need_w, ws)
+            done(n4 + 2 + len(blocks) - 1 - i)
             ctx.recs[i] = None
         c0, y0, s0, am = ctx.stem
         ctx.stem = None
@@ -315,6 +330,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
         gs = model.conv1.geom()
         if need_w and model.conv1.weight.grad is not None:
             _wgrad(ws, gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
+        done(None)
         dx = None
         if ctx.needs_input_grad[1]:
             dx = K.as_nchw(K.conv_dgrad(gs, dy0, n, h, w, [model.conv1.weight]))

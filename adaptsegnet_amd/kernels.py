@@ -395,7 +395,9 @@ MEM_KERNELS = {1000: "upsample_fwd_kernel", 1001: "upsample_bwd_{x,y}_kernel", 1
                1003: "softmax_bwd", 1004: "ce_fwd (+final)", 1005: "ce_bwd", 1006: "bn_apply2d_kernel",
                1007: "bn_bwd_apply2d_kernel", 1008: "up2_relu_cat_fwd_kernel", 1009: "up2_relu_cat_bwd_kernel",
                1010: "grid_warp_fwd_kernel", 1011: "grid_warp_dflow_kernel",
-               1012: "grid_warp input-gradient scatter (memset + absmax + scatter + convert)"}
+               1012: "grid_warp input-gradient scatter (memset + absmax + scatter + convert)",
+               1013: "bn_reduce_kernel<0> (stats)", 1014: "bn_reduce_kernel<1> (backward sums)",
+               1015: "splitk_reduce{4}_kernel"}
 
 
 def timing_enable_mem(enable: bool = True):

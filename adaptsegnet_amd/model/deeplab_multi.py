@@ -78,6 +78,9 @@ class ResNetMulti(nn.Module):
         normal_init_(self, 0.01)
         self._arena = None
         self._arena_valid = False
+        # data parallel: called as hook(unit_ordinal, stream) after the engine launched a
+        # backward unit's weight gradients (see _bwd_units), hook(None, stream) at the end
+        self._grad_hook = None
 
     def _make_layer(self, block, planes, blocks, stride=1, dilation=1):
         downsample = None
@@ -127,6 +130,60 @@ class ResNetMulti(nn.Module):
             segs.append(([p for p in order if counts[id(p)] == mult], 0, mult))
         segs.append((list(self.get_10x_lr_params()), 1, 1))
         return segs
+
+    # -- gradient buckets (data parallel) -----------------------------------------------
+    def _bwd_units(self):
+        """The generator backward's weight-gradient units in the order the engine finishes
+        them (engine._DeeplabMultiFn.backward): layer6, layer4 blocks last to first, layer5,
+        layer3 .. layer1 blocks last to first, the stem.  [(name, arena param indices)]."""
+        A = self._arena
+
+        def idx(*mods):
+            return A.index_of([p for m in mods for p in m.parameters() if p.requires_grad])
+
+        units = [("layer6", idx(self.layer6))]
+        units += [(f"layer4.{i}", idx(self.layer4[i])) for i in reversed(range(len(self.layer4)))]
+        units.append(("layer5", idx(self.layer5)))
+        blocks = [(f"layer{li}.{i}", b) for li, layer in ((1, self.layer1), (2, self.layer2),
+                                                          (3, self.layer3)) for i, b in enumerate(layer)]
+        units += [(nm, idx(b)) for nm, b in reversed(blocks)]
+        units.append(("stem", idx(self.conv1, self.bn1)))
+        return units
+
+    def _grad_buckets(self, bucket_bytes):
+        """Split the gradient arena into all-reduce buckets that complete in backward order.
+
+        Consecutive backward units are grouped until a bucket holds >= ``bucket_bytes``; a
+        bucket is ready once the engine has launched the weight gradients of its last unit.
+        Returns [(last_unit_ordinal, [(start, end), ...])] with each bucket's arena element
+        ranges coalesced into contiguous runs (block convs, downsample convs and the 10x
+        classifier sit in different arena segments, so a bucket spans 1-3 runs).  The runs of
+        all buckets tile the arena exactly once (padding between parameters included)."""
+        A = self._arena
+        ends = A.offsets[1:] + [A.numel]
+        units = self._bwd_units()
+        seen = set()
+        buckets, cur, cur_bytes = [], [], 0
+        for ordinal, (_name, ids) in enumerate(units):
+            ids = [i for i in ids if i not in seen]
+            seen.update(ids)
+            cur += ids
+            cur_bytes += sum(4 * (ends[i] - A.offsets[i]) for i in ids)
+            if cur and (cur_bytes >= bucket_bytes or ordinal == len(units) - 1):
+                buckets.append((ordinal, cur))
+                cur, cur_bytes = [], 0
+        assert len(seen) == len(A.params), "every trainable parameter belongs to one unit"
+        out = []
+        for ordinal, ids in buckets:
+            runs = []
+            for i in sorted(ids, key=lambda i: A.offsets[i]):
+                s, e = A.offsets[i], ends[i]
+                if runs and runs[-1][1] == s:
+                    runs[-1][1] = e
+                else:
+                    runs.append([s, e])
+            out.append((ordinal, [tuple(r) for r in runs]))
+        return out
 
     # -- arena --------------------------------------------------------------------------
     def _apply(self, fn, *args, **kwargs):

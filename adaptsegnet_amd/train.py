@@ -23,10 +23,14 @@ passed as the initial gradient of ``backward`` instead of multiplying the loss t
 constant label tensors (:621, ...) are folded into the loss kernels, and the per-loss
 ``.item()`` host syncs are deferred to ``StepLosses.values()``.
 
-Data parallel (one process per GPU): every rank runs the step on its own shard, then ONE
-all-reduce (SUM) per parameter arena replaces DataParallel's gradient gather; the 1/world
-average is folded into the optimiser.  BN statistics stay per-rank, as in the reference's
-per-replica DataParallel semantics.
+Data parallel (one process per GPU): every rank runs the step on its own shard, and SUM
+all-reduces of the gradient arenas replace DataParallel's gradient gather
+(train_gta2cityscapes_multi.py:224-225); the 1/world average is folded into the optimiser.
+DeeplabMulti's 178 MB arena is reduced in buckets (``bucket_mb``) launched from inside the
+step's last generator backward as each bucket's weight gradients are queued (layer6 and layer4
+first), so the collectives overlap the rest of that backward; the discriminators' arenas follow
+their last backward.  BN statistics stay per-rank, as in the reference's per-replica
+DataParallel semantics.
 """
 from __future__ import annotations
 
@@ -66,6 +70,9 @@ class StepConfig:
     # but every forward conv then shares the GPU with backward kernels, which halves the
     # per-launch roofline of the dominant kernel that bench.py reports.
     overlap_domains: bool = False
+    # data parallel: size of the generator's gradient all-reduce buckets (DeeplabMulti); 0 =
+    # one all-reduce of the whole arena after its last backward
+    bucket_mb: float = 32.0
     # HIP stream priority of the step's main chain (None: the caller's stream; "auto": high
     # for DeeplabMulti, the caller's stream for DeeplabVGG); see step()
     main_priority: int | str | None = "auto"
@@ -198,6 +205,28 @@ class AdaptSegTrainer:
                 pending.append(dist.all_reduce(m.arena.grad, op=dist.ReduceOp.SUM,
                                                      group=self.pg, async_op=True))
 
+    def _g_sync_begin(self):
+        """Before the step's last generator backward: install the bucketed all-reduce hook on
+        a generator that supports it (DeeplabMulti).  Returns the hook or None."""
+        if self.world == 1 or self.cfg.bucket_mb <= 0 or not hasattr(self.model, "_grad_buckets"):
+            return None
+        if getattr(self.model, "_arena", None) is None:
+            return None
+        hook = _BucketAllReduce(self, self.model.arena.grad,
+                                self.model._grad_buckets(int(self.cfg.bucket_mb * 2 ** 20)))
+        self.model._grad_hook = hook
+        return hook
+
+    def _g_sync_end(self, hook):
+        """After the step's last generator backward: every bucket (or the whole arena) has its
+        all-reduce in flight."""
+        if hook is None:
+            self._start_sync((self.model,))
+            return
+        self.model._grad_hook = None
+        hook(None, None)
+        self.g_allreduce_ranges = list(hook.launched)   # (start, end) arena ranges, launch order
+
     def _finish_sync(self):
         """Make the current stream wait for every launched all-reduce (no host sync)."""
         for w in self.__dict__.get("_pending", ()):
@@ -251,7 +280,7 @@ class AdaptSegTrainer:
         batches = list(batches)
         self._pending = []
         for idx, batch in enumerate(batches):
-            g_done = (lambda: self._start_sync((self.model,))) if idx == len(batches) - 1 else None
+            g_done = _GSync(self) if idx == len(batches) - 1 else None
             if c.level == "source-only":
                 self._sub_source_only(batch[0], batch[1], inv, L, g_done)
                 continue
@@ -287,10 +316,12 @@ class AdaptSegTrainer:
         second head, backward; the step is the generator's SGD only."""
         pred2 = self._pred_single(images, self.cfg.input_size, self._flow(images))
         loss_seg2 = F.cross_entropy2d(pred2, labels, self.cfg.ignore_label)
+        if g_done is not None:
+            g_done.begin()
         self._backward([loss_seg2], [inv])
         L.add("loss_seg2", loss_seg2, inv)
         if g_done is not None:
-            g_done()
+            g_done.end()
 
     def _sub_single(self, images, labels, images_t, inv, tsize, L, g_done=None):
         """train_gta2cityscapes_multi.py:385-461."""
@@ -308,10 +339,12 @@ class AdaptSegTrainer:
             d_out2 = D2(F.softmax2d(pred_target2))
             loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
             self._join_source(ov)
+            if g_done is not None:
+                g_done.begin()
             self._backward([loss_adv_target2], [c.lambda_adv_target2 * inv])
             L.add("loss_adv_target2", loss_adv_target2, inv)
             if g_done is not None:
-                g_done()
+                g_done.end()
         self._overlap_end(ov, pred_target2, loss_adv_target2)
 
         self._set_requires_grad(D2, True)
@@ -344,12 +377,14 @@ class AdaptSegTrainer:
             loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
             loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
             self._join_source(ov)
+            if g_done is not None:
+                g_done.begin()
             self._backward([loss_adv1, loss_adv2],
                            [c.lambda_adv_target1 * inv, c.lambda_adv_target2 * inv])
             L.add("loss_adv_target1", loss_adv1, inv)
             L.add("loss_adv_target2", loss_adv2, inv)
             if g_done is not None:
-                g_done()
+                g_done.end()
         self._overlap_end(ov, pred_target1, pred_target2, loss_adv1, loss_adv2)
 
         self._set_requires_grad(D1, True)
@@ -368,3 +403,44 @@ class AdaptSegTrainer:
         self._backward([loss_d2], [inv / 2])
         L.add("loss_D1", loss_d1, inv / 2)
         L.add("loss_D2", loss_d2, inv / 2)
+
+
+class _GSync:
+    """begin() / end() around the step's last generator backward (the gradients are final
+    after it): bucketed all-reduces launched from inside that backward, or one whole-arena
+    all-reduce after it."""
+
+    def __init__(self, trainer):
+        self.tr, self.hook = trainer, None
+
+    def begin(self):
+        self.hook = self.tr._g_sync_begin()
+
+    def end(self):
+        self.tr._g_sync_end(self.hook)
+
+
+class _BucketAllReduce:
+    """The generator backward's data-parallel hook (DeeplabMulti._grad_hook).
+
+    ``buckets`` = DeeplabMulti._grad_buckets(): [(last_unit_ordinal, [(start, end), ...])] in
+    completion order.  hook(ordinal, stream) launches the SUM all-reduce of every bucket whose
+    last backward unit is <= ordinal (units skipped by this backward, e.g. layer5 in the
+    single-level step, ride with the next unit); hook(None, _) launches the rest.  The
+    collectives are issued with ``stream`` (the weight-gradient side stream) current, so the
+    process group orders them after the weight-gradient GEMMs already queued there and they run
+    while the backward continues; the optimiser's stream waits for them in _finish_sync."""
+
+    def __init__(self, trainer, grad, buckets):
+        self.tr, self.grad, self.buckets, self.next = trainer, grad, buckets, 0
+        self.launched = []           # (start, end) ranges, in launch order (tests)
+
+    def __call__(self, ordinal, stream):
+        while self.next < len(self.buckets) and (ordinal is None or self.buckets[self.next][0] <= ordinal):
+            ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+            with ctx:
+                for a, b in self.buckets[self.next][1]:
+                    self.tr._pending.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM,
+                                                            group=self.tr.pg, async_op=True))
+                    self.launched.append((a, b))
+            self.next += 1

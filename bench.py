@@ -177,41 +177,65 @@ def selector_symbol(sel):
 def pmc_traffic(config, sel):
     """Per-launch HBM-side bytes of the dominant kernel from the committed PMC passes
     (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command)."""
-    path = os.path.join(REPO, "profiles", "r1", "pmc", f"traffic_{config}.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None, None
-    if d.get("kernel") != selector_symbol(sel) or not d.get("traffic_bytes_per_launch"):
-        return None, None
-    return float(d["traffic_bytes_per_launch"]), os.path.relpath(path, REPO)
+    for rnd in ("r2", "r1"):   # newest committed pass first
+        path = os.path.join(REPO, "profiles", rnd, "pmc", f"traffic_{config}.json")
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == selector_symbol(sel) and d.get("traffic_bytes_per_launch"):
+            return float(d["traffic_bytes_per_launch"]), os.path.relpath(path, REPO)
+    return None, None
 
 
 def cpu_baseline(threads):
-    """The oracle's single-level step at batch 1, 1024x512, fp32 on `threads` host cores."""
+    """The oracle's step on `threads` host cores, fp32, batch 1 (SURVEY §8(d) CPU reference):
+
+    * c2 shape (single-level Vanilla, 1024x512 source and target): 1 warm-up + 2 timed steps,
+      `value` = images/s of the timed steps;
+    * c3 shape (multi-level Vanilla, source 1280x720, target 1024x512, D1 + D2): 1 warm-up +
+      1 timed step, reported as `c3_step_s`;
+    * BASELINE config c1 (forward + CrossEntropy2d, 1x3x321x321): 1 warm-up + 1 timed.
+    The warm-up keeps oneDNN primitive creation out of the timed steps.
+    """
     from oracle import reference_torch as R
     torch.set_num_threads(threads)
-    G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
-    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
-    cfg = dict(level="single-level", gan="Vanilla", input_size=(1024, 512), input_size_target=(1024, 512))
-    opts = R.make_optimizers(G, None, D2, R.DEFAULT_CFG | cfg)
-    xs = torch.from_numpy(R.det_images((1, 3, 512, 1024), 1)).float()
-    lab = torch.from_numpy(R.det_labels((1, 512, 1024), 2))
-    xt = torch.from_numpy(R.det_images((1, 3, 512, 1024), 3)).float()
-    t0 = time.perf_counter()
-    R.oracle_step(G, None, D2, opts, cfg, 0, [(xs, lab, xt)])
-    dt = time.perf_counter() - t0
-    # BASELINE config c1 (the reference's CPU-runnable case): forward + CrossEntropy2d, 1x3x321x321
+
+    def run(level, src, tgt, n_timed):
+        G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
+        d = lambda seed: R.to_torch(R.det_state(R.d_specs(), seed), dtype=torch.float32,
+                                    trainable=lambda k: True)
+        D1 = d(2001) if level == "multi-level" else None
+        D2 = d(2002)
+        cfg = dict(level=level, gan="Vanilla", input_size=src, input_size_target=tgt)
+        opts = R.make_optimizers(G, D1, D2, R.DEFAULT_CFG | cfg)
+        xs = torch.from_numpy(R.det_images((1, 3, src[1], src[0]), 1)).float()
+        lab = torch.from_numpy(R.det_labels((1, src[1], src[0]), 2))
+        xt = torch.from_numpy(R.det_images((1, 3, tgt[1], tgt[0]), 3)).float()
+        R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)])          # warm-up
+        t0 = time.perf_counter()
+        for it in range(n_timed):
+            R.oracle_step(G, D1, D2, opts, cfg, 1 + it, [(xs, lab, xt)])
+        return (time.perf_counter() - t0) / n_timed, G
+
+    c2_s, G = run("single-level", (1024, 512), (1024, 512), 2)
+    c3_s, _ = run("multi-level", (1280, 720), (1024, 512), 1)
     x1 = torch.from_numpy(R.det_images((1, 3, 321, 321), 5)).float()
     l1 = torch.from_numpy(R.det_labels((1, 321, 321), 6))
-    t1 = time.perf_counter()
+    times = []
     with torch.no_grad():
-        R.cross_entropy2d(R.g_forward(G, x1, (321, 321), train=True)[1], l1)
-    c1 = time.perf_counter() - t1
-    return {"value": 1.0 / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": "1 single-level adversarial step (oracle/reference_torch.py, stock PyTorch "
-                      f"CPU fp32), batch 1, source+target 1024x512; {dt:.2f} s",
-            "c1_forward_ce_s": c1,
+        for _ in range(2):
+            t1 = time.perf_counter()
+            R.cross_entropy2d(R.g_forward(G, x1, (321, 321), train=True)[1], l1)
+            times.append(time.perf_counter() - t1)
+    return {"value": 1.0 / c2_s, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "oracle/reference_torch.py step (stock PyTorch CPU fp32), batch 1: c2 shape "
+                      f"single-level 1024x512, 1 warm-up + 2 timed, {c2_s:.2f} s/step",
+            "c3_step_s": c3_s,
+            "c3_sample": "multi-level Vanilla, source 1280x720 + target 1024x512, batch 1, "
+                         "1 warm-up + 1 timed",
+            "c3_images_per_s": 1.0 / c3_s,
+            "c1_forward_ce_s": times[-1],
             "calibration": "the port times within +6 % (step) / -12 % (c1) of the reference's own "
                            "modules on the same cores (profiles/r1/cpu_calibration.json)"}
 

@@ -322,7 +322,8 @@ int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream)
 /* selector = 100*op + 10*tile + variant names ONE kernel symbol: op 0 fwd, 1 bwd-data,     */
 /* 2 bwd-weight; tile 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256, 4 = 256x64;          */
 /* variant 0..3 = generic gather (2*vecA + vecB), 4 = FAST, 5 = FAST stride-2 parity path;    */
-/* tile 9 = the bf16-MFMA kernel (128x128x64), variant 0 / 1 (stride-2 parity path).         */
+/* tile 9 = the bf16-MFMA kernels: variant 0 / 1 bf16 operands (stride-2 parity path),      */
+/* 2 / 3 the same on the 128x256 tile, 5 / 6 the F32X3 kernel (3-term bf16 splits).          */
 /* ------------------------------------------------------------------------------------ */
 int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
@@ -330,7 +331,8 @@ int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launche
    fwd (id 1000) / bwd (1001), softmax fwd (1002) / bwd (1003), cross-entropy fwd (1004) / bwd
    (1005), BN apply (1006) / backward apply (1007), the warper's up2_relu_cat fwd (1008) / bwd
    (1009), grid warp fwd (1010) / field gradient (1011) / input-gradient scatter (1012, all of its
-   passes) is bracketed the same way with its
+   passes), BN statistics reduce (1013) / backward-sums reduce (1014) and the conv split-K
+   reduce (1015) is bracketed the same way with its
    ALGORITHMIC bytes (compulsory reads + writes at the op interface) as units. */
 int adaptseg_timing_enable_mem(int enable);
 int adaptseg_timing_read_id(int kernel_id, double *total_ms, double *total_units, int64_t *launches);

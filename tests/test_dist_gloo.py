@@ -125,3 +125,79 @@ def test_sgd_grad_scale_folds_the_average():
     # restatement of adaptseg_sgd_step (first step, multiplicity 1) with grad_scale
     d = g_sum * (1.0 / world) + 5e-4 * p0
     assert torch.allclose(ref.detach(), p0 - 0.1 * d, rtol=1e-12)
+
+
+# ---------------------------------------------------------------------------------------
+# Bucketed generator all-reduce (train._BucketAllReduce + DeeplabMulti._grad_buckets)
+# ---------------------------------------------------------------------------------------
+
+def _cpu_deeplab():
+    from adaptsegnet_amd.model import DeeplabMulti
+    m = DeeplabMulti(num_classes=19)
+    m._ensure_arena(torch.device("cpu"))
+    return m
+
+
+@pytest.mark.parametrize("mb", [8, 32, 1000])
+def test_grad_buckets_tile_the_arena_in_backward_order(mb):
+    m = _cpu_deeplab()
+    A = m._arena
+    buckets = m._grad_buckets(mb * 2 ** 20)
+    units = m._bwd_units()
+    ords = [o for o, _ in buckets]
+    assert ords == sorted(ords) and ords[-1] == len(units) - 1
+    cover = torch.zeros(A.numel, dtype=torch.int32)
+    for _, runs in buckets:
+        for a, b in runs:
+            assert 0 <= a < b <= A.numel
+            cover[a:b] += 1
+    assert bool((cover == 1).all()), "every arena element in exactly one bucket"
+    # the first bucket holds the heads: layer6 and layer4 finish first in backward
+    first = {A.params[i] for i in range(len(A.params))
+             if any(a <= A.offsets[i] < b for a, b in buckets[0][1])}
+    assert all(p in first for p in m.layer6.parameters())
+    if mb == 1000:
+        assert len(buckets) == 1
+    else:
+        sizes = [4 * sum(b - a for a, b in runs) for _, runs in buckets]
+        assert all(s >= mb * 2 ** 20 for s in sizes[:-1])
+        assert len(buckets) >= 2 and all(s < 3 * mb * 2 ** 20 + 24 * 2 ** 20 for s in sizes)
+
+
+def _bucket_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from adaptsegnet_amd.train import _BucketAllReduce
+        m = _cpu_deeplab()
+        g = torch.Generator().manual_seed(7 + rank)
+        grad = torch.randn(m._arena.numel, generator=g, dtype=torch.float32)
+        orig = grad.clone()
+        tr = type("T", (), {})()
+        tr._pending, tr.pg = [], None
+        hook = _BucketAllReduce(tr, grad, m._grad_buckets(16 * 2 ** 20))
+        # the single-level backward skips layer5 (ordinal len(layer4) + 1) and the stem unit
+        skip = {len(m.layer4) + 1, len(m._bwd_units()) - 1}
+        for o in range(len(m._bwd_units())):
+            if o not in skip:
+                hook(o, None)
+        hook(None, None)
+        for w in tr._pending:
+            w.wait()
+        out[rank] = (orig, grad.clone(), list(hook.launched))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_sums_every_element_once():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, port, out), nprocs=world, join=True)
+    total = out[0][0] + out[1][0]
+    for r in range(world):
+        assert torch.allclose(out[r][1], total, rtol=1e-6, atol=1e-6)
+    assert torch.equal(out[0][1], out[1][1])
+    launched = out[0][2]
+    assert len(launched) > 3 and launched == out[1][2]

@@ -17,6 +17,7 @@ if [ "$SEL" != "none" ]; then
   tail -3 gpurun_out/pytest_$TAG.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi   # 1 = test failures: still bench
 fi
+[ "$CFGS" = "none" ] && exit 0
 for cfg in $CFGS; do
   timeout -k 10 400 python -u bench.py --config "$cfg" --steps 10 --warmup 3 --no-cpu-baseline \
     > gpurun_out/bench_${cfg}_$TAG.json 2> gpurun_out/bench_${cfg}_$TAG.err || exit 4
