@@ -28,15 +28,12 @@ __device__ __forceinline__ float4 relu_mask_from_x(float4 g, float4 v, float4 m,
 }
 
 // Activation-derivative mask of the backward (rmode): 0 none; 1 ReLU, sign from the saved output
-// y; 2 ReLU, sign recomputed from x; 3 LeakyReLU(0.2), sign from y; 4 LeakyReLU(0.2), sign from
-// x.  LeakyReLU keeps the sign, so its output is as good a mask source as ReLU's.
-__device__ __forceinline__ float4 act_mask(float4 g, int rmode, const float *y, int64_t e, float4 v, float4 m,
-                                           float4 is, float4 w, float4 b) {
-  if (rmode == 0) return g;
-  float4 o;
-  if (rmode == 1 || rmode == 3) {
-    o = *reinterpret_cast<const float4 *>(y + e);
-  } else {
+// y (`o`, loaded by the caller); 2 ReLU, sign recomputed from x; 3 LeakyReLU(0.2), sign from y;
+// 4 LeakyReLU(0.2), sign from x.  LeakyReLU keeps the sign, so its output is as good a mask
+// source as ReLU's.
+__device__ __forceinline__ float4 act_mask_o(float4 g, int rmode, float4 o, float4 v, float4 m, float4 is,
+                                             float4 w, float4 b) {
+  if (rmode == 2 || rmode == 4) {
     o.x = bn_affine(v.x, m.x, is.x, w.x, b.x);
     o.y = bn_affine(v.y, m.y, is.y, w.y, b.y);
     o.z = bn_affine(v.z, m.z, is.z, w.z, b.z);
@@ -49,6 +46,11 @@ __device__ __forceinline__ float4 act_mask(float4 g, int rmode, const float *y, 
   g.w = o.w > 0.f ? g.w : k * g.w;
   return g;
 }
+
+constexpr int kReduceUnroll = 4;
+// ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
+// GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
+constexpr int kReduceBlocks = 512, kApplyBlocks = 512;
 
 // Forward activation: 0 none, 1 ReLU, 2 LeakyReLU(0.2) (model/custom_layers.py:83-96).
 __device__ __forceinline__ float fwd_act(float v, int act) {
@@ -83,18 +85,36 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
       ww = w ? *reinterpret_cast<const float4 *>(w + c0) : make_float4(1, 1, 1, 1);
       bb = b ? *reinterpret_cast<const float4 *>(b + c0) : make_float4(0, 0, 0, 0);
     }
-    for (int64_t r = r0 + rl; r < r1; r += tr) {
-      float4 v = *reinterpret_cast<const float4 *>(x + r * C + c0);
-      float4 d = make_float4(v.x - piv.x, v.y - piv.y, v.z - piv.z, v.w - piv.w);
-      if (MODE == 0) {
-        s1.x += d.x; s1.y += d.y; s1.z += d.z; s1.w += d.w;
-        s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
-      } else {
-        float4 g = *reinterpret_cast<const float4 *>(dy + r * C + c0);
-        if (relu == 2) g = relu_mask_from_x(g, v, piv, is, ww, bb);
-        else if (relu) g = act_mask(g, relu, y, r * C + c0, v, piv, is, ww, bb);
-        s1.x += g.x; s1.y += g.y; s1.z += g.z; s1.w += g.w;
-        s2.x += g.x * d.x; s2.y += g.y * d.y; s2.z += g.z * d.z; s2.w += g.w * d.w;
+    // rows unrolled x kReduceUnroll with every load issued before any use (memory-level
+    // parallelism: one float4 per tensor in flight per thread measured 3-4 TB/s); tail rows
+    // re-read row r and are masked out of the sums
+    constexpr int U = kReduceUnroll;
+    for (int64_t r = r0 + rl; r < r1; r += U * tr) {
+      float4 v[U], g[U], o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + (int64_t)u * tr;
+        const int64_t e = (ru < r1 ? ru : r) * C + c0;
+        v[u] = *reinterpret_cast<const float4 *>(x + e);
+        if (MODE == 1) {
+          g[u] = *reinterpret_cast<const float4 *>(dy + e);
+          if (relu == 1 || relu == 3) o[u] = *reinterpret_cast<const float4 *>(y + e);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + (int64_t)u * tr >= r1) break;
+        const float4 d = make_float4(v[u].x - piv.x, v[u].y - piv.y, v[u].z - piv.z, v[u].w - piv.w);
+        if (MODE == 0) {
+          s1.x += d.x; s1.y += d.y; s1.z += d.z; s1.w += d.w;
+          s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
+        } else {
+          float4 gg = g[u];
+          if (relu == 2) gg = relu_mask_from_x(gg, v[u], piv, is, ww, bb);
+          else if (relu) gg = act_mask_o(gg, relu, o[u], v[u], piv, is, ww, bb);
+          s1.x += gg.x; s1.y += gg.y; s1.z += gg.z; s1.w += gg.w;
+          s2.x += gg.x * d.x; s2.y += gg.y * d.y; s2.z += gg.z * d.z; s2.w += gg.w * d.w;
+        }
       }
     }
   }
@@ -370,7 +390,7 @@ static ApplyPlan apply_plan(int64_t rows, int C) {
   const int tr = 256 / a.tc;
   // ~2 blocks per CU: the apply passes run beside the weight-gradient GEMMs; 512 blocks measured
   // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (two runs each)
-  const int want = std::max(1, 512 / a.cblocks);
+  const int want = std::max(1, kApplyBlocks / a.cblocks);
   const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * kApplyUnroll));
   a.rsplits = (int)std::min<int64_t>(want, maxs);
   a.per = ceil_div(rows, a.rsplits);
@@ -392,7 +412,7 @@ static ReducePlan reduce_plan(int64_t rows, int C) {
   r.cblocks = (int)ceil_div(C, 4 * r.tc);
   // 512 blocks: 256 / 1024 measured -2 % / -4.5 % at c2 — the reduction shares the chip with
   // the weight-gradient GEMMs, more blocks take CUs from them
-  int want = std::max(1, 512 / r.cblocks);
+  int want = std::max(1, kReduceBlocks / r.cblocks);
   int tr = 256 / r.tc;
   int64_t max_splits = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * 8));
   r.splits = (int)std::min<int64_t>(want, max_splits);
