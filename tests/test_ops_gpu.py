@@ -637,3 +637,35 @@ def test_f32x3_accuracy_matches_fp32_mfma(op):
             errs[math] = rel(out, ref)
         print(f"op {op} K={cin * ks * ks}: max rel err f32 {errs['f32']:.3e}  f32x3 {errs['f32x3']:.3e}")
         assert errs["f32x3"] <= 1.5 * errs["f32"] + 1e-7, errs
+
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_f32x3_is_unbiased(op):
+    """The bf16 MFMA's internal sum does not round to nearest: addends far below the largest one
+    lose their low bits (a downward bias, tools/dbg/mfma_round.hip).  With the five cross terms
+    in the same accumulator as a0*b0 that bias piled up to a mean signed error of -1.1e-8 x
+    max|y| on this conv (positive data; fp32 MFMA: +-1e-10); conv_x3.hpp keeps them in their own
+    accumulator.  Guard: |mean signed error| <= 1e-9 x max|ref| on all-positive operands, the
+    worst case for a one-signed rounding bias."""
+    k = K()
+    g = torch.Generator().manual_seed(1)
+    n, cin, h, w, cout = 2, 256, 32, 48, 256
+    geom = k.ConvGeom(cin, cout, 3, 3, 1, (1,), (1,))
+    x = torch.rand(n, cin, h, w, generator=g, dtype=torch.float64).float().double()
+    wt = (torch.rand(cout, cin, 3, 3, generator=g, dtype=torch.float64) / 2304).float().double()
+    gy = torch.rand(n, cout, h, w, generator=g, dtype=torch.float64).float().double()
+    assert k.get_conv_math() == k.MATH_F32X3
+    if op == 0:
+        ref = F.conv2d(x, wt, None, 1, 1)
+        out = nchw(k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)]))
+    elif op == 1:
+        ref = torch.nn.grad.conv2d_input(x.shape, wt, gy, 1, 1)
+        out = nchw(k.conv_dgrad(geom, nhwc(gy), n, h, w, [w_cl(wt)]))
+    else:
+        ref = torch.nn.grad.conv2d_weight(x, wt.shape, gy, 1, 1)
+        dw = torch.zeros(cout, 3, 3, cin, device=DEV)
+        k.conv_wgrad(geom, nhwc(gy), nhwc(x), n, h, w, [dw], accumulate=False)
+        out = dw.permute(0, 3, 1, 2).double().cpu()
+    bias = float(((out - ref) / ref.abs().max()).mean())
+    print(f"op {op}: mean signed error {bias:+.2e} x max|ref|")
+    assert abs(bias) <= 1e-9, bias
