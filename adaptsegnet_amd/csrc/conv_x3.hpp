@@ -294,6 +294,11 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
 #pragma unroll
       for (int r = 0; r < 16; ++r) accs[i][j][r] = 0.f;
 
+  // Wave priority: FWD / DGRAD raise it over their MFMAs (the waves holding MFMA work issue
+  // first); WGRAD, whose staging splits both operands (twice the vector work), raises it over
+  // the split + LDS stores instead, so a staging wave is not starved behind the other wave's
+  // MFMAs (measured: FWD 152.5 vs 148.6 TF/s with the WGRAD choice, WGRAD 142.0 vs 131.8 with
+  // the FWD one, tools/dbg/ab_libs.sh).
   int cur = 0;
   // One 16-deep K step from LDS buffer `cur`: the six split products of every 32x32 tile,
   // term-major so consecutive MFMAs write different accumulators.
@@ -312,7 +317,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
     }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
     constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!MC) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int u = 0; u < 6; ++u)
 #pragma unroll
@@ -322,7 +327,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
           if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
           else accs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[TA[u]][i], b[TB[u]][j], accs[i][j], 0, 0, 0);
         }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!MC) __builtin_amdgcn_s_setprio(0);
   };
 
   if (kt0 < kt1) {
@@ -333,7 +338,11 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
       const bool more = kt + 1 < kt1;
       if (more) load_tile(kt + 1);
       compute();
-      if (more) store_tile(cur ^ 1);
+      if (more) {
+        if constexpr (MC) __builtin_amdgcn_s_setprio(1);
+        store_tile(cur ^ 1);
+        if constexpr (MC) __builtin_amdgcn_s_setprio(0);
+      }
       __syncthreads();
       cur ^= 1;
     }
