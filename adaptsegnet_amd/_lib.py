@@ -85,6 +85,7 @@ _SIGS = {
     "adaptseg_adam_step": [_L, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _P],
     "adaptseg_zero": [_P, _SZ, _P],
     "adaptseg_to_nhwc": [_I, _I, _I, _I, ctypes.POINTER(_L), _P, _P, _P],
+    "adaptseg_to_nhwc_pad": [_I, _I, _I, _I, ctypes.POINTER(_L), _P, _I, _P, _I, _P],
     "adaptseg_axpy": [_L, _F, _P, _P, _I, _P],
     "adaptseg_add_i64": [_P, _L, _L, _P],
     "adaptseg_preprocess_workspace_size": [_I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],

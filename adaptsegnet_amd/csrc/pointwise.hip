@@ -572,17 +572,47 @@ struct Strides4 {
   int64_t s[4];
 };
 
-__global__ void to_nhwc_kernel(int n, int C, int H, int W, Strides4 st, const float *__restrict__ src,
+// dst[b][y][x][c] (Cd channels, Cd >= C) = c < C ? src(b, c, y, x) : 0, (+ dst with ACC)
+template <bool ACC>
+__global__ void to_nhwc_kernel(int n, int C, int Cd, int H, int W, Strides4 st, const float *__restrict__ src,
                                float *__restrict__ dst) {
-  const int64_t total = (int64_t)n * C * H * W;
+  const int64_t total = (int64_t)n * Cd * H * W;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    int c = (int)(i % C);
-    int64_t t = i / C;
+    int c = (int)(i % Cd);
+    int64_t t = i / Cd;
     int x = (int)(t % W); t /= W;
     int y = (int)(t % H);
     int b = (int)(t / H);
-    dst[i] = src[b * st.s[0] + c * st.s[1] + y * st.s[2] + x * st.s[3]];
+    const float v = c < C ? src[b * st.s[0] + c * st.s[1] + y * st.s[2] + x * st.s[3]] : 0.f;
+    dst[i] = ACC ? dst[i] + v : v;
+  }
+}
+
+// Same transform, c_dst % 4 == 0: a block row per (image, y), a thread per (x, 4 output channels)
+// (one float4 store, 32-bit index math) — the thin convs' input pads run on this one.
+template <bool ACC>
+__global__ void to_nhwc4_kernel(int C, int Cd, int H, int W, Strides4 st, const float *__restrict__ src,
+                                float *__restrict__ dst) {
+  const int Q = Cd >> 2;
+  const int row = blockIdx.y, b = row / H, y = row - b * H;
+  const int64_t base_row = (int64_t)b * st.s[0] + (int64_t)y * st.s[2];
+  float4 *drow = reinterpret_cast<float4 *>(dst) + (int64_t)row * W * Q;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < W * Q; t += gridDim.x * blockDim.x) {
+    const int x = t / Q, q = t - x * Q;
+    const float *sp = src + base_row + (int64_t)x * st.s[3];
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * q + j;
+      v[j] = c < C ? sp[(int64_t)c * st.s[1]] : 0.f;
+    }
+    float4 o = make_float4(v[0], v[1], v[2], v[3]);
+    if (ACC) {
+      const float4 d = drow[t];
+      o.x += d.x; o.y += d.y; o.z += d.z; o.w += d.w;
+    }
+    drow[t] = o;
   }
 }
 
@@ -913,12 +943,26 @@ int adaptseg_zero(void *ptr, size_t bytes, adaptseg_stream_t stream) {
 
 int adaptseg_to_nhwc(int n, int c, int h, int w, const int64_t *src_stride, const float *src, float *dst,
                      adaptseg_stream_t stream) {
-  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && src_stride && src && dst, "to_nhwc: bad args");
+  return adaptseg_to_nhwc_pad(n, c, h, w, src_stride, src, c, dst, 0, stream);
+}
+
+int adaptseg_to_nhwc_pad(int n, int c, int h, int w, const int64_t *src_stride, const float *src, int c_dst,
+                         float *dst, int flags, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && c_dst >= c && src_stride && src && dst,
+               "to_nhwc_pad: bad args (c %d, c_dst %d)", c, c_dst);
   Strides4 st;
   for (int i = 0; i < 4; ++i) st.s[i] = src_stride[i];
-  int64_t total = (int64_t)n * c * h * w;
-  to_nhwc_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, st, src, dst);
-  AS_CHECK_LAUNCH("to_nhwc");
+  const int64_t total = (int64_t)n * c_dst * h * w;
+  const bool acc = flags & ADAPTSEG_EPI_ACCUMULATE;
+  if (c_dst % 4 == 0 && ((uintptr_t)dst & 15) == 0 && (int64_t)n * h < 65536 && (int64_t)w * c_dst < (1 << 30)) {
+    const dim3 grid((unsigned)std::min<int64_t>(ceil_div((int64_t)w * (c_dst / 4), 256), 64), (unsigned)(n * h));
+    if (acc) to_nhwc4_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(c, c_dst, h, w, st, src, dst);
+    else to_nhwc4_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(c, c_dst, h, w, st, src, dst);
+  } else if (acc)
+    to_nhwc_kernel<true><<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, c_dst, h, w, st, src, dst);
+  else
+    to_nhwc_kernel<false><<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, c_dst, h, w, st, src, dst);
+  AS_CHECK_LAUNCH("to_nhwc_pad");
   return ADAPTSEG_OK;
 }
 

@@ -20,6 +20,8 @@ Reference semantics followed (file:line in /root/reference):
 """
 from __future__ import annotations
 
+import dataclasses
+
 
 import torch
 
@@ -149,6 +151,41 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
     """Weight gradient of one conv: on the side stream when ``ws`` is given."""
     def run():
         K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides)
+    if ws is None:
+        run()
+    else:
+        ws.launch(run, dy, x)
+
+
+# ---------------------------------------------------------------------------------------
+# Thin input convs (the stem's Cin 3, the discriminator's Cin 19): channel-padded operands
+# ---------------------------------------------------------------------------------------
+def _round_up(v, m):
+    return (v + m - 1) // m * m
+
+
+_PAD_THIN_CONVS = True   # the channel-padded thin-conv paths below (False: A/B reference only)
+
+
+def _wgrad_padded(ws, g, dy, x, n, h, w, dw, db=None):
+    """Weight gradient of a conv whose Cin is not a multiple of 4 (the stem's 3, D.conv1's 19,
+    DeeplabVGG conv1_1's 3): without float4 rows the implicit GEMM falls back to per-element
+    gathers (24-30 TF/s).  The NCHW-shaped input ``x`` (any strides) is copied to
+    c4 = round_up(Cin, 4) channels (zeros above Cin), the weight gradient runs on the vector /
+    F32X3 path into a padded temporary, and its first Cin channels are folded into ``dw``
+    (accumulate); ``db`` accumulates directly.  Measured per c2 step: stem 2 x 402 -> 247 µs,
+    D.conv1 2 x 701 -> 449 µs (pad copy included).  The forwards stay unpadded: padding
+    D.conv1's forward to Cin 32 ran slower (347 -> 533 µs: Cout 64 fills half of the F32X3
+    kernel's 128-wide column tile)."""
+    c4 = _round_up(g.cin, 4)
+    g4 = dataclasses.replace(g, cin=c4)
+
+    def run():
+        xp = K.to_nhwc_pad(x, c4)
+        dwp = K.zero_(torch.empty((g.cout, g.kh, g.kw, c4), device=dy.device, dtype=torch.float32))
+        K.conv_wgrad(g4, dy, xp, n, h, w, [dwp], [db] if db is not None else None,
+                     strides=K.nhwc_strides(n, h, w, c4))
+        K.to_nhwc_pad(dwp.permute(0, 3, 1, 2)[:, :g.cin], g.cin, out=dw.permute(0, 2, 3, 1), accumulate=True)
     if ws is None:
         run()
     else:
@@ -329,7 +366,10 @@ class _DeeplabMultiFn(torch.autograd.Function):
         bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0, mask_from_x=True)
         gs = model.conv1.geom()
         if need_w and model.conv1.weight.grad is not None:
-            _wgrad(ws, gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
+            if gs.cin % 4 and _PAD_THIN_CONVS:   # Cin 3: on a 4-channel padded copy of the input
+                _wgrad_padded(ws, gs, dy0, ctx.x, n, h, w, model.conv1.weight.grad)
+            else:
+                _wgrad(ws, gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
         done(None)
         dx = None
         if ctx.needs_input_grad[1]:
@@ -403,8 +443,11 @@ class _FCDiscriminatorFn(torch.autograd.Function):
             geo = conv.geom()
             ch, cw, cs = dims[i]
             if need_w and conv.weight.grad is not None:
-                _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
-                       strides=cs)
+                if geo.cin % 4 and _PAD_THIN_CONVS:   # D.conv1 (Cin 19): on a 20-channel padded copy
+                    _wgrad_padded(ws, geo, g, acts[i], n, ch, cw, conv.weight.grad, conv.bias.grad)
+                else:
+                    _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
+                           strides=cs)
             if i > 0:
                 # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
                 g = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i])
@@ -497,7 +540,10 @@ class _DeeplabVGGFn(torch.autograd.Function):
             geo = conv.geom()
             xin, ih, iw, cs, _ = acts[i]
             if need_w and conv.weight.grad is not None:
-                _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
+                if geo.cin % 4 and _PAD_THIN_CONVS:   # conv1_1 (Cin 3): on a 4-channel padded copy
+                    _wgrad_padded(ws, geo, g, xin, n, ih, iw, conv.weight.grad, conv.bias.grad)
+                else:
+                    _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
             if i > 0:
                 # grad of the previous conv's pre-activation.  xin is its post-ReLU output,
                 # or the 2x2 max of it: relu' at the routed (argmax) position = [max > 0].

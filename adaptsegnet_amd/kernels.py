@@ -362,6 +362,21 @@ def add_i64(t: torch.Tensor, v: int = 1):
     _OP.add_i64(t, int(v))
 
 
+def to_nhwc_pad(t: torch.Tensor, c_dst: int, out: torch.Tensor | None = None,
+                accumulate: bool = False) -> torch.Tensor:
+    """NCHW-shaped tensor [n, c, h, w] (any strides) -> NHWC buffer [n, h, w, c_dst], channels
+    c..c_dst-1 zero (out += with accumulate: the first c channels of a padded gradient fold
+    back into an unpadded one)."""
+    _require(t, "to_nhwc_pad")
+    n, c, h, w = t.shape
+    if out is None:
+        out = torch.empty((n, h, w, c_dst), device=t.device, dtype=torch.float32)
+    if tuple(out.shape) != (n, h, w, c_dst) or not out.is_contiguous() or c_dst < c:
+        raise RuntimeError(f"to_nhwc_pad: out must be a contiguous [{n}, {h}, {w}, {c_dst}] buffer, c_dst >= {c}")
+    _OP.to_nhwc_pad(t, out, bool(accumulate))
+    return out
+
+
 def nhwc_view(t: torch.Tensor) -> torch.Tensor:
     """NCHW-shaped tensor -> its NHWC buffer (no copy if channels_last-contiguous)."""
     if t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous():

@@ -414,6 +414,15 @@ def _to_nhwc(x, out):
     check(_lib.lib().adaptseg_to_nhwc(n, c, h, w, st, _p(x), _p(out), _stream()), "to_nhwc")
 
 
+@_op("to_nhwc_pad(Tensor x, Tensor(a!) out, bool accumulate) -> ()")
+def _to_nhwc_pad(x, out, accumulate):
+    """out [n, h, w, c_dst] (=|+=) x (NCHW-shaped, any strides), channels >= c zero."""
+    n, c, h, w = x.shape
+    st = (ctypes.c_int64 * 4)(*x.stride())
+    check(_lib.lib().adaptseg_to_nhwc_pad(n, c, h, w, st, _p(x), out.shape[-1], _p(out),
+                                          _lib.EPI_ACCUMULATE if accumulate else 0, _stream()), "to_nhwc_pad")
+
+
 @_op("axpy(float alpha, Tensor src, Tensor(a!) dst, bool accumulate) -> ()")
 def _axpy(alpha, src, dst, accumulate):
     check(_lib.lib().adaptseg_axpy(src.numel(), float(alpha), _p(src), _p(dst),

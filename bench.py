@@ -26,6 +26,7 @@ reference's own arithmetic) timed on this host for ONE single-level step at batc
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -62,9 +63,11 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
     from adaptsegnet_amd import engine
     inv = {}
 
-    def add(geom, n, h, w, op, strides=None, count=1):
+    def add(geom, n, h, w, op, strides=None, count=1, algo=None):
+        # geom: the geometry the engine launches; algo: the reference's (unpadded) one, whose
+        # FLOPs are counted
         kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides)
-        inv[kid] = inv.get(kid, 0.0) + count * geom.flops(n, h, w)
+        inv[kid] = inv.get(kid, 0.0) + count * (algo or geom).flops(n, h, w)
         if products is not None:
             products.add((op, kid, sp > 1))
 
@@ -76,7 +79,10 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
             add(g, batch, h, w, 0, st)
             if i > 0:
                 add(g, batch, h, w, 1)
-            add(g, batch, h, w, 2, st)
+            if g.cin % 4:   # conv1_1: weight gradient on the 4-channel padded input
+                add(dataclasses.replace(g, cin=4), batch, h, w, 2, (4 * h * w, 1, 4 * w, 4), algo=g)
+            else:
+                add(g, batch, h, w, 2, st)
             h, w = g.out_hw(h, w)
             if pool:
                 h, w = h // 2, w // 2
@@ -91,8 +97,8 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
         w, h = wh
         gs = model.conv1.geom()
         add(gs, batch, h, w, 0, (3 * h * w, h * w, w, 1))
-        if backward:
-            add(gs, batch, h, w, 2, (3 * h * w, h * w, w, 1))
+        if backward:   # weight gradient on the 4-channel padded input (engine._wgrad_padded)
+            add(dataclasses.replace(gs, cin=4), batch, h, w, 2, (4 * h * w, 1, 4 * w, 4), algo=gs)
         h, w = gs.out_hw(h, w)
         h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
         for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4), 1):
@@ -124,12 +130,17 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
         w, h = wh
         for i, conv in enumerate(D._convs()):
             g = conv.geom()
-            st = (19 * h * w, 1, w * 19, 19) if i == 0 else None
-            add(g, batch, h, w, 0, st)
-            if i > 0 or dgrad_input:
+            if i == 0:   # Cin 19; weight gradient on a 20-channel padded copy (engine._wgrad_padded)
+                add(g, batch, h, w, 0, (19 * h * w, 1, w * 19, 19))
+                if dgrad_input:
+                    add(g, batch, h, w, 1)
+                if wgrad:
+                    add(dataclasses.replace(g, cin=20), batch, h, w, 2, (20 * h * w, 1, w * 20, 20), algo=g)
+            else:
+                add(g, batch, h, w, 0)
                 add(g, batch, h, w, 1)
-            if wgrad:
-                add(g, batch, h, w, 2, st)
+                if wgrad:
+                    add(g, batch, h, w, 2)
             h, w = g.out_hw(h, w)
 
     heads = {"l6"} if level == "single-level" else {"l5", "l6"}
@@ -384,6 +395,11 @@ def main():
     }
     if not args.no_roofline and k_launches:
         avg_ms = k_ms / k_launches
+        # algorithmic FLOPs from the step inventory (unpadded geometries): the library's own
+        # count includes the zero channels of the channel-padded thin convs (D.conv1 runs
+        # Cin 19 as 32), which are not the reference's work
+        launched_flops = k_flops
+        k_flops = inv[dom] * args.steps
         ach = k_flops / (k_ms / 1e3) / 1e12
         traffic, tsrc = pmc_traffic(args.config, dom)
         out["roofline"] = {"bound": "mfma", "achieved": ach, "peak": peak,
@@ -393,6 +409,7 @@ def main():
                            "traffic_unit": "bytes/launch (L2 memory-side FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": tsrc,
                            "algorithmic_flop_per_launch": k_flops / k_launches,
+                           "launched_flop_per_launch": launched_flops / k_launches,
                            "kernel": selector_symbol(dom), "selector": dom,
                            "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,

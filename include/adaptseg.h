@@ -307,6 +307,13 @@ int adaptseg_zero(void *ptr, size_t bytes, adaptseg_stream_t stream);
 /* dst[n][h][w][c] = src(n, c, h, w) read through arbitrary element strides. */
 int adaptseg_to_nhwc(int n, int c, int h, int w, const int64_t *src_stride, const float *src,
                      float *dst, adaptseg_stream_t stream);
+/* to_nhwc with channel padding (c_dst >= c: channels c..c_dst-1 written as 0) and, with
+   ADAPTSEG_EPI_ACCUMULATE, dst += instead of dst =.  Pads a thin conv's input / weight to a
+   vector-friendly channel count (the stem's Cin 3 -> 4, D.conv1's Cin 19 -> 32) and folds a
+   padded weight gradient back into the unpadded one (src = its first c channels).  Stands in
+   for no reference call: the reference convs take the unpadded tensors directly. */
+int adaptseg_to_nhwc_pad(int n, int c, int h, int w, const int64_t *src_stride, const float *src, int c_dst,
+                         float *dst, int flags, adaptseg_stream_t stream);
 /* dst[i] += src[i] (or dst = src when flags lacks ADAPTSEG_EPI_ACCUMULATE). */
 int adaptseg_axpy(int64_t n, float alpha, const float *src, float *dst, int flags,
                   adaptseg_stream_t stream);

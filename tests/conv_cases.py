@@ -16,6 +16,8 @@ CONV_CASES = [
     (1, 256, 9, 12, 256, 3, 1, (4,), (4,), False),        # layer4 atrous d4
     (2, 3, 37, 45, 64, 7, 2, (3,), (1,), False),          # stem 7x7/2
     (2, 19, 32, 40, 64, 4, 2, (1,), (1,), True),          # D conv1 (Cin 19)
+    (2, 20, 32, 40, 64, 4, 2, (1,), (1,), True),          # D conv1 as run: weight gradient at Cin 20
+    (2, 4, 37, 45, 64, 7, 2, (3,), (1,), False),          # stem weight gradient on the Cin-4 padded input
     (2, 64, 16, 20, 128, 4, 2, (1,), (1,), True),         # D conv2
     (2, 128, 6, 8, 1, 4, 2, (1,), (1,), True),            # D classifier (Cout 1)
     (2, 64, 7, 9, 19, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24), True),  # ASPP, dil > spatial
@@ -35,6 +37,7 @@ CONV_CASES = [
     (2, 100, 13, 9, 48, 1, 1, (0,), (1,), False),         # ... ragged N (Cin 100), K = 48 (BK16 but not BK32)
     (1, 1024, 3, 5, 256, 1, 1, (0,), (1,), False),        # ... split-K (M = 15: one row tile)
     (2, 3, 40, 48, 64, 3, 1, (1,), (1,), True),           # DeeplabVGG conv1_1 (Cin 3: per-element wgrad B, 64x64 tile)
+    (2, 4, 40, 48, 64, 3, 1, (1,), (1,), True),           # DeeplabVGG conv1_1 weight gradient as run (Cin 4)
 ]
 
 # Large grids (>= 257 output tiles): forward and data gradient store straight from the

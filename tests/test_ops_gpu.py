@@ -669,3 +669,26 @@ def test_f32x3_is_unbiased(op):
     bias = float(((out - ref) / ref.abs().max()).mean())
     print(f"op {op}: mean signed error {bias:+.2e} x max|ref|")
     assert abs(bias) <= 1e-9, bias
+
+
+def test_to_nhwc_pad():
+    """adaptseg_to_nhwc_pad: strided NCHW source -> NHWC with zero channels, and the
+    accumulate form that folds a padded weight gradient back (engine._wgrad_padded)."""
+    k = K()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 19, 7, 9, generator=g)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)[:, :, :, :]
+    out = k.to_nhwc_pad(xd, 32)
+    ref = torch.zeros(2, 7, 9, 32)
+    ref[..., :19] = x.permute(0, 2, 3, 1)
+    assert torch.equal(out.cpu(), ref)
+    # fold: dst[..., :19] += src[..., :19] of a 20-channel buffer
+    src = torch.randn(64, 4, 4, 20, generator=g).to(DEV)
+    dst0 = torch.randn(64, 4, 4, 19, generator=g)
+    dst = dst0.to(DEV)
+    k.to_nhwc_pad(src.permute(0, 3, 1, 2)[:, :19], 19, out=dst, accumulate=True)
+    assert torch.allclose(dst.cpu(), dst0 + src.cpu()[..., :19], rtol=0, atol=1e-6)
+    # NCHW-contiguous 3-channel image -> 4 channels (the stem's weight-gradient input)
+    img = torch.randn(2, 3, 11, 13, generator=g)
+    p4 = k.to_nhwc_pad(img.to(DEV), 4).cpu()
+    assert torch.equal(p4[..., :3], img.permute(0, 2, 3, 1)) and not p4[..., 3].any()

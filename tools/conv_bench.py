@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import argparse
 import collections
+import dataclasses
 import os
 import sys
 
@@ -27,6 +28,8 @@ def shapes(batch, W=1024, H=512):
     out = collections.OrderedDict()
 
     def add(name, g, n, h, w, ops, count, st=None):
+        # thin input convs run channel-padded (engine._wgrad_padded / _FCDiscriminatorFn):
+        # timed as the engine runs them (pad copies included), FLOPs of the unpadded geometry
         key = (g, n, h, w, ops, st)
         if key in out:
             out[key][0] += count
@@ -100,12 +103,21 @@ def main():
         dy = torch.randn(n, oh, ow, g.cout, device=dev)
         dws = [torch.zeros_like(t) for t in ws]
         dbs = [torch.zeros_like(t) for t in bs] if has_bias else None
+        pad_wgrad = g.cin % 4 != 0                     # D.conv1 (Cin 20), stem (Cin 4)
+        xn = x.permute(0, 3, 1, 2) if x.dim() == 4 and x.shape[-1] == g.cin else x
         for op in ops:
             def run():
                 if op == 0:
                     K.conv_fwd(g, x, n, h, w, ws, bs, strides=st)
                 elif op == 1:
                     K.conv_dgrad(g, dy, n, h, w, ws)
+                elif pad_wgrad:
+                    c4 = (g.cin + 3) // 4 * 4
+                    xp = K.to_nhwc_pad(xn, c4)
+                    dwp = K.zero_(torch.empty(g.cout, g.kh, g.kw, c4, device=dev))
+                    K.conv_wgrad(dataclasses.replace(g, cin=c4), dy, xp, n, h, w, [dwp], dbs,
+                                 strides=K.nhwc_strides(n, h, w, c4))
+                    K.to_nhwc_pad(dwp.permute(0, 3, 1, 2)[:, :g.cin], g.cin, out=dws[0], accumulate=True)
                 else:
                     K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=st)
             run()
@@ -118,7 +130,11 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
             fl = g.flops(n, h, w)
-            sel, sp = K.conv_kernel_id(g, n, h, w, op, st)
+            if op == 2 and pad_wgrad:
+                c4 = (g.cin + 3) // 4 * 4
+                sel, sp = K.conv_kernel_id(dataclasses.replace(g, cin=c4), n, h, w, op, K.nhwc_strides(n, h, w, c4))
+            else:
+                sel, sp = K.conv_kernel_id(g, n, h, w, op, st)
             c = count[op] if isinstance(count, dict) else count
             tot_ms += ms * c
             tot_fl += fl * c
