@@ -323,7 +323,7 @@ void set_splits(Plan &pl) {
   if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
   const int bm = (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
-  const int bn = pl.bf16 ? pl.bf16_bn : pl.x3 ? 128 : kCfgBN[pl.cfg];
+  const int bn = pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
   pl.bk = pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);

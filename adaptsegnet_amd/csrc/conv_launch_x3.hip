@@ -4,15 +4,15 @@
 
 namespace adaptseg {
 
-// packed B operand: rows padded to whole 128-row tiles, three bf16 terms per weight
+// packed B operand: rows padded to whole column tiles (x3_bn), three bf16 terms per weight
 static void x3_pack_dims(const Plan &pl, int &rows_pad, int &ktot) {
   const ConvParams &p = pl.p;
   rows_pad = ktot = 0;
   if (pl.mode == MODE_FWD) {
-    rows_pad = (int)ceil_div(p.k, 128) * 128;
+    rows_pad = (int)ceil_div(p.k, x3_bn(MODE_FWD)) * x3_bn(MODE_FWD);
     ktot = p.nseg * p.kseg;
   } else if (pl.mode == MODE_DGRAD) {
-    rows_pad = (int)ceil_div(p.c, 128) * 128;
+    rows_pad = (int)ceil_div(p.c, x3_bn(MODE_DGRAD)) * x3_bn(MODE_DGRAD);
     ktot = p.ntaps * p.k;
   }
 }
@@ -33,7 +33,7 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
   else if (pl.mode == MODE_DGRAD) conv_wpack_x3_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, rows_pad, ktot);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(256);
+  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(x3_threads(pl.mode));
   if (pl.mode == MODE_FWD) igemm_x3_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, wb);
   else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, wb);
   else if (pl.mode == MODE_DGRAD) igemm_x3_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, wb);

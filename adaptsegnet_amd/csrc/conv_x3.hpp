@@ -34,9 +34,18 @@
 //   * K-contiguous images are 32-B rows (16 k) with the 16-B chunk XOR-swizzled by row bit 3
 //     (conflict-free ds_read_b128 fragments); M/N-contiguous images (weight gradient) are the
 //     bf16 kernel's 256-B k-rows read with ds_read_b64_tr_b16.
-// Block tile 128x128x16, 4 waves (2x2), each wave 64x64 = 2x2 MFMA tiles (x2 accumulators); 48 KB of LDS.
+// Block tile 128x128x16, 48 KB of LDS (two stages).  FWD / DGRAD: 8 waves (2x4) of 64x32 wave
+// tiles (2x1 MFMA tiles, x2 accumulators: 124-126 VGPRs, two blocks = 16 waves per CU), the
+// next K step's split and LDS stores interleaved with this step's MFMAs (T14 order: staged
+// registers hold step kt+1, reloaded with kt+2 right after the stores) — measured +4.4 % c2 /
+// +5.3 % c3 over 4 waves of 64x64 (staging after the MFMAs, which spilled at 256 VGPRs when
+// interleaved).  A / B decomposition on l3.conv2 (tools/dbg): dropping the global loads saves
+// 22 % of the time, dropping the split + stores with them the same — what is left is bound by
+// the gathered loads, not the MFMAs.  WGRAD: 4 waves (2x2) of 64x64, staging after the MFMAs
+// with raised priority (its M/N-contiguous images are 128 wide).
 #pragma once
 #include "conv_bf16.hpp"
+
 
 namespace adaptseg {
 
@@ -79,12 +88,16 @@ __device__ __forceinline__ void split3(float4 v, uint2 &hi, uint2 &mid, uint2 &l
 }
 
 template <int MODE, bool S2>
-__global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
-  constexpr int BM = 128, BN = 128, BK = kX3BK, NT = 256;
-  constexpr int WAVES_M = 2, WAVES_N = 2, TM = 2, TN = 2;
+__global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
   constexpr bool MC = MODE == MODE_WGRAD;   // both operands M/N-contiguous (k = output pixel)
-  constexpr int IMG = kX3Img;
-  constexpr int STAGE = 6 * IMG;            // A hi/mid/lo, B hi/mid/lo
+  constexpr int BM = 128, BN = 128, BK = kX3BK, NT = x3_threads(MODE);
+  constexpr int WAVES_M = 2, WAVES_N = NT / 128;        // 2x2 (WGRAD) or 2x4 waves
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;  // wave tile 64x64 / 64x32
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int IMG = kX3Img;               // A term image: 128 rows x 16 k bf16
+  constexpr int IMGB = BN * kX3BK * 2;      // B term image
+  constexpr int BPT = IMGB / NT;            // packed-B bytes per thread and term (16 or 8)
+  constexpr int STAGE = 3 * IMG + 3 * IMGB; // A hi/mid/lo, B hi/mid/lo
 
   __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
@@ -118,7 +131,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
   // ---- per-slot constants ----
   // K-contiguous A: slot i = row (tid>>2) + 64*i, float4 (tid&3) of its 16 k.
   // M/N-contiguous: slot q = tid + 256*i: k-row q>>5, columns 4*(q&31) .. +3.
-  constexpr int NQ = 2;
+  constexpr int NQ = MC ? 2 : 1;
   int a_pix[NQ], a_y[NQ], a_x[NQ];
   bool a_ok[NQ];
   int b_off[NQ], b_dy[NQ], b_dx[NQ];
@@ -167,12 +180,13 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
       b_off[i] = nn - tap * p.c;                   // input channel of the column
     }
   }
-  // packed B tiles of this column tile: [K step][term][4 KB]
-  const char *wtile = reinterpret_cast<const char *>(wb) + (size_t)tn * ktot / BK * 3 * IMG + 16 * tid;
+  // packed B tiles of this column tile: [K step][term][IMGB]
+  const char *wtile = reinterpret_cast<const char *>(wb) + (size_t)tn * ktot / BK * 3 * IMGB + BPT * tid;
+  typedef typename std::conditional<BPT == 16, u32x4, uint2>::type BChunk;
 
   float4 ra[NQ];           // A: one float4 per slot
   float4 rbf[MC ? NQ : 1]; // MC: B float4 per slot
-  u32x4 rbh[MC ? 1 : 3];   // K-contiguous B: this thread's 16 B of each packed term image
+  BChunk rbh[MC ? 1 : 3];  // K-contiguous B: this thread's BPT bytes of each packed term image
   bool ma[NQ], mb[NQ];
 
   auto load_tile = [&](int kt) {
@@ -191,7 +205,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
         ra[i] = ld4(p.x + (v ? a_pix[i] + soff : 0));
       }
 #pragma unroll
-      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const u32x4 *>(wtile + (size_t)(kt * 3 + s) * IMG);
+      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const BChunk *>(wtile + (size_t)(kt * 3 + s) * IMGB);
     } else if constexpr (MODE == MODE_DGRAD) {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
       const int co0 = kbase - tap * p.k;
@@ -218,7 +232,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
       }
       const int wkt = wk / BK;
 #pragma unroll
-      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const u32x4 *>(wtile + (size_t)(wkt * 3 + s) * IMG);
+      for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const BChunk *>(wtile + (size_t)(wkt * 3 + s) * IMGB);
     } else {  // WGRAD: k = output pixel
       const int krow0 = tid >> 5;
 #pragma unroll
@@ -255,7 +269,7 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
         *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
       }
 #pragma unroll
-      for (int s = 0; s < 3; ++s) *reinterpret_cast<u32x4 *>(Bs + s * IMG + 16 * tid) = rbh[s];
+      for (int s = 0; s < 3; ++s) *reinterpret_cast<BChunk *>(Bs + s * IMGB + BPT * tid) = rbh[s];
     } else {
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
@@ -269,8 +283,8 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
         *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
         split3(rbf[i], h, m, l);
         *reinterpret_cast<uint2 *>(Bs + o) = mb[i] ? h : z2;
-        *reinterpret_cast<uint2 *>(Bs + IMG + o) = mb[i] ? m : z2;
-        *reinterpret_cast<uint2 *>(Bs + 2 * IMG + o) = mb[i] ? l : z2;
+        *reinterpret_cast<uint2 *>(Bs + IMGB + o) = mb[i] ? m : z2;
+        *reinterpret_cast<uint2 *>(Bs + 2 * IMGB + o) = mb[i] ? l : z2;
       }
     }
   };
@@ -301,8 +315,11 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
   // the FWD one, tools/dbg/ab_libs.sh).
   int cur = 0;
   // One 16-deep K step from LDS buffer `cur`: the six split products of every 32x32 tile,
-  // term-major so consecutive MFMAs write different accumulators.
-  auto compute = [&]() {
+  // term-major so consecutive MFMAs write different accumulators.  The K-contiguous kernels
+  // then split + store the NEXT step's staged registers into LDS buffer cur^1 in the same basic
+  // block, and the scheduler interleaves that vector / LDS work between the MFMAs (one MFMA,
+  // three VALU, one LDS store) instead of running it after them.
+  auto compute = [&](auto with_store) {
     const char *As = lds + cur * STAGE;
     const char *Bs = As + 3 * IMG;
     bf16x8 a[3][TM], b[3][TN];
@@ -310,10 +327,11 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
     for (int s = 0; s < 3; ++s) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        a[s][i] = MC ? mc_frag(As + s * IMG, wm * 64 + i * 32, 0, lane) : kc16_frag(As + s * IMG, wm * 64 + i * 32, lane);
+        a[s][i] = MC ? mc_frag(As + s * IMG, wm * WTM + i * 32, 0, lane) : kc16_frag(As + s * IMG, wm * WTM + i * 32, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        b[s][j] = MC ? mc_frag(Bs + s * IMG, wn * 64 + j * 32, 0, lane) : kc16_frag(Bs + s * IMG, wn * 64 + j * 32, lane);
+        b[s][j] = MC ? mc_frag(Bs + s * IMGB, wn * WTN + j * 32, 0, lane)
+                     : kc16_frag(Bs + s * IMGB, wn * WTN + j * 32, lane);
     }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
     constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
@@ -327,24 +345,49 @@ __global__ void __launch_bounds__(256, 2) igemm_x3_kernel(const ConvParams p, co
           if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
           else accs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[TA[u]][i], b[TB[u]][j], accs[i][j], 0, 0, 0);
         }
+    if constexpr (decltype(with_store)::value) {
+      store_tile(cur ^ 1);
+#pragma unroll
+      for (int q = 0; q < 6 * TM * TN; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // 3 VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // 1 LDS store
+      }
+    }
     if constexpr (!MC) __builtin_amdgcn_s_setprio(0);
   };
 
   if (kt0 < kt1) {
-    load_tile(kt0);
-    store_tile(0);
-    __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
-      compute();
-      if (more) {
-        if constexpr (MC) __builtin_amdgcn_s_setprio(1);
-        store_tile(cur ^ 1);
-        if constexpr (MC) __builtin_amdgcn_s_setprio(0);
-      }
+    if constexpr (!MC) {
+      // T14 order with unconditional staging (past the last step it re-reads step kt1-1 into
+      // the LDS buffer nobody reads again): registers hold step kt+1 while step kt computes
+      const int klast = kt1 - 1;
+      load_tile(kt0);
+      store_tile(0);
+      load_tile(min(kt0 + 1, klast));
       __syncthreads();
-      cur ^= 1;
+      for (int kt = kt0; kt < kt1; ++kt) {
+        compute(std::true_type{});
+        load_tile(min(kt + 2, klast));
+        __syncthreads();
+        cur ^= 1;
+      }
+    } else {
+      load_tile(kt0);
+      store_tile(0);
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) load_tile(kt + 1);
+        compute(std::false_type{});
+        if (more) {
+          if constexpr (MC) __builtin_amdgcn_s_setprio(1);
+          store_tile(cur ^ 1);
+          if constexpr (MC) __builtin_amdgcn_s_setprio(0);
+        }
+        __syncthreads();
+        cur ^= 1;
+      }
     }
   }
 
@@ -383,14 +426,15 @@ __global__ void conv_wpack_x3_kernel(const ConvParams p, char *out, int rows_pad
         v = seg_ptr(p, seg)[((size_t)co * p.taps_per_seg + t) * p.c + n];
       }
     }
-    const int r = n & 127, kk = k & (kX3BK - 1);
-    char *dst = out + ((size_t)(n >> 7) * nkt + (k >> 4)) * 3 * kX3Img + kc16_off(r, kk >> 3) + 2 * (kk & 7);
+    constexpr int TR = x3_bn(MODE), IMGB = TR * kX3BK * 2;   // the kernel's column tile
+    const int r = n % TR, kk = k & (kX3BK - 1);
+    char *dst = out + ((size_t)(n / TR) * nkt + (k >> 4)) * 3 * IMGB + kc16_off(r, kk >> 3) + 2 * (kk & 7);
     const __bf16 h = (__bf16)v;
     const float r1 = v - (float)h;
     const __bf16 m = (__bf16)r1;
     *reinterpret_cast<__bf16 *>(dst) = h;
-    *reinterpret_cast<__bf16 *>(dst + kX3Img) = m;
-    *reinterpret_cast<__bf16 *>(dst + 2 * kX3Img) = (__bf16)(r1 - (float)m);
+    *reinterpret_cast<__bf16 *>(dst + IMGB) = m;
+    *reinterpret_cast<__bf16 *>(dst + 2 * IMGB) = (__bf16)(r1 - (float)m);
   }
 }
 
