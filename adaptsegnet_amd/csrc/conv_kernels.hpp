@@ -35,7 +35,7 @@ constexpr int kX3BK = 16;
 // F32X3 kernel block: 128x128 tiles; 4 waves of 64x64 for the weight gradient, 8 waves of 64x32
 // for the K-contiguous products (FWD / DGRAD)
 constexpr int x3_bn(int mode) { return 128; }
-constexpr int x3_threads(int mode) { return mode == MODE_WGRAD ? 256 : 512; }  // K step of the F32X3 kernel (conv_x3.hpp)
+constexpr int x3_threads(int mode) { return 512; }  // K step of the F32X3 kernel (conv_x3.hpp)
 
 struct ConvParams {
   int M, N, K;                 // GEMM extents

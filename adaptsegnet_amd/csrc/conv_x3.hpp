@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
   // ---- per-slot constants ----
   // K-contiguous A: slot i = row (tid>>2) + 64*i, float4 (tid&3) of its 16 k.
   // M/N-contiguous: slot q = tid + 256*i: k-row q>>5, columns 4*(q&31) .. +3.
-  constexpr int NQ = MC ? 2 : 1;
+  constexpr int NQ = 1;
   int a_pix[NQ], a_y[NQ], a_x[NQ];
   bool a_ok[NQ];
   int b_off[NQ], b_dy[NQ], b_dx[NQ];
@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
     }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
     constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
-    if constexpr (!MC) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int u = 0; u < 6; ++u)
 #pragma unroll
@@ -354,11 +354,11 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // 1 LDS store
       }
     }
-    if constexpr (!MC) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   if (kt0 < kt1) {
-    if constexpr (!MC) {
+    if constexpr (true) {
       // T14 order with unconditional staging (past the last step it re-reads step kt1-1 into
       // the LDS buffer nobody reads again): registers hold step kt+1 while step kt computes
       const int klast = kt1 - 1;
