@@ -347,10 +347,16 @@ void set_splits(Plan &pl) {
   // count: ceil(512 / 36) = 15 splits puts 3 blocks on 28 CUs (0.2 units) where 14 puts at most
   // 2 on every CU (0.143) — round down.
   constexpr int kSplitTarget = 512;
-  const int split_below = pl.mode == MODE_WGRAD ? kSplitTarget : 257;
+  // F32X3 weight gradients (side stream) split to ~384 blocks (1.5 per CU), not 512: a full
+  // 2-per-CU grid of 16-wave blocks holds every CU for a whole split, and the main stream's
+  // short BN / split-K kernels then wait for CU slots.  384 measured c2 +2.4 %, c3 +2.6 %
+  // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2, tools/dbg/ab_bench_many.sh).
+  constexpr int kX3WgradTarget = 384;
+  const int target = (pl.mode == MODE_WGRAD && pl.x3) ? kX3WgradTarget : kSplitTarget;
+  const int split_below = pl.mode == MODE_WGRAD ? target : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, kSplitTarget / pl.tiles);
+    splits = std::max(1, target / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
