@@ -13,7 +13,10 @@
 //     ds_write_b128 stores); an M/N-contiguous operand (both WGRAD operands: k = output pixel)
 //     is [64 k][128 m] (256-B rows, chunk ch at ch ^ ((r&3)<<2 | (r>>2)&3)) read with the
 //     ds_read_b64_tr_b16 transpose, so neither operand is transposed through registers.
-// Block tile 128x128x64, 4 waves (2x2), each wave 64x64 = 2x2 MFMA tiles of 32x32x16.
+// Block tile 128x128x64.  FWD / DGRAD: 8 waves (2x4) of 64x32 wave tiles, 114-116 VGPRs (two
+// blocks per CU), the next K step's conversion + LDS stores interleaved with this step's MFMAs
+// in T14 order (+6 % on the c2-shape bf16 products over 4 waves of 64x64 with staging after
+// the MFMAs).  WGRAD: 4 waves (2x2) of 64x64.
 #pragma once
 #include "conv_kernels.hpp"
 #include <type_traits>
@@ -26,6 +29,9 @@ typedef float floatx4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int kB16BK = 64;
+// threads per block: 4 waves (2x2 of 64x64) for the weight gradient, 8 waves (2x4) for the
+// K-contiguous products
+constexpr int bf16_threads(int mode) { return mode == MODE_WGRAD ? 256 : 512; }
 
 // 128-B row (64 bf16 along k), 16-B chunk ch (8 k) of row r
 __device__ __forceinline__ int kc_off(int r, int ch) { return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4); }
@@ -65,10 +71,12 @@ __device__ __forceinline__ bf16x8 kc_frag(const char *img, int r0, int ks, int l
 // BN_ = 128 (4 waves, 2x2) or 256 (8 waves, 2x4; K-contiguous products only): the wider tile
 // halves the refetch of the gathered fp32 A operand, which bounds this kernel.
 template <int MODE, bool S2, int BN_ = 128>
-__global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
-  constexpr int BM = 128, BN = BN_, BK = kB16BK, NT = BN_ * 2;
-  constexpr int WAVES_M = 2, WAVES_N = BN_ / 64, TM = 2, TN = 2;
+__global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
   constexpr bool MC = MODE == MODE_WGRAD;      // both operands M/N-contiguous
+  constexpr int BM = 128, BN = BN_, BK = kB16BK, NT = bf16_threads(MODE);
+  constexpr int WAVES_M = 2, WAVES_N = NT / 128;  // 2x2 (WGRAD) or 2x4 waves
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(!MC || BN_ == 128, "weight-gradient images are 128 wide");
   constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;  // bytes per operand image (bf16)
   constexpr int STAGE = IMGA + IMGB;
@@ -190,7 +198,7 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
       const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
-        const bool v = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h && (unsigned)(a_x[i] + dx) < (unsigned)p.w;
+        const bool v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.h) & ((unsigned)(a_x[i] + dx) < (unsigned)p.w);
         ma[S][i] = v;
         const float *src = p.x + (v ? a_pix[i] + soff : 0);
         ra[S][2 * i] = ld4(src);
@@ -221,7 +229,7 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
       const int soff = uni(co0 - (dy * p.ow + dx) * p.k);
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
-        const bool v = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh && (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
+        const bool v = a_ok[i] & ((unsigned)(a_y[i] - dy) < (unsigned)p.oh) & ((unsigned)(a_x[i] - dx) < (unsigned)p.ow);
         ma[S][i] = v;
         const float *src = p.dy + (v ? a_pix[i] + soff : 0);
         ra[S][2 * i] = ld4(src);
@@ -297,17 +305,17 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
   using I1 = std::integral_constant<int, NSETS - 1>;
   int cur = 0;
   // MFMAs of one K step from LDS buffer `cur`
-  auto compute = [&]() {
+  auto compute = [&](auto with_store) {
     const char *As = lds + cur * STAGE;
     const char *Bs = As + IMGA;
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        a[slot][i] = MC ? mc_frag(As, wm * 64 + i * 32, ks, lane) : kc_frag(As, wm * 64 + i * 32, ks, lane);
+        a[slot][i] = MC ? mc_frag(As, wm * WTM + i * 32, ks, lane) : kc_frag(As, wm * WTM + i * 32, ks, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        b[slot][j] = MC ? mc_frag(Bs, wn * 64 + j * 32, ks, lane) : kc_frag(Bs, wn * 64 + j * 32, ks, lane);
+        b[slot][j] = MC ? mc_frag(Bs, wn * WTN + j * 32, ks, lane) : kc_frag(Bs, wn * WTN + j * 32, ks, lane);
     };
     read_frags(0, 0);
 #pragma unroll
@@ -321,6 +329,17 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
     }
+    if constexpr (decltype(with_store)::value) {
+      // the next K step's registers converted and stored into the other LDS buffer in the
+      // MFMAs' shadow (same basic block: the scheduler interleaves them)
+      store_tile(cur ^ 1, I0{});
+#pragma unroll
+      for (int q = 0; q < (BK / 16) * TM * TN; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // 4 VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // 1 LDS store
+      }
+    }
   };
   if (kt0 < kt1) {
     load_tile(kt0, I0{});
@@ -333,7 +352,7 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
         constexpr int H = decltype(held)::value;
         using Free = std::integral_constant<int, 1 - H>;
         if (kt + 2 < kt1) load_tile(kt + 2, Free{});
-        compute();
+        compute(std::false_type{});
         if (kt + 1 < kt1) store_tile(cur ^ 1, held);
         __syncthreads();
         cur ^= 1;
@@ -342,12 +361,25 @@ __global__ void __launch_bounds__(BN_ * 2) igemm_bf16_kernel(const ConvParams p,
         kstep(kt, I1{});
         if (kt + 1 < kt1) kstep(kt + 1, I0{});
       }
+    } else if constexpr (!MC) {
+      // K-contiguous products (8 waves): T14 order with unconditional staging — registers hold
+      // step kt+1 while step kt computes and stores them; past the last step the loads re-read
+      // step kt1-1 into the LDS buffer nobody reads again
+      const int klast = kt1 - 1;
+      load_tile(min(kt0 + 1, klast), I0{});
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; ++kt) {
+        compute(std::true_type{});
+        load_tile(min(kt + 2, klast), I0{});
+        __syncthreads();
+        cur ^= 1;
+      }
     } else {
       __syncthreads();
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
         if (more) load_tile(kt + 1, I0{});
-        compute();
+        compute(std::false_type{});
         if (more) store_tile(cur ^ 1, I0{});
         __syncthreads();
         cur ^= 1;

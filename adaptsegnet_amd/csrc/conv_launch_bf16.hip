@@ -57,7 +57,7 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;
-  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(w256 ? 512 : 256);
+  dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(bf16_threads(pl.mode));
   if (pl.mode == MODE_FWD) {
     if (w256) igemm_bf16_kernel<MODE_FWD, false, 256><<<grid, block, 0, s>>>(p, wb);
     else igemm_bf16_kernel<MODE_FWD, false, 128><<<grid, block, 0, s>>>(p, wb);
