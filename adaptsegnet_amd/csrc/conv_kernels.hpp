@@ -1296,10 +1296,12 @@ hipError_t launch_fwd(const Plan &pl, hipStream_t s);
 // bf16 conv math (adaptseg_conv_set_math): weight-pack bytes and launcher (conv_launch_bf16.hip)
 int conv_math();
 size_t bf16_wpack_bytes(const Plan &pl);
-hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s);
+hipError_t prep_bf16(Plan &pl, void *ws, hipStream_t s);   // the weight pack
+hipError_t launch_bf16(const Plan &pl, void *ws, hipStream_t s);
 // F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)
 size_t x3_wpack_bytes(const Plan &pl);
-hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s);
+hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s);    // the weight pack
+hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s);  // the GEMM
 hipError_t launch_dgrad(const Plan &pl, hipStream_t s);
 hipError_t launch_wgrad(const Plan &pl, hipStream_t s);
 

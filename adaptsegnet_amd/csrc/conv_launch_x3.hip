@@ -23,16 +23,19 @@ size_t x3_wpack_bytes(const Plan &pl) {
   return 3 * (size_t)rows_pad * ktot * sizeof(__bf16);
 }
 
-hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
+hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
-  __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
   int rows_pad, ktot;
   x3_pack_dims(pl, rows_pad, ktot);
   const unsigned pg = (unsigned)std::min<int64_t>(ceil_div((int64_t)rows_pad * ktot, 256), 8192);
   if (pl.mode == MODE_FWD) conv_wpack_x3_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)wpack, rows_pad, ktot);
   else if (pl.mode == MODE_DGRAD) conv_wpack_x3_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, rows_pad, ktot);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
+  const ConvParams &p = pl.p;
+  __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(x3_threads(pl.mode));
   if (pl.mode == MODE_FWD) igemm_x3_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, wb);
   else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, wb);
