@@ -1,0 +1,211 @@
+// bf16 implicit-GEMM convolution fed by LDS-DMA (global_load_lds_dwordx4) — the forward and
+// stride-1 data-gradient products of the bf16 conv math (config c5) whose operands are bf16 in
+// HBM: the activation operand is a bf16 NHWC copy (written once per call by bf16_copy_kernel,
+// conv_launch_bf16.hip), the weights the K-contiguous bf16 pack of conv_bf16.hpp.
+//
+// Why a second bf16 kernel: igemm_bf16_kernel gathers the fp32 activations into registers and
+// rounds them while staging.  Its PMC (profiles/r2/pmc/bf16_l3conv2_counters.txt): 163 VALU per
+// 16 MFMAs per wave and K step, 30 % of wave time waiting on loads, MFMA busy 0.25 — one K step
+// of prefetch (one register set; a second one does not fit) does not cover the gather latency,
+// and every step moves twice the bytes the MFMA consumes.  Here no operand passes through
+// registers: each K step is 6 LDS-DMA instructions per wave into a 3-deep LDS ring, two tiles
+// stay in flight across each barrier (counted vmcnt, raw s_barrier — a __syncthreads() would
+// drain them), and the loop body is ds_read + MFMA only.
+//
+// Tile BM x BN x 64 (128x256 or 256x128), 8 waves of 64x64 (2x2 MFMA tiles of 32x32x16), LDS
+// 3 x 48 KB (one block per CU).  The LDS images are conv_bf16.hpp's K-contiguous [row][64 k]
+// images with the 16-B chunk of row r at (ch ^ (r>>1 & 7)): an LDS-DMA instruction writes its
+// 64 lanes' 16 B linearly (8 whole 128-B rows), so the swizzle goes on the SOURCE address —
+// lane l of the instruction loads chunk (l&7) ^ (r>>1 & 7) of its row r.  Rows outside the
+// image (padding taps, m >= M, n >= N) load from a 16-B zero block instead.
+#pragma once
+#include "conv_bf16.hpp"
+
+namespace adaptseg {
+
+// 16 zero bytes: the source of every padded operand row
+__device__ __attribute__((aligned(16))) unsigned int g_bf16g_zero[4];
+
+// One LDS-DMA wave instruction: lane l's 16 source bytes land at LDS byte lds_dst + 16 l.  In
+// inline asm, not __builtin_amdgcn_global_load_lds: hipcc (ROCm 7.2) cannot tell the DMA's LDS
+// writes from the ring stages the ds_reads use and waits vmcnt(0) before the first ds_read of
+// every K step, draining the two steps in flight.  The kernel counts these loads itself
+// (s_waitcnt vmcnt(N) + raw s_barrier); M0 is written and restored in the same statement.
+__device__ __forceinline__ void glds16(const void *src, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_dst)
+               : "memory");
+}
+
+constexpr int kG16BK = 64;
+constexpr int kG16Stages = 3;
+constexpr int g16_stage_bytes(int bm, int bn) { return (bm + bn) * kG16BK * 2; }
+
+template <int MODE, int BM, int BN>
+__global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p, const __bf16 *__restrict__ ab,
+                                                             const __bf16 *__restrict__ wb) {
+  static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
+  constexpr int NT = 512, BK = kG16BK;
+  constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;  // 64x64 wave tiles
+  static_assert(WAVES_M * WAVES_N == 8, "8 waves");
+  constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2;
+  constexpr int NA = BM / 64, NB = BN / 64;             // LDS-DMA instructions per wave and K step
+  constexpr int IMGA = BM * BK * 2;
+  constexpr int STAGE = g16_stage_bytes(BM, BN);
+
+  __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int ntn = (p.N + BN - 1) / BN;
+  int tile, split;
+  xcd_tile_split(tile, split);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int bm = tm * BM, bn = tn * BN;
+  const SegRegs sr = seg_regs(p);
+
+  const int M = p.M, K = p.K;
+  const int nkt = (K + BK - 1) / BK;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
+  const int ktot = p.ntaps * (MODE == MODE_FWD ? p.c : p.k);  // packed weight row length
+  // bf16 copy of the activation operand: NHWC contiguous, channel count ca
+  const int ca = MODE == MODE_FWD ? p.c : p.k;
+
+  // ---- per-lane rows: instruction i of wave w covers image rows 64 i + 8 w .. +7 ----
+  const int rsub = wave * 8 + (lane >> 3);                 // row within a 64-row group
+  const int chs = ((lane & 7) ^ ((rsub >> 1) & 7)) * 8;    // source chunk (elements) of this lane
+  int a_pix[NA], a_y[NA], a_x[NA];
+  bool a_ok[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = bm + 64 * i + rsub;
+    a_ok[i] = m < M;
+    const int mm = min(m, M - 1);
+    if constexpr (MODE == MODE_FWD) {
+      uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
+      const int ow = mm - (int)t * p.ow;
+      uint32_t b = fdiv(t, p.fd_oh);
+      const int oh = (int)t - (int)b * p.oh;
+      a_y[i] = oh * p.stride;
+      a_x[i] = ow * p.stride;
+      a_pix[i] = (((int)b * p.h + a_y[i]) * p.w + a_x[i]) * ca + chs;
+    } else {
+      uint32_t t = fdiv((uint32_t)mm, p.fd_w);
+      const int iw = mm - (int)t * p.w;
+      uint32_t b = fdiv(t, p.fd_hw);
+      const int ih = (int)t - (int)b * p.h;
+      a_y[i] = ih;
+      a_x[i] = iw;
+      a_pix[i] = (((int)b * p.oh + ih) * p.ow + iw) * ca + chs;
+    }
+  }
+  int b_off[NB];
+  bool b_ok[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int n = bn + 64 * j + rsub;
+    b_ok[j] = n < p.N;
+    b_off[j] = min(n, p.N - 1) * ktot + chs;
+  }
+  const __bf16 *zero = reinterpret_cast<const __bf16 *>(g_bf16g_zero);
+
+  // LDS-DMA of K step kt into ring stage st: NA + NB instructions per wave
+  auto issue = [&](int kt, int st) {
+    const int kbase = kt * BK;
+    const uint32_t As = uni((int)((uint32_t)(uintptr_t)lds + st * STAGE + wave * 8 * 128));
+    const uint32_t Bs = As + IMGA;
+    int soff, wk, dy, dx;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_c));
+      int seg, t;
+      seg_geom(p, sr, tap, seg, t, dy, dx);
+      dy = uni(dy);
+      dx = uni(dx);
+      soff = uni((dy * p.w + dx) * ca + kbase - tap * p.c);
+      wk = kbase;
+    } else {
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
+      int seg, t;
+      seg_geom(p, sr, tap, seg, t, dy, dx);
+      dy = uni(-dy);   // the data gradient reads dY at (ih - dy, iw - dx)
+      dx = uni(-dx);
+      soff = uni((dy * p.ow + dx) * ca + kbase - tap * p.k);
+      wk = kbase;
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      bool v;
+      if constexpr (MODE == MODE_FWD)
+        v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.h) & ((unsigned)(a_x[i] + dx) < (unsigned)p.w);
+      else
+        v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.oh) & ((unsigned)(a_x[i] + dx) < (unsigned)p.ow);
+      glds16(v ? ab + a_pix[i] + soff : zero, As + i * 64 * 128);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) glds16(b_ok[j] ? wb + b_off[j] + wk : zero, Bs + j * 64 * 128);
+  };
+
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int st) {
+    const char *As = lds + st * STAGE;
+    const char *Bs = As + IMGA;
+    bf16x8 a[2][TM], b[2][TN];
+    auto read_frags = [&](int ks, int slot) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[slot][i] = kc_frag(As, wm * WTM + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[slot][j] = kc_frag(Bs, wn * WTN + j * 32, ks, lane);
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int cb = ks & 1;
+      if (ks + 1 < BK / 16) read_frags(ks + 1, cb ^ 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (kt0 < kt1) {
+    // Ring of 3 stages, two K steps in flight: step kt lives in stage (kt - kt0) % 3.  The loads
+    // past the last step re-read it into a stage nobody reads again, so every wave always has
+    // exactly NA + NB instructions per step outstanding and the counted wait stays constant.
+    const int klast = kt1 - 1;
+    issue(kt0, 0);
+    issue(min(kt0 + 1, klast), 1);
+    int st = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      // this wave's DMAs of step kt are done (step kt+1's NA + NB stay in flight) ...
+      static_assert(NA + NB == 6, "vmcnt below counts 6 instructions per step");
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      // ... and after the barrier every wave's are, and every wave has finished reading the
+      // stage that step kt+2 overwrites (step kt-1's)
+      __builtin_amdgcn_s_barrier();
+      const int st2 = st == 0 ? 2 : st - 1;  // (st + 2) % 3
+      issue(min(kt + 2, klast), st2);
+      compute(st);
+      st = st == 2 ? 0 : st + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the epilogue reuses the LDS
+  }
+
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, false>(p, acc, bm, bn, tm, tn, split, M, p.h, p.w, 0, 0,
+                                                         reinterpret_cast<float *>(lds));
+}
+
+}  // namespace adaptseg

@@ -320,10 +320,10 @@ double conv_flops(const adaptseg_conv_desc *d) {
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.g16 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
-  const int bm = (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
-  const int bn = pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
+  const int bm = pl.g16 ? pl.g16_bm : (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
+  const int bn = pl.g16 ? pl.g16_bn : pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
   pl.bk = pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
@@ -353,10 +353,11 @@ void set_splits(Plan &pl) {
   // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2, tools/dbg/ab_bench_many.sh).
   constexpr int kX3WgradTarget = 384;
   const int target = (pl.mode == MODE_WGRAD && pl.x3) ? kX3WgradTarget : kSplitTarget;
-  const int split_below = pl.mode == MODE_WGRAD ? target : 257;
+  // the LDS-DMA bf16 kernel runs one block per CU: split only grids under half the CUs
+  const int split_below = pl.mode == MODE_WGRAD ? target : pl.g16 ? 128 : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, target / pl.tiles);
+    splits = std::max(1, (pl.g16 ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -365,7 +366,7 @@ void set_splits(Plan &pl) {
   p.splits = splits;
   p.ktiles_per_split = per;
   pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
-  if (pl.bf16) pl.slab_bytes += (bf16_wpack_bytes(pl) + 255) / 256 * 256;
+  if (pl.bf16) pl.slab_bytes += bf16_pre_bytes(pl);
   if (pl.x3) pl.slab_bytes += (x3_wpack_bytes(pl) + 255) / 256 * 256;
 }
 
@@ -448,7 +449,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     pl.be = !(nhwc_in && d->c % 4 == 0);
   }
   // bf16 conv math: the vector FAST cases whose K tiles of 64 stay inside one tap
-  pl.bf16 = false;
+  pl.bf16 = pl.g16 = false;
   const bool bf16_math = conv_math() == ADAPTSEG_MATH_BF16 || conv_math() == ADAPTSEG_MATH_BF16_WIDE;
   if (bf16_math && pl.fast && !pl.ae && !pl.be) {
     if (op == ADAPTSEG_CONV_FWD) pl.bf16 = d->c % 64 == 0;
@@ -469,6 +470,13 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // (c5 27.6 vs 27.7 images/s, per-shape within +-5 %): only with ADAPTSEG_MATH_BF16_WIDE
     const bool w256 = conv_math() == ADAPTSEG_MATH_BF16_WIDE;
     pl.bf16_bn = (w256 && op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 256) ? 256 : 128;
+    // forward / stride-1 data gradients with N >= 128 on the LDS-DMA kernel (conv_bf16g.hpp):
+    // 128x256 tiles when N >= 256 (the activation operand is fetched once per tap), else 256x128
+    if (op != ADAPTSEG_CONV_BWD_WEIGHT && !pl.s2 && p.N >= 128) {
+      pl.g16 = true;
+      pl.g16_bm = p.N >= 256 ? 128 : 256;
+      pl.g16_bn = p.N >= 256 ? 256 : 128;
+    }
   }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
   if (pl.cfg == 8 && (!pl.fast || pl.ae || pl.be || pl.s2)) {
@@ -483,6 +491,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
+  if (pl.g16) return 100 * mode + (pl.g16_bn == 256 ? 97 : 98);
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)
@@ -502,7 +511,7 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   hipError_t e;
   int slot;
   if (pl.bf16 || pl.x3) {  // [bf16 weight pack(s)][slabs]
-    const size_t wb = ((pl.x3 ? x3_wpack_bytes(pl) : bf16_wpack_bytes(pl)) + 255) / 256 * 256;
+    const size_t wb = pl.x3 ? (x3_wpack_bytes(pl) + 255) / 256 * 256 : bf16_pre_bytes(pl);
     if (!ws || ws_bytes < pl.slab_bytes) {
       set_error("conv (%s): workspace %zu < required %zu", pl.x3 ? "f32x3" : "bf16", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
@@ -667,7 +676,8 @@ int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
   if (tapgemm_eligible(d)) return ADAPTSEG_OK;
-  if (pl.fast && pl.p.splits == 1) *ntiles = (int)ceil_div(pl.p.M, pl.bf16 ? 128 : kCfgBM[pl.cfg]);
+  if (pl.fast && pl.p.splits == 1)
+    *ntiles = (int)ceil_div(pl.p.M, pl.g16 ? pl.g16_bm : pl.bf16 ? 128 : kCfgBM[pl.cfg]);
   return ADAPTSEG_OK;
 }
 
@@ -694,7 +704,7 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
   p.out = y;
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
-    const int nt = (int)ceil_div(p.M, kCfgBM[pl.cfg]);
+    const int nt = (int)ceil_div(p.M, pl.g16 ? pl.g16_bm : kCfgBM[pl.cfg]);
     if ((size_t)(nt + 2 * (int64_t)p.N * nt) * sizeof(float) <= stats_bytes) {
       p.stats = stats;
       p.stats_ntiles = nt;

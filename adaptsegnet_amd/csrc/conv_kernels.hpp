@@ -1254,6 +1254,8 @@ struct Plan {
   bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
   bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
+  bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
+  int g16_bm, g16_bn;
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
   int mode;
@@ -1296,6 +1298,7 @@ hipError_t launch_fwd(const Plan &pl, hipStream_t s);
 // bf16 conv math (adaptseg_conv_set_math): weight-pack bytes and launcher (conv_launch_bf16.hip)
 int conv_math();
 size_t bf16_wpack_bytes(const Plan &pl);
+size_t bf16_pre_bytes(const Plan &pl);   // workspace ahead of the slabs: weight pack (+ activation copy)
 hipError_t prep_bf16(Plan &pl, void *ws, hipStream_t s);   // the weight pack
 hipError_t launch_bf16(const Plan &pl, void *ws, hipStream_t s);
 // F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)

@@ -1,5 +1,6 @@
 // Kernel instantiations and host launchers of the bf16-MFMA conv path (conv_bf16.hpp).
 #include "conv_bf16.hpp"
+#include "conv_bf16g.hpp"
 
 namespace adaptseg {
 
@@ -37,6 +38,34 @@ __global__ void __launch_bounds__(256) conv_wpack_dgrad_kernel(const ConvParams 
 }
 
 
+// fp32 NHWC activations (pixel strides sxn / sxh / sxw, unit channel stride) -> contiguous
+// NHWC bf16 (RNE), 8 channels per thread: the activation operand of the LDS-DMA kernel.
+__global__ void bf16_copy_kernel(const float *__restrict__ x, int n, int h, int w, int c8, int sxn, int sxh,
+                                 int sxw, uint4 *__restrict__ out) {
+  const int64_t total = (int64_t)n * h * w * c8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cq = (int)(i % c8);
+    const int64_t pix = i / c8;
+    const int xx = (int)(pix % w);
+    const int64_t t = pix / w;
+    const int yy = (int)(t % h), b = (int)(t / h);
+    const float *src = x + (int64_t)b * sxn + (int64_t)yy * sxh + (int64_t)xx * sxw + 8 * cq;
+    const uint2 lo = cvt4_bf16(ld4(src)), hi = cvt4_bf16(ld4(src + 4));
+    out[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+
+// elements of the LDS-DMA kernel's bf16 activation copy (FWD: x, DGRAD: dY)
+static size_t g16_act_elems(const Plan &pl) {
+  const ConvParams &p = pl.p;
+  if (!pl.g16) return 0;
+  return pl.mode == MODE_FWD ? (size_t)p.n * p.h * p.w * p.c : (size_t)p.n * p.oh * p.ow * p.k;
+}
+
+size_t bf16_pre_bytes(const Plan &pl) {
+  return (bf16_wpack_bytes(pl) + 255) / 256 * 256 + (g16_act_elems(pl) * sizeof(__bf16) + 255) / 256 * 256;
+}
+
 size_t bf16_wpack_bytes(const Plan &pl) {
   const ConvParams &p = pl.p;
   if (pl.mode == MODE_FWD) return (size_t)p.k * p.nseg * p.kseg * sizeof(__bf16);
@@ -55,12 +84,35 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
     dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
     conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
+  if (pl.g16) {  // the activation operand's bf16 copy, after the (256-B aligned) weight pack
+    uint4 *act = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(wpack) + (bf16_wpack_bytes(pl) + 255) / 256 * 256);
+    const int64_t n8 = (int64_t)g16_act_elems(pl) / 8;
+    const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192);
+    if (pl.mode == MODE_FWD)
+      bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.x, p.n, p.h, p.w, p.c / 8, p.sxn, p.sxh, p.sxw, act);
+    else
+      bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.dy, p.n, p.oh, p.ow, p.k / 8, p.oh * p.ow * p.k, p.ow * p.k,
+                                              p.k, act);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
+  if (pl.g16) {
+    const __bf16 *act = reinterpret_cast<const __bf16 *>(reinterpret_cast<const char *>(wpack) +
+                                                         (bf16_wpack_bytes(pl) + 255) / 256 * 256);
+    dim3 grid(pl.tiles, p.splits), block(512);
+    if (pl.mode == MODE_FWD) {
+      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_FWD, 128, 256><<<grid, block, 0, s>>>(p, act, wb);
+      else igemm_bf16g_kernel<MODE_FWD, 256, 128><<<grid, block, 0, s>>>(p, act, wb);
+    } else {
+      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_DGRAD, 128, 256><<<grid, block, 0, s>>>(p, act, wb);
+      else igemm_bf16g_kernel<MODE_DGRAD, 256, 128><<<grid, block, 0, s>>>(p, act, wb);
+    }
+    return hipGetLastError();
+  }
   const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(bf16_threads(pl.mode));
   if (pl.mode == MODE_FWD) {
