@@ -39,21 +39,36 @@ __device__ __forceinline__ void glds16(const void *src, uint32_t lds_dst) {
                : "memory");
 }
 
-constexpr int kG16BK = 64;
 constexpr int kG16Stages = 3;
-constexpr int g16_stage_bytes(int bm, int bn) { return (bm + bn) * kG16BK * 2; }
+constexpr int g16_stage_bytes(int bm, int bn, int bk) { return (bm + bn) * bk * 2; }
 
-template <int MODE, int BM, int BN>
-__global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p, const __bf16 *__restrict__ ab,
-                                                             const __bf16 *__restrict__ wb) {
+// Byte offset of 16-B chunk ch of row r in a K-contiguous image of BK bf16 per row.  BK 64:
+// conv_bf16.hpp's kc_off (128-B rows, ch ^ (r>>1 & 7)); BK 32: 64-B rows, ch ^ (r>>2 & 3) —
+// conflict-free for the ds_read_b128 lane groups of the 32x32x16 fragment reads.
+template <int BK>
+__device__ __forceinline__ int g16_off(int r, int ch) {
+  if constexpr (BK == 64) return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4);
+  else return r * 64 + ((ch ^ ((r >> 2) & 3)) << 4);
+}
+
+// BK 64: one block per CU (3 x 48 KB ring); BK 32: two (3 x 24 KB), so one block's epilogue and
+// prologue overlap the other's K loop (short-K 1x1 products).
+template <int MODE, int BM, int BN, int BK>
+__global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(const ConvParams p,
+                                                                              const __bf16 *__restrict__ ab,
+                                                                              const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
-  constexpr int NT = 512, BK = kG16BK;
+  static_assert(BK == 64 || BK == 32, "K step");
+  constexpr int NT = 512;
   constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;  // 64x64 wave tiles
   static_assert(WAVES_M * WAVES_N == 8, "8 waves");
   constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2;
-  constexpr int NA = BM / 64, NB = BN / 64;             // LDS-DMA instructions per wave and K step
+  constexpr int LPR = BK / 8;                          // lanes per image row (16 B each)
+  constexpr int RPI = 64 / LPR;                        // rows per LDS-DMA instruction
+  constexpr int NA = BM / (8 * RPI), NB = BN / (8 * RPI);  // instructions per wave and K step
   constexpr int IMGA = BM * BK * 2;
-  constexpr int STAGE = g16_stage_bytes(BM, BN);
+  constexpr int STAGE = g16_stage_bytes(BM, BN, BK);
+  (void)NT;
 
   __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
 
@@ -74,14 +89,15 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
   // bf16 copy of the activation operand: NHWC contiguous, channel count ca
   const int ca = MODE == MODE_FWD ? p.c : p.k;
 
-  // ---- per-lane rows: instruction i of wave w covers image rows 64 i + 8 w .. +7 ----
-  const int rsub = wave * 8 + (lane >> 3);                 // row within a 64-row group
-  const int chs = ((lane & 7) ^ ((rsub >> 1) & 7)) * 8;    // source chunk (elements) of this lane
+  // ---- per-lane rows: instruction i of wave w covers image rows 8 RPI i + RPI w .. +RPI-1 ----
+  const int rsub = wave * RPI + lane / LPR;                 // row within an 8 RPI-row group
+  // source chunk (elements) of this lane: the one whose swizzled slot is the lane's (lane % LPR)
+  const int chs = (BK == 64 ? ((lane & 7) ^ ((rsub >> 1) & 7)) : ((lane & 3) ^ ((rsub >> 2) & 3))) * 8;
   int a_pix[NA], a_y[NA], a_x[NA];
   bool a_ok[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int m = bm + 64 * i + rsub;
+    const int m = bm + 8 * RPI * i + rsub;
     a_ok[i] = m < M;
     const int mm = min(m, M - 1);
     if constexpr (MODE == MODE_FWD) {
@@ -106,7 +122,7 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
   bool b_ok[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int n = bn + 64 * j + rsub;
+    const int n = bn + 8 * RPI * j + rsub;
     b_ok[j] = n < p.N;
     b_off[j] = min(n, p.N - 1) * ktot + chs;
   }
@@ -115,7 +131,7 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
   // LDS-DMA of K step kt into ring stage st: NA + NB instructions per wave
   auto issue = [&](int kt, int st) {
     const int kbase = kt * BK;
-    const uint32_t As = uni((int)((uint32_t)(uintptr_t)lds + st * STAGE + wave * 8 * 128));
+    const uint32_t As = uni((int)((uint32_t)(uintptr_t)lds + st * STAGE + wave * 1024));
     const uint32_t Bs = As + IMGA;
     int soff, wk, dy, dx;
     if constexpr (MODE == MODE_FWD) {
@@ -142,10 +158,10 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
         v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.h) & ((unsigned)(a_x[i] + dx) < (unsigned)p.w);
       else
         v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.oh) & ((unsigned)(a_x[i] + dx) < (unsigned)p.ow);
-      glds16(v ? ab + a_pix[i] + soff : zero, As + i * 64 * 128);
+      glds16(v ? ab + a_pix[i] + soff : zero, As + i * 8 * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) glds16(b_ok[j] ? wb + b_off[j] + wk : zero, Bs + j * 64 * 128);
+    for (int j = 0; j < NB; ++j) glds16(b_ok[j] ? wb + b_off[j] + wk : zero, Bs + j * 8 * 1024);
   };
 
   const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
@@ -163,9 +179,13 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[slot][i] = kc_frag(As, wm * WTM + i * 32, ks, lane);
+      for (int i = 0; i < TM; ++i)
+        a[slot][i] = as_bf16x8(*reinterpret_cast<const uint4 *>(
+            As + g16_off<BK>(wm * WTM + i * 32 + (lane & 31), 2 * ks + (lane >> 5))));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[slot][j] = kc_frag(Bs, wn * WTN + j * 32, ks, lane);
+      for (int j = 0; j < TN; ++j)
+        b[slot][j] = as_bf16x8(*reinterpret_cast<const uint4 *>(
+            Bs + g16_off<BK>(wn * WTN + j * 32 + (lane & 31), 2 * ks + (lane >> 5))));
     };
     read_frags(0, 0);
 #pragma unroll
@@ -190,8 +210,9 @@ __global__ void __launch_bounds__(512, 1) igemm_bf16g_kernel(const ConvParams p,
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       // this wave's DMAs of step kt are done (step kt+1's NA + NB stay in flight) ...
-      static_assert(NA + NB == 6, "vmcnt below counts 6 instructions per step");
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      static_assert(NA + NB == 6 || NA + NB == 3, "vmcnt below counts 6 or 3 instructions per step");
+      if constexpr (NA + NB == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       // ... and after the barrier every wave's are, and every wave has finished reading the
       // stage that step kt+2 overwrites (step kt-1's)
       __builtin_amdgcn_s_barrier();

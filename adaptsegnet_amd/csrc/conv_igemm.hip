@@ -324,7 +324,7 @@ void set_splits(Plan &pl) {
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
   const int bm = pl.g16 ? pl.g16_bm : (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
   const int bn = pl.g16 ? pl.g16_bn : pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
-  pl.bk = pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
+  pl.bk = pl.g16 ? pl.g16_bk : pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
     p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
@@ -476,6 +476,11 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16 = true;
       pl.g16_bm = p.N >= 256 ? 128 : 256;
       pl.g16_bn = p.N >= 256 ? 256 : 128;
+      // K step: 64 (one block per CU) for K >= 2048, else 32 (two blocks per CU: one block's
+      // prologue / epilogue overlaps the other's loop on short-K products) — per shape
+      // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
+      // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
+      pl.g16_bk = p.K >= 2048 ? 64 : 32;
     }
   }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
@@ -491,7 +496,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
-  if (pl.g16) return 100 * mode + (pl.g16_bn == 256 ? 97 : 98);
+  if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
   // FAST: 4 + (S2 ? 4 : 0) + (AE ? 2 : 0) + (BE ? 1 : 0)  ->  4..11 (S2 variants 8, 9)

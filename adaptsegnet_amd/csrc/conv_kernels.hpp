@@ -1255,7 +1255,7 @@ struct Plan {
   bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
-  int g16_bm, g16_bn;
+  int g16_bm, g16_bn, g16_bk;
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
   int mode;

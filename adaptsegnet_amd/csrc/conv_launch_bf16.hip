@@ -104,13 +104,19 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
     const __bf16 *act = reinterpret_cast<const __bf16 *>(reinterpret_cast<const char *>(wpack) +
                                                          (bf16_wpack_bytes(pl) + 255) / 256 * 256);
     dim3 grid(pl.tiles, p.splits), block(512);
+#define G16_LAUNCH(MODE_, BK_)                                                                  \
+  do {                                                                                          \
+    if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_, 128, 256, BK_><<<grid, block, 0, s>>>(p, act, wb); \
+    else igemm_bf16g_kernel<MODE_, 256, 128, BK_><<<grid, block, 0, s>>>(p, act, wb);          \
+  } while (0)
     if (pl.mode == MODE_FWD) {
-      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_FWD, 128, 256><<<grid, block, 0, s>>>(p, act, wb);
-      else igemm_bf16g_kernel<MODE_FWD, 256, 128><<<grid, block, 0, s>>>(p, act, wb);
+      if (pl.g16_bk == 64) G16_LAUNCH(MODE_FWD, 64);
+      else G16_LAUNCH(MODE_FWD, 32);
     } else {
-      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_DGRAD, 128, 256><<<grid, block, 0, s>>>(p, act, wb);
-      else igemm_bf16g_kernel<MODE_DGRAD, 256, 128><<<grid, block, 0, s>>>(p, act, wb);
+      if (pl.g16_bk == 64) G16_LAUNCH(MODE_DGRAD, 64);
+      else G16_LAUNCH(MODE_DGRAD, 32);
     }
+#undef G16_LAUNCH
     return hipGetLastError();
   }
   const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;

@@ -86,7 +86,7 @@ def main():
     tot_ms, tot_fl = 0.0, 0.0
     per_op = collections.defaultdict(lambda: [0.0, 0.0])
     print(f"{'conv':<10} {'op':>3} {'n':>2} {'hxw':>9} {'cin':>5} {'cout':>5} {'k':>2} {'sel':>4} {'spl':>3} "
-          f"{'cnt':>4} {'avg us':>9} {'TF/s':>7}")
+          f"{'cnt':>4} {'avg us':>9} {'TF/s':>7} {'kern us':>9} {'kTF/s':>7}")
     for (g, n, h, w, ops, st), (count, name) in shapes(args.batch, args.width, args.height).items():
         if args.filter and args.filter not in name:
             continue
@@ -129,6 +129,15 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
+            # the GEMM kernel alone (the library's own hipEvent bracket: no weight pack,
+            # activation copy or split-K reduce)
+            K.timing_enable(-1, True)
+            for _ in range(args.reps):
+                run()
+            torch.cuda.synchronize()
+            kms, _, kn = K.timing_read()
+            K.timing_enable(-1, False)
+            kus = 1e3 * kms / max(1, args.reps)
             fl = g.flops(n, h, w)
             if op == 2 and pad_wgrad:
                 c4 = (g.cin + 3) // 4 * 4
@@ -141,7 +150,7 @@ def main():
             per_op[op][0] += ms * c
             per_op[op][1] += fl * c
             print(f"{name:<10} {op:>3} {n:>2} {h:>4}x{w:<4} {g.cin:>5} {g.cout:>5} {g.kh:>2} {sel:>4} {sp:>3} "
-                  f"{c:>4} {ms * 1e3:9.1f} {fl / ms / 1e9:7.1f}", flush=True)
+                  f"{c:>4} {ms * 1e3:9.1f} {fl / ms / 1e9:7.1f} {kus:9.1f} {fl / max(kus, 1e-3) / 1e6:7.1f}", flush=True)
     for op, (ms, fl) in sorted(per_op.items()):
         print(f"op {op}: {ms:8.2f} ms/step  {fl / 1e12:6.3f} TFLOP  {fl / ms / 1e9:6.1f} TF/s")
     print(f"TOTAL conv: {tot_ms:8.2f} ms/step, {tot_fl / 1e12:.3f} TFLOP, {tot_fl / tot_ms / 1e9:.1f} TF/s")
