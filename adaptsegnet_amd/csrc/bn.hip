@@ -243,10 +243,19 @@ __global__ void bn_bwd_final_kernel(int64_t rows, int C, int splits, const float
   if (dweight) dweight[c] += (float)(s2 * (double)invstd[c]);
 }
 
+// four floats -> four bf16 (RNE) in 8 bytes: the bf16 operand copy a BN pass writes beside its
+// fp32 output for the bf16-operand convs (conv math BF16) that consume it
+__device__ __forceinline__ uint2 bf16x4_rne(float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef __bf16 b4v __attribute__((ext_vector_type(4)));
+  const f4v f = {v.x, v.y, v.z, v.w};
+  return __builtin_bit_cast(uint2, __builtin_convertvector(f, b4v));
+}
+
 __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
-                                      const float *__restrict__ res, float *__restrict__ y, int relu) {
+                                      const float *__restrict__ res, float *__restrict__ y, uint2 *yb, int relu) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
@@ -264,6 +273,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__rest
       o[j] = fwd_act(t, relu);
     }
     reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    if (yb) yb[i] = bf16x4_rne(make_float4(o[0], o[1], o[2], o[3]));
   }
 }
 
@@ -273,13 +283,14 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__rest
 // every element is still read before it is written, by the same thread).
 constexpr int kApplyUnroll = 4;
 
+
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
 __global__ void __launch_bounds__(256)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
-                  const float *res, float *y, int act) {
+                  const float *res, float *y, uint2 *yb, int act) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -308,6 +319,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, cons
       o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
       o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
       st4(y + ru * C + c0, o);
+      if (yb) yb[(ru * C + c0) >> 2] = bf16x4_rne(o);
     }
   }
 }
@@ -315,8 +327,8 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, cons
 __global__ void __launch_bounds__(256)
 bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, const float *y, const float *x,
                       const float *__restrict__ w, const float *__restrict__ b, const float *__restrict__ mean,
-                      const float *__restrict__ invstd, const float *__restrict__ coef, float *dx, float *dres,
-                      int rmode, int train) {
+                      const float *__restrict__ invstd, const float *__restrict__ coef, float *dx, uint2 *dxb,
+                      float *dres, int rmode, int train) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -372,6 +384,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
         out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
       }
       st4(dx + e, out);
+      if (dxb) dxb[e >> 2] = bf16x4_rne(out);
     }
   }
 }
@@ -441,10 +454,10 @@ int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes) {
   return ADAPTSEG_OK;
 }
 
-int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                          float *running_mean, float *running_var, float momentum, float eps,
-                          float *save_mean, float *save_invstd, const float *res, float *y, int relu,
-                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                            float *running_mean, float *running_var, float momentum, float eps,
+                            float *save_mean, float *save_invstd, const float *res, float *y, uint16_t *y_bf16,
+                            int relu, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
@@ -470,16 +483,26 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
   const ApplyPlan ap = apply_plan(rows, c);
   timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                 weight, bias, res, y, relu);
+                                                                 weight, bias, res, y,
+                                                                 reinterpret_cast<uint2 *>(y_bf16), relu);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
 }
 
-int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
-                                const float *weight, const float *bias, float *running_mean, float *running_var,
-                                float momentum, float eps, float *save_mean, float *save_invstd, const float *res,
-                                float *y, int relu, adaptseg_stream_t stream) {
+int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          float *running_mean, float *running_var, float momentum, float eps,
+                          float *save_mean, float *save_invstd, const float *res, float *y, int relu,
+                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_train_x(rows, c, x, weight, bias, running_mean, running_var, momentum, eps, save_mean,
+                                 save_invstd, res, y, nullptr, relu, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                  const float *weight, const float *bias, float *running_mean, float *running_var,
+                                  float momentum, float eps, float *save_mean, float *save_invstd,
+                                  const float *res, float *y, uint16_t *y_bf16, int relu,
+                                  adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(stats && ntiles > 0 && x && y && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
@@ -491,30 +514,46 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
   int slot;  // x (+res) in, y out
   timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                 weight, bias, res, y, relu);
+                                                                 weight, bias, res, y,
+                                                                 reinterpret_cast<uint2 *>(y_bf16), relu);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
 }
 
-int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                          const float *running_mean, const float *running_var, float eps, const float *res,
-                          float *y, int relu, adaptseg_stream_t stream) {
+int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                const float *weight, const float *bias, float *running_mean, float *running_var,
+                                float momentum, float eps, float *save_mean, float *save_invstd, const float *res,
+                                float *y, int relu, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_train_tiles_x(rows, c, stats, ntiles, x, weight, bias, running_mean, running_var, momentum,
+                                       eps, save_mean, save_invstd, res, y, nullptr, relu, stream);
+}
+
+int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                            const float *running_mean, const float *running_var, float eps, const float *res,
+                            float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
   AS_CHECK_ARG(x && y && running_mean && running_var, "bn_fwd_infer: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
   hipStream_t s = as_stream(stream);
   int64_t total4 = rows * c / 4;
   bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight,
-                                                         bias, res, y, relu);
+                                                         bias, res, y, reinterpret_cast<uint2 *>(y_bf16), relu);
   AS_CHECK_LAUNCH("bn_infer_apply");
   return ADAPTSEG_OK;
 }
 
+int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          const float *running_mean, const float *running_var, float eps, const float *res,
+                          float *y, int relu, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_infer_x(rows, c, x, weight, bias, running_mean, running_var, eps, res, y, nullptr, relu,
+                                 stream);
+}
+
 static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
-                       const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
-                       int relu, int train, float *dweight, float *dbias, void *ws, size_t ws_bytes,
-                       adaptseg_stream_t stream) {
+                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
+                       uint16_t *dx_bf16, float *dres, int relu, int train, float *dweight, float *dbias, void *ws,
+                       size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
   AS_CHECK_ARG(dy && dx && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
@@ -552,7 +591,8 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);
   bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, y, x, weight, bias,
-                                                                     save_mean, save_invstd, coef, dx, dres, rmode,
+                                                                     save_mean, save_invstd, coef, dx,
+                                                                     reinterpret_cast<uint2 *>(dx_bf16), dres, rmode,
                                                                      train);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
@@ -562,8 +602,16 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
                     int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dres, relu, train, nullptr,
-                     nullptr, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, nullptr, dres, relu, train,
+                     nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
+                      const float *bias, const float *save_mean, const float *save_invstd, float *dx,
+                      uint16_t *dx_bf16, float *dres, int relu, int train, void *ws, size_t ws_bytes,
+                      adaptseg_stream_t stream) {
+  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, relu, train,
+                     nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,
@@ -571,8 +619,8 @@ int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y,
                            const float *save_invstd, float *dx, float *dres, int act, float *dweight,
                            float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(dweight || dbias, "bn_bwd_affine: no affine gradient requested");
-  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dres, act, 1, dweight, dbias,
-                     ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, nullptr, dres, act, 1, dweight,
+                     dbias, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

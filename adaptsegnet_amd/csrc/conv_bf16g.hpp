@@ -229,4 +229,117 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
                                                          reinterpret_cast<float *>(lds));
 }
 
+// Weight gradient on the same LDS-DMA ring: dW[co][tap, ci] = sum_pix dY[pix][co] x[pix+tap][ci]
+// with both operands bf16 copies in HBM (dY: the producing BN backward's copy, x: the forward
+// BN's).  k = output pixel, so both images are M/N-contiguous [32 k][128] (conv_bf16.hpp's
+// 256-B rows, read with ds_read_b64_tr_b16); one LDS-DMA instruction fills 4 k-rows, so each of
+// the 8 waves issues one A and one B instruction per K step of 32 pixels.  A 128-column tile
+// lies in one tap (Cin % 128 == 0), so a k-row of B is one contiguous 256-B run of x or, for a
+// tap outside the image, zeros.  3 x 16 KB ring, two blocks per CU.
+template <int BKP>
+__global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvParams p, const __bf16 *__restrict__ dyb,
+                                                                    const __bf16 *__restrict__ xb) {
+  static_assert(BKP == 32, "one A and one B instruction per wave and K step");
+  constexpr int BM = 128, BN = 128, WAVES_M = 2, WAVES_N = 4;
+  constexpr int WTM = 64, WTN = 32, TM = 2, TN = 1;
+  constexpr int IMG = BKP * 256;              // [32 k][128] bf16
+  constexpr int STAGE = 2 * IMG;
+
+  __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int ntn = (p.N + BN - 1) / BN;
+  int tile, split;
+  xcd_tile_split(tile, split);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int bm = tm * BM, bn = tn * BN;
+  const SegRegs sr = seg_regs(p);
+
+  const int K = p.K;                          // output pixels
+  const int nkt = (K + BKP - 1) / BKP;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
+
+  // this lane's k-row (pixel within the step) and 16-B slot; the source chunk whose swizzled
+  // position (mc_off) is that slot
+  const int kr = 4 * wave + (lane >> 4);
+  const int chs = ((lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3))) * 8;
+  const bool a_col = bm + chs < p.M;          // Cout % 8 == 0: a chunk is all in or all out
+  const int tap = uni((int)fdiv((uint32_t)bn, p.fd_c));
+  int seg, t, tdy, tdx;
+  seg_geom(p, sr, tap, seg, t, tdy, tdx);
+  tdy = uni(tdy);
+  tdx = uni(tdx);
+  const int ci = bn - tap * p.c + chs;
+  const bool b_col = bn + chs < p.N;
+  const __bf16 *zero = reinterpret_cast<const __bf16 *>(g_bf16g_zero);
+
+  auto issue = [&](int kt, int st) {
+    const uint32_t As = uni((int)((uint32_t)(uintptr_t)lds + st * STAGE + wave * 1024));
+    const int m = kt * BKP + kr;
+    const bool rv = m < K;
+    const int mm = rv ? m : 0;
+    uint32_t q = fdiv((uint32_t)mm, p.fd_ow);
+    const int ow = mm - (int)q * p.ow;
+    uint32_t b = fdiv(q, p.fd_oh);
+    const int oh = (int)q - (int)b * p.oh;
+    const int iy = oh * p.stride + tdy, ix = ow * p.stride + tdx;
+    const bool bv = rv & b_col & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
+    glds16(rv & a_col ? dyb + (size_t)mm * p.k + bm + chs : zero, As);
+    glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci : zero, As + IMG);
+  };
+
+  const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int st) {
+    const char *As = lds + st * STAGE;
+    const char *Bs = As + IMG;
+    bf16x8 a[2][TM], b[2][TN];
+    auto read_frags = [&](int ks, int slot) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[slot][i] = mc_frag(As, wm * WTM + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[slot][j] = mc_frag(Bs, wn * WTN + j * 32, ks, lane);
+    };
+    read_frags(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < BKP / 16; ++ks) {
+      const int cb = ks & 1;
+      if (ks + 1 < BKP / 16) read_frags(ks + 1, cb ^ 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cb][i], b[cb][j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (kt0 < kt1) {
+    const int klast = kt1 - 1;
+    issue(kt0, 0);
+    issue(min(kt0 + 1, klast), 1);
+    int st = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // step kt landed, kt+1 in flight
+      __builtin_amdgcn_s_barrier();
+      issue(min(kt + 2, klast), st == 0 ? 2 : st - 1);
+      compute(st);
+      st = st == 2 ? 0 : st + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  igemm_epilogue<MODE_WGRAD, BM, BN, WAVES_M, WAVES_N, false>(p, acc, bm, bn, tm, tn, split, p.M, p.h, p.w, 0, 0,
+                                                              reinterpret_cast<float *>(lds));
+}
+
 }  // namespace adaptseg

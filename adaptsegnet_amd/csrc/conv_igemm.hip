@@ -357,7 +357,7 @@ void set_splits(Plan &pl) {
   const int split_below = pl.mode == MODE_WGRAD ? target : pl.g16 ? 128 : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, (pl.g16 ? 256 : target) / pl.tiles);
+    splits = std::max(1, (pl.g16 && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -376,6 +376,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   ConvParams &p = pl.p;
   fill_common(p, d);
   pl.mode = op;
+  pl.act_ext = pl.act_ext2 = nullptr;
   const bool nhwc_in = d->in_stride[1] == 1;
   if (op == ADAPTSEG_CONV_FWD) {
     p.M = d->n * d->oh * d->ow;
@@ -481,6 +482,13 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = p.K >= 2048 ? 64 : 32;
+    }
+    // weight gradients whose 128-column tiles lie in one tap (Cin % 128 == 0) on the LDS-DMA
+    // weight-gradient kernel: 128x128 tiles, K steps of 32 output pixels
+    if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 128 == 0 && d->k % 8 == 0) {
+      pl.g16 = true;
+      pl.g16_bm = pl.g16_bn = 128;
+      pl.g16_bk = 32;
     }
   }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
@@ -634,6 +642,12 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                         const float *const *bias, const float *res, float *y, int flags, void *ws,
                         size_t ws_bytes, adaptseg_stream_t stream) {
+  return adaptseg_conv2d_fwd_x(d, x, nullptr, w, bias, res, y, flags, ws, ws_bytes, stream);
+}
+
+int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                          const float *const *w, const float *const *bias, const float *res, float *y, int flags,
+                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
@@ -657,6 +671,7 @@ int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float
   }
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
+  pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
   p.out = y;
   p.res = res;
   p.flags = flags;
@@ -689,6 +704,12 @@ int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
 int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w, float *y,
                                 float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
                                 adaptseg_stream_t stream) {
+  return adaptseg_conv2d_fwd_bnstats_x(d, x, nullptr, w, y, stats, stats_bytes, ntiles, ws, ws_bytes, stream);
+}
+
+int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                                  const float *const *w, float *y, float *stats, size_t stats_bytes, int *ntiles,
+                                  void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(ntiles && stats, "conv fwd_bnstats: null stats / ntiles");
   *ntiles = 0;
   Plan pl;
@@ -697,7 +718,7 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
   AS_CHECK_ARG(x && w && y, "conv fwd_bnstats: null pointer");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
   if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
-    return adaptseg_conv2d_fwd(d, x, w, nullptr, nullptr, y, 0, ws, ws_bytes, stream);
+    return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, y, 0, ws, ws_bytes, stream);
   ConvParams &p = pl.p;
   p.x = x;
   for (int s = 0; s < d->nseg; ++s) {
@@ -706,6 +727,7 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
   }
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
+  pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
   p.out = y;
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
@@ -722,6 +744,12 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream) {
+  return adaptseg_conv2d_bwd_data_x(d, dy, nullptr, w, res, aux, dx, flags, ws, ws_bytes, stream);
+}
+
+int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                               const float *const *w, const float *res, const float *aux, float *dx, int flags,
+                               void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
@@ -746,6 +774,7 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
   }
   if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
   set_splits(pl);
+  pl.act_ext = aligned16(dy_bf16) ? dy_bf16 : nullptr;
   p.out = dx;
   p.res = res;
   p.aux = aux;
@@ -756,6 +785,12 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
                                float *const *dw, float *const *db, int flags, void *ws,
                                size_t ws_bytes, adaptseg_stream_t stream) {
+  return adaptseg_conv2d_bwd_weight_x(d, dy, nullptr, x, nullptr, dw, db, flags, ws, ws_bytes, stream);
+}
+
+int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                 const float *x, const uint16_t *x_bf16, float *const *dw, float *const *db,
+                                 int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_WEIGHT, pl);
   if (st) return st;
@@ -779,6 +814,10 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
     if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
     if (reinterpret_cast<uintptr_t>(x) & 15) pl.vb = pl.fast = false;
     set_splits(pl);
+    if (aligned16(dy_bf16) && aligned16(x_bf16) && dy_bf16 && x_bf16) {  // both copies or none
+      pl.act_ext = dy_bf16;
+      pl.act_ext2 = x_bf16;
+    }
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
     st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
   }

@@ -1256,6 +1256,8 @@ struct Plan {
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
   int g16_bm, g16_bn, g16_bk;
+  const void *act_ext;  // caller's bf16 copy of the activation operand (g16; NULL: copied per call)
+  const void *act_ext2; // weight gradient: the caller's bf16 copy of x (act_ext: of dY)
   bool ae, be; // FAST per-element gathers for the A / B operand
   int bk;
   int mode;

@@ -56,14 +56,21 @@ __global__ void bf16_copy_kernel(const float *__restrict__ x, int n, int h, int 
 }
 
 // elements of the LDS-DMA kernel's bf16 activation copy (FWD: x, DGRAD: dY)
+// (weight gradient: dY's copy, then x's)
 static size_t g16_act_elems(const Plan &pl) {
   const ConvParams &p = pl.p;
   if (!pl.g16) return 0;
   return pl.mode == MODE_FWD ? (size_t)p.n * p.h * p.w * p.c : (size_t)p.n * p.oh * p.ow * p.k;
 }
+static size_t g16_act2_elems(const Plan &pl) {
+  const ConvParams &p = pl.p;
+  return pl.g16 && pl.mode == MODE_WGRAD ? (size_t)p.n * p.h * p.w * p.c : 0;
+}
+static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
 size_t bf16_pre_bytes(const Plan &pl) {
-  return (bf16_wpack_bytes(pl) + 255) / 256 * 256 + (g16_act_elems(pl) * sizeof(__bf16) + 255) / 256 * 256;
+  return al256(bf16_wpack_bytes(pl)) + al256(g16_act_elems(pl) * sizeof(__bf16)) +
+         al256(g16_act2_elems(pl) * sizeof(__bf16));
 }
 
 size_t bf16_wpack_bytes(const Plan &pl) {
@@ -84,8 +91,9 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
     dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
     conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
-  if (pl.g16) {  // the activation operand's bf16 copy, after the (256-B aligned) weight pack
-    uint4 *act = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(wpack) + (bf16_wpack_bytes(pl) + 255) / 256 * 256);
+  if (pl.g16 && !pl.act_ext) {  // the activation operands' bf16 copies, after the (256-B aligned) weight pack
+    char *base = reinterpret_cast<char *>(wpack) + al256(bf16_wpack_bytes(pl));
+    uint4 *act = reinterpret_cast<uint4 *>(base);
     const int64_t n8 = (int64_t)g16_act_elems(pl) / 8;
     const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192);
     if (pl.mode == MODE_FWD)
@@ -93,6 +101,12 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
     else
       bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.dy, p.n, p.oh, p.ow, p.k / 8, p.oh * p.ow * p.k, p.ow * p.k,
                                               p.k, act);
+    if (pl.mode == MODE_WGRAD) {
+      uint4 *act2 = reinterpret_cast<uint4 *>(base + al256(g16_act_elems(pl) * sizeof(__bf16)));
+      const int64_t m8 = (int64_t)g16_act2_elems(pl) / 8;
+      bf16_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(m8, 256), 8192), 256, 0, s>>>(
+          p.x, p.n, p.h, p.w, p.c / 8, p.sxn, p.sxh, p.sxw, act2);
+    }
   }
   return hipGetLastError();
 }
@@ -101,9 +115,17 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
   if (pl.g16) {
-    const __bf16 *act = reinterpret_cast<const __bf16 *>(reinterpret_cast<const char *>(wpack) +
-                                                         (bf16_wpack_bytes(pl) + 255) / 256 * 256);
+    const char *base = reinterpret_cast<const char *>(wpack) + al256(bf16_wpack_bytes(pl));
+    const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext)
+                                   : reinterpret_cast<const __bf16 *>(base);
     dim3 grid(pl.tiles, p.splits), block(512);
+    if (pl.mode == MODE_WGRAD) {
+      const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
+                                       : reinterpret_cast<const __bf16 *>(
+                                             base + al256(g16_act_elems(pl) * sizeof(__bf16)));
+      igemm_bf16g_wgrad_kernel<32><<<grid, block, 0, s>>>(p, act, act2);
+      return hipGetLastError();
+    }
 #define G16_LAUNCH(MODE_, BK_)                                                                  \
   do {                                                                                          \
     if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_, 128, 256, BK_><<<grid, block, 0, s>>>(p, act, wb); \

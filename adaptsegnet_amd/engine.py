@@ -73,33 +73,48 @@ class WgradStream:
 # ---------------------------------------------------------------------------------------
 
 
+def bf16_operands() -> bool:
+    """Under the bf16 conv math (config c5) the BN passes that produce conv operands also write
+    a bf16 copy of them, which the bf16 LDS-DMA conv kernel reads instead of converting the
+    fp32 tensor itself (adaptseg_conv2d_*_x): one pass over every such activation less."""
+    return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
+
+
+def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False):
+    """bn_forward that also returns the bf16 copy of y (None unless ``bf16``)."""
+    if training:
+        if tiles is not None:
+            r = K.bn_fwd_train_tiles(x, tiles, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     bn.momentum, bn.eps, res=res, relu=relu, bf16_out=bf16)
+        else:
+            r = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
+                               bn.eps, res=res, relu=relu, bf16_out=bf16)
+        y, mean, invstd = r[:3]
+        return y, (mean, invstd, True), (r[3] if bf16 else None)
+    r = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
+                       relu=relu, bf16_out=bf16)
+    y, yb = r if bf16 else (r, None)
+    return y, (bn.running_mean, None, False), yb
+
+
 def bn_forward(bn, x, res, relu, training, tiles=None):
     """tiles: row-tile statistics of x from the producing conv (conv_fwd_bnstats), which
     replace the BN's own statistics pass in train mode."""
-    if training:
-        if tiles is not None:
-            y, mean, invstd = K.bn_fwd_train_tiles(x, tiles, bn.weight, bn.bias, bn.running_mean,
-                                                   bn.running_var, bn.momentum, bn.eps, res=res,
-                                                   relu=relu)
-        else:
-            y, mean, invstd = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                             bn.momentum, bn.eps, res=res, relu=relu)
-        return y, (mean, invstd, True)
-    y = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
-                       relu=relu)
-    return y, (bn.running_mean, None, False)
+    y, st, _ = bn_forward_b(bn, x, res, relu, training, tiles)
+    return y, st
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
-    mode instead of reading the saved output y (one activation read less per pass)."""
+    mode instead of reading the saved output y (one activation read less per pass).
+    bf16: return (dx, bf16 copy of dx) for the bf16-math data gradient that consumes dx."""
     mean, invstd, train = st
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
     elif mask_from_x and relu:
         y = None
     return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train,
-                    bias=bn.bias)
+                    bias=bn.bias, bf16_out=bf16)
 
 
 # ---------------------------------------------------------------------------------------
@@ -109,52 +124,56 @@ def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False):
 
 class BlockRec:
     __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
-                 "n", "h", "w", "oh", "ow")
+                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b")
 
 
-def _conv_bn(g, x, n, h, w, weight, strides=None):
+def _conv_bn(g, x, n, h, w, weight, strides=None, xb=None):
     """Conv feeding a train-mode BN: also returns the BN's row-tile statistics (or None)."""
-    return K.conv_fwd_bnstats(g, x, n, h, w, [weight], strides=strides)
+    return K.conv_fwd_bnstats(g, x, n, h, w, [weight], strides=strides, xb=xb)
 
 
-def _conv_plain(g, x, n, h, w, weight, strides=None):
-    return K.conv_fwd(g, x, n, h, w, [weight], strides=strides), None
+def _conv_plain(g, x, n, h, w, weight, strides=None, xb=None):
+    return K.conv_fwd(g, x, n, h, w, [weight], strides=strides, xb=xb), None
 
 
-def block_forward(blk, x, n, h, w, training, save):
+def block_forward(blk, x, n, h, w, training, save, xb=None):
+    """xb: bf16 copy of x (bf16 conv math), or None.  Returns (out, rec, bf16 copy of out)."""
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     oh, ow = g1.out_hw(h, w)
     conv = _conv_bn if training else _conv_plain
-    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight)
-    y1, s1 = bn_forward(blk.bn1, c1, None, True, training, t1)
-    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight)
-    y2, s2 = bn_forward(blk.bn2, c2, None, True, training, t2)
-    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight)
+    sh = bf16_operands()
+    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb)
+    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh)
+    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b)
+    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh)
+    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b)
     cd = sd = None
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
-        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight)
+        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight, xb=xb)
         r, sd = bn_forward(dbn, cd, None, False, training, td)
     else:
         r = x
-    out, s3 = bn_forward(blk.bn3, c3, r, True, training, t3)
+    out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh)
     rec = None
     if save:
         rec = BlockRec()
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
-    return out, rec
+        rec.xb, rec.y1b, rec.y2b = xb, y1b, y2b   # the weight gradients' bf16 x operands
+    return out, rec, outb
 
 
-def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None):
-    """Weight gradient of one conv: on the side stream when ``ws`` is given."""
+def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None, dyb=None, xb=None):
+    """Weight gradient of one conv: on the side stream when ``ws`` is given.  dyb / xb: bf16
+    copies of both operands (bf16 conv math)."""
     def run():
-        K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides)
+        K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides, dyb=dyb, xb=xb)
     if ws is None:
         run()
     else:
-        ws.launch(run, dy, x)
+        ws.launch(run, *[t for t in (dy, x, dyb, xb) if t is not None])
 
 
 # ---------------------------------------------------------------------------------------
@@ -197,30 +216,36 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
-    dc3 = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout)
-    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight])
+    sh = bf16_operands()   # bf16 copies of each data-gradient operand (bf16 conv math)
+    r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh)
+    dc3, dc3b = r if sh else (r, None)
+    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b)
     if need_w and blk.conv3.weight.grad is not None:
-        _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad])
-    del dc3
-    bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True)
-    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight])
+        _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
+    del dc3, dc3b
+    r = bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, bf16=sh)
+    dy2b = r[1] if sh else None
+    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b)
     if need_w and blk.conv2.weight.grad is not None:
-        _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad])
-    del dy2
-    bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True)
+        _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
+    del dy2, dy2b
+    r = bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, bf16=sh)
+    dy1b = r[1] if sh else None
     if need_w and blk.conv1.weight.grad is not None:
-        _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad])
+        _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad], dyb=dy1b, xb=rec.xb)
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
-        bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout)
+        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout, bf16=sh)
+        goutb = r[1] if sh else None
         if need_w and dconv.weight.grad is not None:
-            _wgrad(ws, gd, gout, rec.x, n, h, w, [dconv.weight.grad])
-        dx = K.conv_dgrad(gd, gout, n, h, w, [dconv.weight])
-        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE)
+            _wgrad(ws, gd, gout, rec.x, n, h, w, [dconv.weight.grad], dyb=goutb, xb=rec.xb)
+        dx = K.conv_dgrad(gd, gout, n, h, w, [dconv.weight], dyb=goutb)
+        del goutb
+        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE, dyb=dy1b)
     else:
         # identity residual: dx = dgrad(conv1) + g, written over g in place
-        dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout)
+        dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout, dyb=dy1b)
     return dx
 
 
@@ -279,20 +304,21 @@ class _DeeplabMultiFn(torch.autograd.Function):
         p, am = K.maxpool_fwd(y0)
         ph, pw = p.shape[1], p.shape[2]
         recs = []
-        cur, ch, cw = p, ph, pw
+        cur, curb, ch, cw = p, None, ph, pw
         for layer in (model.layer1, model.layer2, model.layer3):
             for blk in layer:
                 nh, nw = blk.conv1.geom().out_hw(ch, cw)
-                cur, rec = block_forward(blk, cur, n, ch, cw, training, save)
+                cur, rec, curb = block_forward(blk, cur, n, ch, cw, training, save, xb=curb)
                 recs.append(rec)
                 ch, cw = nh, nw
         p3, h3, w3 = cur, ch, cw
         x1 = aspp_forward(model.layer5, p3, n, h3, w3)
-        q = p3
+        q, qb = p3, curb
         recs4 = []
         for blk in model.layer4:
-            q, rec = block_forward(blk, q, n, h3, w3, training, save)
+            q, rec, qb = block_forward(blk, q, n, h3, w3, training, save, xb=qb)
             recs4.append(rec)
+        del curb, qb
         x2 = aspp_forward(model.layer6, q, n, h3, w3)
         x1_up = K.upsample_fwd(x1, out_h, out_w)
         x2_up = K.upsample_fwd(x2, out_h, out_w)

@@ -98,15 +98,16 @@ def _wshape(g: ConvGeom):
 
 
 def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, biases=None,
-             strides=None, out=None, res=None, flags: int = 0) -> torch.Tensor:
-    """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (EPI_LEAKY / EPI_RELU)."""
+             strides=None, out=None, res=None, flags: int = 0, xb=None) -> torch.Tensor:
+    """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (EPI_LEAKY / EPI_RELU).
+    xb: optional bf16 copy of x (contiguous NHWC) for the bf16 conv math (bn_* ``bf16_out``)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
     oh, ow = g.out_hw(h, w)
     if out is None:
         out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
-    _OP.conv2d_fwd(x, list(weights), list(biases) if biases is not None else [], res, out, (n, g.cin, h, w),
+    _OP.conv2d_fwd(x, xb, list(weights), list(biases) if biases is not None else [], res, out, (n, g.cin, h, w),
                    strides, _wshape(g), g.stride, g.pads, g.dils, flags)
     return out
 
@@ -118,23 +119,23 @@ def conv_bnstats_tiles(g: ConvGeom, n: int, h: int, w: int, strides) -> int:
     return nt.value
 
 
-def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, strides=None):
+def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, strides=None, xb=None):
     """y = conv(x, w) plus the per-row-tile BatchNorm statistics of y when the kernel can
     produce them: returns (y, (stats, ntiles)) or (y, None)."""
     strides = tuple(strides or nhwc_strides(n, h, w, g.cin))
     nt = conv_bnstats_tiles(g, n, h, w, strides)
     if nt == 0:
-        return conv_fwd(g, x, n, h, w, weights, strides=strides), None
+        return conv_fwd(g, x, n, h, w, weights, strides=strides, xb=xb), None
     oh, ow = g.out_hw(h, w)
     out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
     stats = torch.empty(nt * (1 + 2 * g.cout), device=x.device, dtype=torch.float32)
-    _OP.conv2d_fwd_bnstats(x, list(weights), out, stats, (n, g.cin, h, w), strides, _wshape(g), g.stride,
+    _OP.conv2d_fwd_bnstats(x, xb, list(weights), out, stats, (n, g.cin, h, w), strides, _wshape(g), g.stride,
                            g.pads, g.dils, nt)
     return out, (stats, nt)
 
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
-               res=None, aux=None, flags: int = 0) -> torch.Tensor:
+               res=None, aux=None, flags: int = 0, dyb=None) -> torch.Tensor:
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD)."""
     if out is None:
         out = torch.empty((n, h, w, g.cin), device=dy.device, dtype=torch.float32)
@@ -142,59 +143,75 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
         flags |= EPI_RESIDUAL
     if aux is not None and not flags & EPI_RELU_GRAD:
         flags |= EPI_LEAKY_GRAD
-    _OP.conv2d_bwd_data(dy, list(weights), res, aux, out, (n, g.cin, h, w), _wshape(g), g.stride, g.pads,
+    _OP.conv2d_bwd_data(dy, dyb, list(weights), res, aux, out, (n, g.cin, h, w), _wshape(g), g.stride, g.pads,
                         g.dils, flags)
     return out
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
-               dbs=None, strides=None, accumulate: bool = True) -> None:
-    """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy."""
+               dbs=None, strides=None, accumulate: bool = True, dyb=None, xb=None) -> None:
+    """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy.  dyb / xb: bf16 copies of both
+    operands (bf16 conv math; used only together)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
-    _OP.conv2d_bwd_weight(dy, x, list(dws), list(dbs) if dbs is not None else [], (n, g.cin, h, w), strides,
+    if dyb is None or xb is None:
+        dyb = xb = None
+    _OP.conv2d_bwd_weight(dy, dyb, x, xb, list(dws), list(dbs) if dbs is not None else [], (n, g.cin, h, w), strides,
                           _wshape(g), g.stride, g.pads, g.dils, EPI_ACCUMULATE if accumulate else 0)
 
 
 # ---------------------------------------------------------------------------------------
 # BatchNorm (x as [rows, C])
 # ---------------------------------------------------------------------------------------
+def _bf16_like(t, want):
+    return torch.empty(t.shape, device=t.device, dtype=torch.bfloat16) if want else None
+
+
 def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                 relu=True, out=None):
+                 relu=True, out=None, bf16_out=False):
+    """bf16_out: also return a bf16 (RNE) copy of y, the operand of a bf16-math conv: (y, mean,
+    invstd, yb)."""
     c = x.shape[-1]
     y = torch.empty_like(x) if out is None else out
+    yb = _bf16_like(y, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
-    _OP.bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, mean, invstd, float(momentum),
+    _OP.bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, float(momentum),
                      float(eps), int(relu))
-    return y, mean, invstd
+    return (y, mean, invstd, yb) if bf16_out else (y, mean, invstd)
 
 
 def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                       relu=True, out=None):
+                       relu=True, out=None, bf16_out=False):
     """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles."""
     stats, ntiles = tiles
     c = x.shape[-1]
     y = torch.empty_like(x) if out is None else out
+    yb = _bf16_like(y, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
-    _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, mean,
+    _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, yb, mean,
                            invstd, float(momentum), float(eps), int(relu))
-    return y, mean, invstd
+    return (y, mean, invstd, yb) if bf16_out else (y, mean, invstd)
 
 
-def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None):
+def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None,
+                 bf16_out=False):
     y = torch.empty_like(x) if out is None else out
-    _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, float(eps), int(relu))
-    return y
+    yb = _bf16_like(y, bf16_out)
+    _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, float(eps), int(relu))
+    return (y, yb) if bf16_out else y
 
 
-def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None):
+def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None,
+           bf16_out=False):
     """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy.
-    y=None with relu (train mode): the mask is recomputed from x, weight and bias."""
+    y=None with relu (train mode): the mask is recomputed from x, weight and bias.
+    bf16_out: return (dx, dxb) with a bf16 (RNE) copy of dx (a bf16-math data-gradient operand)."""
     if dx is None:
         dx = torch.empty_like(dy)
-    _OP.bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dres, int(relu), bool(train))
-    return dx
+    dxb = _bf16_like(dx, bf16_out)
+    _OP.bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
+    return (dx, dxb) if bf16_out else dx
 
 
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2   # the BN entry points' activation codes

@@ -147,49 +147,49 @@ def _op(schema):
 
 
 # ---- convolution ------------------------------------------------------------------------
-@_op("conv2d_fwd(Tensor x, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, int[] in_shape, "
-     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_fwd(x, weight, bias, res, out, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+@_op("conv2d_fwd(Tensor x, Tensor? xb, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, "
+     "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_fwd(x, xb, weight, bias, res, out, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_FWD], x.device)
-    check(_lib.lib().adaptseg_conv2d_fwd(
-        ctypes.byref(d), _p(x), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out), flags,
-        wp, wsz, _stream()), "conv2d_fwd")
+    check(_lib.lib().adaptseg_conv2d_fwd_x(
+        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out),
+        flags, wp, wsz, _stream()), "conv2d_fwd")
 
 
-@_op("conv2d_fwd_bnstats(Tensor x, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, int[] in_shape, "
-     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int ntiles) -> ()")
-def _conv2d_fwd_bnstats(x, weight, out, stats, in_shape, in_stride, w_shape, stride, pad, dil, ntiles):
+@_op("conv2d_fwd_bnstats(Tensor x, Tensor? xb, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, "
+     "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int ntiles) -> ()")
+def _conv2d_fwd_bnstats(x, xb, weight, out, stats, in_shape, in_stride, w_shape, stride, pad, dil, ntiles):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_FWD], x.device)
     nt = ctypes.c_int(0)
-    check(_lib.lib().adaptseg_conv2d_fwd_bnstats(
-        ctypes.byref(d), _p(x), _ptrs(weight), _p(out), _p(stats), ctypes.c_size_t(stats.numel() * 4),
+    check(_lib.lib().adaptseg_conv2d_fwd_bnstats_x(
+        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(out), _p(stats), ctypes.c_size_t(stats.numel() * 4),
         ctypes.byref(nt), wp, wsz, _stream()), "conv2d_fwd_bnstats")
     if nt.value != ntiles:
         raise RuntimeError(f"conv2d_fwd_bnstats: planned {ntiles} statistics tiles, the launch produced "
                            f"{nt.value} (unaligned operand?)")
 
 
-@_op("conv2d_bwd_data(Tensor dy, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, int[] in_shape, "
-     "int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_bwd_data(dy, weight, res, aux, dx, in_shape, w_shape, stride, pad, dil, flags):
+@_op("conv2d_bwd_data(Tensor dy, Tensor? dyb, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, "
+     "int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_bwd_data(dy, dyb, weight, res, aux, dx, in_shape, w_shape, stride, pad, dil, flags):
     n, c, h, w = in_shape
     d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
-    check(_lib.lib().adaptseg_conv2d_bwd_data(
-        ctypes.byref(d), _p(dy), _ptrs(weight), _p(res), _p(aux), _p(dx), flags, wp, wsz, _stream()),
+    check(_lib.lib().adaptseg_conv2d_bwd_data_x(
+        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(res), _p(aux), _p(dx), flags, wp, wsz, _stream()),
         "conv2d_bwd_data")
 
 
-@_op("conv2d_bwd_weight(Tensor dy, Tensor x, Tensor(a!)[] dw, Tensor(b!)[] db, int[] in_shape, "
-     "int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_bwd_weight(dy, x, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+@_op("conv2d_bwd_weight(Tensor dy, Tensor? dyb, Tensor x, Tensor? xb, Tensor(a!)[] dw, Tensor(b!)[] db, "
+     "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_bwd_weight(dy, dyb, x, xb, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dy.device)
-    check(_lib.lib().adaptseg_conv2d_bwd_weight(
-        ctypes.byref(d), _p(dy), _p(x), _ptrs(dw), _ptrs(db) if len(db) else None, flags, wp, wsz,
-        _stream()), "conv2d_bwd_weight")
+    check(_lib.lib().adaptseg_conv2d_bwd_weight_x(
+        ctypes.byref(d), _p(dy), _p(dyb), _p(x), _p(xb), _ptrs(dw), _ptrs(db) if len(db) else None, flags, wp,
+        wsz, _stream()), "conv2d_bwd_weight")
 
 
 # ---- batch norm (x as [rows, C]: the NHWC buffer) ------------------------------------------
@@ -211,44 +211,45 @@ def _rc(t):
 
 
 @_op("bn_fwd_train(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-     "Tensor? res, Tensor(c!) y, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
-def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, mean, invstd, momentum, eps, act):
+     "Tensor? res, Tensor(c!) y, Tensor(f!)? yb, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, "
+     "int act) -> ()")
+def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, momentum, eps, act):
     rows, c = _rc(x)
     wp, wsz = _ws_args(bn_ws_bytes(rows, c), x.device)
-    check(_lib.lib().adaptseg_bn_fwd_train(
+    check(_lib.lib().adaptseg_bn_fwd_train_x(
         rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(momentum), float(eps),
-        _p(mean), _p(invstd), _p(res), _p(y), int(act), wp, wsz, _stream()), "bn_fwd_train")
+        _p(mean), _p(invstd), _p(res), _p(y), _p(yb), int(act), wp, wsz, _stream()), "bn_fwd_train")
 
 
 @_op("bn_fwd_train_tiles(Tensor x, Tensor stats, int ntiles, Tensor? weight, Tensor? bias, "
-     "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!) y, Tensor(d!) mean, "
-     "Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
-def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, mean, invstd,
+     "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!) y, Tensor(f!)? yb, "
+     "Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
+def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, yb, mean, invstd,
                         momentum, eps, act):
     rows, c = _rc(x)
-    check(_lib.lib().adaptseg_bn_fwd_train_tiles(
+    check(_lib.lib().adaptseg_bn_fwd_train_tiles_x(
         rows, c, _p(stats), int(ntiles), _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
-        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), int(act), _stream()),
+        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), _p(yb), int(act), _stream()),
         "bn_fwd_train_tiles")
 
 
 @_op("bn_fwd_infer(Tensor x, Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
-     "Tensor? res, Tensor(a!) y, float eps, int act) -> ()")
-def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, eps, act):
+     "Tensor? res, Tensor(a!) y, Tensor(b!)? yb, float eps, int act) -> ()")
+def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, act):
     rows, c = _rc(x)
-    check(_lib.lib().adaptseg_bn_fwd_infer(
+    check(_lib.lib().adaptseg_bn_fwd_infer_x(
         rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps), _p(res), _p(y),
-        int(act), _stream()), "bn_fwd_infer")
+        _p(yb), int(act), _stream()), "bn_fwd_infer")
 
 
 @_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
-     "Tensor(a!) dx, Tensor(b!)? dres, int act, bool train) -> ()")
-def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dres, act, train):
+     "Tensor(a!) dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
+def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
     rows, c = _rc(dy)
     wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)
-    check(_lib.lib().adaptseg_bn_bwd(
-        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dres), int(act),
-        1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+    check(_lib.lib().adaptseg_bn_bwd_x(
+        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dxb), _p(dres),
+        int(act), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
 
 
 @_op("bn_bwd_affine(Tensor dy, Tensor? y, Tensor x, Tensor? weight, Tensor? bias, Tensor mean, "

@@ -162,7 +162,7 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
 
 def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
-    if sel % 100 >= 95:
+    if sel % 100 in (95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
     if sel % 100 >= 90:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
@@ -171,8 +171,13 @@ def kernel_peak(sel):
 
 def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
-    if sel % 100 >= 95:
+    if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
+    if sel % 100 in (94, 97, 98, 99):   # the bf16 LDS-DMA kernels (conv_bf16g.hpp)
+        if op == 2:
+            return "igemm_bf16g_wgrad_kernel<32>"
+        bm, bn = (128, 256) if var in (4, 7) else (256, 128)
+        return f"igemm_bf16g_kernel<{op}, {bm}, {bn}, {64 if var in (7, 8) else 32}>"
     if cfg == 9:
         return f"igemm_bf16_kernel<{op}, {'true' if var & 1 else 'false'}, {256 if var & 2 else 128}>"
     bm, bn, wm, wn, bk = _CFG[cfg]

@@ -111,6 +111,31 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
                                 float *y, float *stats, size_t stats_bytes, int *ntiles, void *ws,
                                 size_t ws_bytes, adaptseg_stream_t stream);
 
+/* bf16 operand copies (conv math ADAPTSEG_MATH_BF16, config c5).  The _x forms take, beside
+   the fp32 activation operand, an optional bf16 (RNE) copy of it as written by the producing
+   BatchNorm pass (adaptseg_bn_*_x): contiguous NHWC, 16-byte aligned; NULL = none.  The bf16
+   LDS-DMA kernel (forward and stride-1 data gradient with N >= 128) then reads it instead of
+   converting the operand itself, one pass over the activation less per call; every other
+   kernel ignores it.  The results are bitwise those of the plain forms (the copy holds
+   exactly the values the kernel would have rounded).  Same interfaces otherwise
+   (model/deeplab_multi.py:83-103: the Bottleneck convs consume BN+ReLU outputs). */
+int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                          const float *const *w, const float *const *bias, const float *res, float *y,
+                          int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                                  const float *const *w, float *y, float *stats, size_t stats_bytes,
+                                  int *ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                               const float *const *w, const float *res, const float *aux, float *dx,
+                               int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+/* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
+   forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
+   (Cin % 128 == 0) reads them; other kernels ignore them. */
+int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                 const float *x, const uint16_t *x_bf16, float *const *dw,
+                                 float *const *db, int flags, void *ws, size_t ws_bytes,
+                                 adaptseg_stream_t stream);
+
 /* dx[n,h,w,c] = conv_transpose(dy, w)  (NHWC, contiguous).  aux: LEAKY_/RELU_GRAD source. */
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
@@ -147,6 +172,22 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                 float *save_invstd, const float *res, float *y, int relu,
                                 adaptseg_stream_t stream);
 
+/* The forward BN passes with an optional bf16 (RNE) copy of y written beside it (y_bf16,
+   contiguous [rows][c], NULL = none): the operand of the next conv under bf16 conv math. */
+int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                            float *running_mean, float *running_var, float momentum, float eps,
+                            float *save_mean, float *save_invstd, const float *res, float *y,
+                            uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                  const float *weight, const float *bias, float *running_mean,
+                                  float *running_var, float momentum, float eps, float *save_mean,
+                                  float *save_invstd, const float *res, float *y, uint16_t *y_bf16,
+                                  int relu, adaptseg_stream_t stream);
+int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                            const float *running_mean, const float *running_var, float eps,
+                            const float *res, float *y, uint16_t *y_bf16, int relu,
+                            adaptseg_stream_t stream);
+
 /* Eval-mode BN (running statistics): y = (x-rm)/sqrt(rv+eps)*w + b (+res), ReLU if relu. */
 int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight,
                           const float *bias, const float *running_mean, const float *running_var,
@@ -162,6 +203,13 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     const float *weight, const float *bias, const float *save_mean,
                     const float *save_invstd, float *dx, float *dres, int relu, int train,
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+
+/* adaptseg_bn_bwd with an optional bf16 (RNE) copy of dx (dx_bf16, NULL = none): the
+   data-gradient operand of the conv that produced x, under bf16 conv math. */
+int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const float *x,
+                      const float *weight, const float *bias, const float *save_mean,
+                      const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu,
+                      int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's
    NaiveConvolution norms, model/custom_layers.py:25-33): additionally dbias[c] += sum(g),

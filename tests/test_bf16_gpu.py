@@ -175,3 +175,37 @@ def test_c5_multilevel_ls_step_bf16(bf16_math):
         f, c = frob(_updates(None, keys, g0, sd), _updates(G, keys, g0))
         print(f"bf16 {gname} update: rel-frob {f:.3e} cos {c:.6f}")
         assert c >= 0.99, (gname, f, c)
+
+
+def test_bf16_operand_copies_are_bitwise_neutral(bf16_math):
+    """The BN passes' bf16 copies (bn_* bf16_out) equal y.to(bfloat16) exactly, and a conv fed
+    the copy (conv_fwd / conv_dgrad ``xb`` / ``dyb``: the LDS-DMA kernel reads it instead of
+    converting the fp32 operand itself) returns bitwise the result of the plain call."""
+    k = bf16_math
+    g = torch.Generator().manual_seed(21)
+    n, h, w, c, cout = 2, 24, 40, 128, 256
+    geom = k.ConvGeom(c, cout, 3, 3, 1, (2,), (2,))
+    x = torch.randn(n, h, w, c, generator=g).to(DEV)
+    bw, bb = torch.randn(c, generator=g).to(DEV), torch.randn(c, generator=g).to(DEV)
+    rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    y, mean, invstd, yb = k.bn_fwd_train(x, bw, bb, rm, rv, 0.1, 1e-5, relu=True, bf16_out=True)
+    assert torch.equal(yb, y.to(torch.bfloat16))
+    yi, ybi = k.bn_fwd_infer(x, bw, bb, rm, rv, 1e-5, relu=True, bf16_out=True)
+    assert torch.equal(ybi, yi.to(torch.bfloat16))
+    wt = [(torch.randn(cout, 3, 3, c, generator=g) * 0.05).to(DEV)]
+    kid, sp = k.conv_kernel_id(geom, n, h, w, 0)
+    assert kid % 100 in (94, 97, 98, 99), kid   # the LDS-DMA kernel
+    assert torch.equal(k.conv_fwd(geom, y, n, h, w, wt, xb=yb), k.conv_fwd(geom, y, n, h, w, wt))
+    gy = torch.randn(n, h, w, cout, generator=g).to(DEV)
+    dx, dxb = k.bn_bwd(gy, None, x if cout == c else torch.randn(n, h, w, cout, generator=g).to(DEV),
+                       torch.ones(cout, device=DEV), torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV),
+                       relu=False, train=False, bf16_out=True)
+    assert torch.equal(dxb, dx.to(torch.bfloat16))
+    assert torch.equal(k.conv_dgrad(geom, dx, n, h, w, wt, dyb=dxb), k.conv_dgrad(geom, dx, n, h, w, wt))
+    # weight gradient on bf16 copies of both operands: bitwise the plain call's result
+    assert k.conv_kernel_id(geom, n, h, w, 2)[0] % 100 == 99   # the LDS-DMA weight-gradient kernel
+    dw0 = [torch.zeros_like(wt[0])]
+    dw1 = [torch.zeros_like(wt[0])]
+    k.conv_wgrad(geom, gy, y, n, h, w, dw0, accumulate=False)
+    k.conv_wgrad(geom, gy, y, n, h, w, dw1, accumulate=False, dyb=gy.to(torch.bfloat16), xb=yb)
+    assert torch.equal(dw0[0], dw1[0])
