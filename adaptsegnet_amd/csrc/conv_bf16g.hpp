@@ -232,18 +232,21 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
 // Weight gradient on the same LDS-DMA ring: dW[co][tap, ci] = sum_pix dY[pix][co] x[pix+tap][ci]
 // with both operands bf16 copies in HBM (dY: the producing BN backward's copy, x: the forward
 // BN's).  k = output pixel, so both images are M/N-contiguous [32 k][128] (conv_bf16.hpp's
-// 256-B rows, read with ds_read_b64_tr_b16); one LDS-DMA instruction fills 4 k-rows, so each of
-// the 8 waves issues one A and one B instruction per K step of 32 pixels.  A 128-column tile
-// lies in one tap (Cin % 128 == 0), so a k-row of B is one contiguous 256-B run of x or, for a
-// tap outside the image, zeros.  3 x 16 KB ring, two blocks per CU.
-template <int BKP>
+// 256-B rows, read with ds_read_b64_tr_b16; BM 256 = two A images); one LDS-DMA instruction
+// fills 4 k-rows, so a K step of 32 pixels is BM/128 A and one B instruction per wave.  A
+// 128-column tile lies in one tap (Cin % 128 == 0), so a k-row of B is one contiguous 256-B run
+// of x or, for a tap outside the image, zeros.  BM 256 (Cout >= 256) reads dY once per column
+// tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
+// KB, two blocks per CU.
+template <int BM>
 __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvParams p, const __bf16 *__restrict__ dyb,
                                                                     const __bf16 *__restrict__ xb) {
-  static_assert(BKP == 32, "one A and one B instruction per wave and K step");
-  constexpr int BM = 128, BN = 128, WAVES_M = 2, WAVES_N = 4;
-  constexpr int WTM = 64, WTN = 32, TM = 2, TN = 1;
-  constexpr int IMG = BKP * 256;              // [32 k][128] bf16
-  constexpr int STAGE = 2 * IMG;
+  constexpr int BKP = 32, BN = 128;
+  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  constexpr int WTM = 64, WTN = BN / WAVES_N, TM = 2, TN = WTN / 32;
+  constexpr int NA = BM / 128;                // A images / instructions per wave and K step
+  constexpr int IMG = BKP * 256;              // one [32 k][128] bf16 image
+  constexpr int STAGE = (NA + 1) * IMG;
 
   __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
 
@@ -265,7 +268,9 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
   // position (mc_off) is that slot
   const int kr = 4 * wave + (lane >> 4);
   const int chs = ((lane & 15) ^ (((kr & 3) << 2) | ((kr >> 2) & 3))) * 8;
-  const bool a_col = bm + chs < p.M;          // Cout % 8 == 0: a chunk is all in or all out
+  bool a_col[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) a_col[i] = bm + 128 * i + chs < p.M;   // Cout % 8 == 0
   const int tap = uni((int)fdiv((uint32_t)bn, p.fd_c));
   int seg, t, tdy, tdx;
   seg_geom(p, sr, tap, seg, t, tdy, tdx);
@@ -286,8 +291,10 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
     const int oh = (int)q - (int)b * p.oh;
     const int iy = oh * p.stride + tdy, ix = ow * p.stride + tdx;
     const bool bv = rv & b_col & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
-    glds16(rv & a_col ? dyb + (size_t)mm * p.k + bm + chs : zero, As);
-    glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci : zero, As + IMG);
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      glds16(rv & a_col[i] ? dyb + (size_t)mm * p.k + bm + 128 * i + chs : zero, As + i * IMG);
+    glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci : zero, As + NA * IMG);
   };
 
   const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
@@ -300,12 +307,13 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto compute = [&](int st) {
-    const char *As = lds + st * STAGE;
-    const char *Bs = As + IMG;
+    const char *Ai = lds + st * STAGE + (wm * WTM / 128) * IMG;   // the A image of this wave's rows
+    const char *Bs = lds + st * STAGE + NA * IMG;
+    const int ar = (wm * WTM) % 128;
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[slot][i] = mc_frag(As, wm * WTM + i * 32, ks, lane);
+      for (int i = 0; i < TM; ++i) a[slot][i] = mc_frag(Ai, ar + i * 32, ks, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) b[slot][j] = mc_frag(Bs, wn * WTN + j * 32, ks, lane);
     };
@@ -328,7 +336,9 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
     issue(min(kt0 + 1, klast), 1);
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // step kt landed, kt+1 in flight
+      // step kt landed, step kt+1's NA + 1 instructions in flight
+      if constexpr (NA == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       issue(min(kt + 2, klast), st == 0 ? 2 : st - 1);
       compute(st);

@@ -487,7 +487,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // weight-gradient kernel: 128x128 tiles, K steps of 32 output pixels
     if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 128 == 0 && d->k % 8 == 0) {
       pl.g16 = true;
-      pl.g16_bm = pl.g16_bn = 128;
+      pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
+      pl.g16_bn = 128;
       pl.g16_bk = 32;
     }
   }
@@ -504,6 +505,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
+  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);

@@ -123,7 +123,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(
                                              base + al256(g16_act_elems(pl) * sizeof(__bf16)));
-      igemm_bf16g_wgrad_kernel<32><<<grid, block, 0, s>>>(p, act, act2);
+      if (pl.g16_bm == 256) igemm_bf16g_wgrad_kernel<256><<<grid, block, 0, s>>>(p, act, act2);
+      else igemm_bf16g_wgrad_kernel<128><<<grid, block, 0, s>>>(p, act, act2);
       return hipGetLastError();
     }
 #define G16_LAUNCH(MODE_, BK_)                                                                  \

@@ -175,7 +175,7 @@ def selector_symbol(sel):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
     if sel % 100 in (94, 97, 98, 99):   # the bf16 LDS-DMA kernels (conv_bf16g.hpp)
         if op == 2:
-            return "igemm_bf16g_wgrad_kernel<32>"
+            return f"igemm_bf16g_wgrad_kernel<{256 if var == 8 else 128}>"
         bm, bn = (128, 256) if var in (4, 7) else (256, 128)
         return f"igemm_bf16g_kernel<{op}, {bm}, {bn}, {64 if var in (7, 8) else 32}>"
     if cfg == 9:
