@@ -481,7 +481,7 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *we
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
   const ApplyPlan ap = apply_plan(rows, c);
-  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
+  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
                                                                  weight, bias, res, y,
                                                                  reinterpret_cast<uint2 *>(y_bf16), relu);
@@ -512,7 +512,7 @@ int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int n
   AS_CHECK_LAUNCH("bn_tiles_final");
   const ApplyPlan ap = apply_plan(rows, c);
   int slot;  // x (+res) in, y out
-  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2), &slot);
+  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
                                                                  weight, bias, res, y,
                                                                  reinterpret_cast<uint2 *>(y_bf16), relu);
@@ -587,7 +587,8 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   }
   // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
-               4.0 * rows * c * (2 + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)),
+               4.0 * rows * c * (2 + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)) +
+                   (dx_bf16 ? 2.0 * rows * c : 0.0),
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);
   bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, y, x, weight, bias,

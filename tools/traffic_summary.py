@@ -16,11 +16,26 @@ import sys
 root, sym = sys.argv[1], sys.argv[2]
 
 
+def mangled_key(name):
+    """'k<1, 128, 256>' -> 'kILi1ELi128ELi256E': rocprofv3 leaves symbols with bf16 (DF16b)
+    parameters mangled, so an integer-argument template is also matched in that form."""
+    if "<" not in name:
+        return None
+    base, args = name.split("<", 1)
+    parts = [a.strip() for a in args.rstrip(">").split(",")]
+    if not all(a.lstrip("-").isdigit() for a in parts):
+        return None
+    return base + "I" + "".join(f"Li{a}E" for a in parts) + "E"
+
+
+MKEY = mangled_key(sym)
+
+
 def per_launch(counter):
     vals = []
     for path in glob.glob(f"{root}/{counter}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(path)):
-            if r["Counter_Name"] == counter and sym in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter and (sym in r["Kernel_Name"] or (MKEY and MKEY in r["Kernel_Name"])):
                 vals.append(float(r["Counter_Value"]) * 1024.0)
     return sum(vals) / len(vals) if vals else None, len(vals)
 
