@@ -233,9 +233,9 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
 // with both operands bf16 copies in HBM (dY: the producing BN backward's copy, x: the forward
 // BN's).  k = output pixel, so both images are M/N-contiguous [32 k][128] (conv_bf16.hpp's
 // 256-B rows, read with ds_read_b64_tr_b16; BM 256 = two A images); one LDS-DMA instruction
-// fills 4 k-rows, so a K step of 32 pixels is BM/128 A and one B instruction per wave.  A
-// 128-column tile lies in one tap (Cin % 128 == 0), so a k-row of B is one contiguous 256-B run
-// of x or, for a tap outside the image, zeros.  BM 256 (Cout >= 256) reads dY once per column
+// fills 4 k-rows, so a K step of 32 pixels is BM/128 A and one B instruction per wave.  Each
+// lane's 16-B column chunk (8 input channels, Cin % 8 == 0) has its own tap, so a 128-column
+// tile may span taps (Cin 64: two); a chunk of a tap outside the image loads zeros.  BM 256 (Cout >= 256) reads dY once per column
 // tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
 // KB, two blocks per CU.
 template <int BM>
@@ -271,13 +271,14 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
   bool a_col[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) a_col[i] = bm + 128 * i + chs < p.M;   // Cout % 8 == 0
-  const int tap = uni((int)fdiv((uint32_t)bn, p.fd_c));
+  // this lane's column chunk: its tap (per lane: with Cin % 128 != 0 a tile spans taps) and
+  // input channel
+  const bool b_col = bn + chs < p.N;
+  const int ncol = b_col ? bn + chs : 0;
+  const int tap = (int)fdiv((uint32_t)ncol, p.fd_c);
   int seg, t, tdy, tdx;
   seg_geom(p, sr, tap, seg, t, tdy, tdx);
-  tdy = uni(tdy);
-  tdx = uni(tdx);
-  const int ci = bn - tap * p.c + chs;
-  const bool b_col = bn + chs < p.N;
+  const int ci = ncol - tap * p.c;
   const __bf16 *zero = reinterpret_cast<const __bf16 *>(g_bf16g_zero);
 
   auto issue = [&](int kt, int st) {

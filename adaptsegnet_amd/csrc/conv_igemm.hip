@@ -483,9 +483,9 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = p.K >= 2048 ? 64 : 32;
     }
-    // weight gradients whose 128-column tiles lie in one tap (Cin % 128 == 0) on the LDS-DMA
-    // weight-gradient kernel: 128x128 tiles, K steps of 32 output pixels
-    if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 128 == 0 && d->k % 8 == 0) {
+    // weight gradients with 16-B channel chunks (Cin % 8 == 0, Cout % 8 == 0) on the LDS-DMA
+    // weight-gradient kernel: {128,256}x128 tiles, K steps of 32 output pixels
+    if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 8 == 0 && d->k % 8 == 0) {
       pl.g16 = true;
       pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
       pl.g16_bn = 128;

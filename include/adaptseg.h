@@ -130,7 +130,7 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
-   (Cin % 128 == 0) reads them; other kernels ignore them. */
+   (Cin and Cout multiples of 8) reads them; other kernels ignore them. */
 int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                  const float *x, const uint16_t *x_bf16, float *const *dw,
                                  float *const *db, int flags, void *ws, size_t ws_bytes,
