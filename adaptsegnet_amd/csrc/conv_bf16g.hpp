@@ -24,7 +24,7 @@
 namespace adaptseg {
 
 // 16 zero bytes: the source of every padded operand row
-__device__ __attribute__((aligned(16))) unsigned int g_bf16g_zero[4];
+static __device__ __attribute__((aligned(16))) unsigned int g_bf16g_zero[4];
 
 // One LDS-DMA wave instruction: lane l's 16 source bytes land at LDS byte lds_dst + 16 l.  In
 // inline asm, not __builtin_amdgcn_global_load_lds: hipcc (ROCm 7.2) cannot tell the DMA's LDS
@@ -216,6 +216,7 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
       // ... and after the barrier every wave's are, and every wave has finished reading the
       // stage that step kt+2 overwrites (step kt-1's)
       __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");   // no LDS access moves above the barrier
       const int st2 = st == 0 ? 2 : st - 1;  // (st + 2) % 3
       issue(min(kt + 2, klast), st2);
       compute(st);
@@ -341,6 +342,7 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
       if constexpr (NA == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");   // no LDS access moves above the barrier
       issue(min(kt + 2, klast), st == 0 ? 2 : st - 1);
       compute(st);
       st = st == 2 ? 0 : st + 1;
