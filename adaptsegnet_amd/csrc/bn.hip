@@ -272,7 +272,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__rest
       float t = (o[j] - rm[c + j]) * is * (w ? w[c + j] : 1.f) + (b ? b[c + j] : 0.f) + r4[j];
       o[j] = fwd_act(t, relu);
     }
-    reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    if (y) reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
     if (yb) yb[i] = bf16x4_rne(make_float4(o[0], o[1], o[2], o[3]));
   }
 }
@@ -318,7 +318,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, cons
       o.y = fwd_act(bn_affine(v[u].y, m.y, is.y, ww.y, bb.y) + q[u].y, act);
       o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
       o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
-      st4(y + ru * C + c0, o);
+      if (y) st4(y + ru * C + c0, o);
       if (yb) yb[(ru * C + c0) >> 2] = bf16x4_rne(o);
     }
   }
@@ -383,7 +383,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
       } else {
         out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
       }
-      st4(dx + e, out);
+      if (dx) st4(dx + e, out);
       if (dxb) dxb[e >> 2] = bf16x4_rne(out);
     }
   }
@@ -461,7 +461,7 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *we
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
-  AS_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: null pointer");
+  AS_CHECK_ARG(x && (y || y_bf16) && save_mean && save_invstd, "bn_fwd_train: null pointer");
   size_t need = bn_ws_bytes(rows, c);
   if (!ws || ws_bytes < need) {
     set_error("bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
@@ -481,7 +481,7 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *we
                                                                    momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
   const ApplyPlan ap = apply_plan(rows, c);
-  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
+  timing_begin(kTBnApply, s, 4.0 * rows * c * ((res ? 2 : 1) + (y ? 1 : 0)) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
                                                                  weight, bias, res, y,
                                                                  reinterpret_cast<uint2 *>(y_bf16), relu);
@@ -504,7 +504,8 @@ int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int n
                                   const float *res, float *y, uint16_t *y_bf16, int relu,
                                   adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
-  AS_CHECK_ARG(stats && ntiles > 0 && x && y && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
+  AS_CHECK_ARG(stats && ntiles > 0 && x && (y || y_bf16) && save_mean && save_invstd,
+               "bn_fwd_train_tiles: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
   hipStream_t s = as_stream(stream);
   bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
@@ -512,7 +513,7 @@ int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int n
   AS_CHECK_LAUNCH("bn_tiles_final");
   const ApplyPlan ap = apply_plan(rows, c);
   int slot;  // x (+res) in, y out
-  timing_begin(kTBnApply, s, 4.0 * rows * c * (res ? 3 : 2) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
+  timing_begin(kTBnApply, s, 4.0 * rows * c * ((res ? 2 : 1) + (y ? 1 : 0)) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
   bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
                                                                  weight, bias, res, y,
                                                                  reinterpret_cast<uint2 *>(y_bf16), relu);
@@ -533,7 +534,7 @@ int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const float *we
                             const float *running_mean, const float *running_var, float eps, const float *res,
                             float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
-  AS_CHECK_ARG(x && y && running_mean && running_var, "bn_fwd_infer: null pointer");
+  AS_CHECK_ARG(x && (y || y_bf16) && running_mean && running_var, "bn_fwd_infer: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
   hipStream_t s = as_stream(stream);
   int64_t total4 = rows * c / 4;
@@ -555,7 +556,7 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
                        uint16_t *dx_bf16, float *dres, int relu, int train, float *dweight, float *dbias, void *ws,
                        size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
-  AS_CHECK_ARG(dy && dx && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
+  AS_CHECK_ARG(dy && (dx || dx_bf16) && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
   AS_CHECK_ARG(!relu || y || train, "bn_bwd: activation without y needs train mode (mask from x)");
   AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
@@ -587,7 +588,7 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   }
   // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
-               4.0 * rows * c * (2 + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)) +
+               4.0 * rows * c * (1 + (dx ? 1 : 0) + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)) +
                    (dx_bf16 ? 2.0 * rows * c : 0.0),
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);

@@ -653,7 +653,9 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
-  AS_CHECK_ARG(x && w && y, "conv fwd: null pointer");
+  AS_CHECK_ARG((x || x_bf16) && w && y, "conv fwd: null pointer");
+  AS_CHECK_ARG(x || (pl.g16 && !use_thin(d, ADAPTSEG_CONV_FWD) && !tapgemm_eligible(d)),
+               "conv fwd: this product needs the fp32 input (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & kEpiActGrad), "conv fwd: *_GRAD flags not valid");
   AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv fwd: residual flag without res");
@@ -717,7 +719,9 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
-  AS_CHECK_ARG(x && w && y, "conv fwd_bnstats: null pointer");
+  AS_CHECK_ARG((x || x_bf16) && w && y, "conv fwd_bnstats: null pointer");
+  AS_CHECK_ARG(x || (pl.g16 && !tapgemm_eligible(d)),
+               "conv fwd_bnstats: this product needs the fp32 input (no bf16-operand kernel for it)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
   if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
     return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, y, 0, ws, ws_bytes, stream);
@@ -755,7 +759,9 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
-  AS_CHECK_ARG(dy && w && dx, "conv bwd_data: null pointer");
+  AS_CHECK_ARG((dy || dy_bf16) && w && dx, "conv bwd_data: null pointer");
+  AS_CHECK_ARG(dy || (pl.g16 && !use_thin(d, ADAPTSEG_CONV_BWD_DATA) && !tapgemm_eligible(d)),
+               "conv bwd_data: this product needs the fp32 dY (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY | ADAPTSEG_EPI_RELU)), "conv bwd_data: LEAKY/RELU not valid");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv bwd_data: residual flag without res");
   AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
@@ -796,7 +802,10 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_WEIGHT, pl);
   if (st) return st;
-  AS_CHECK_ARG(dy && x && dw, "conv bwd_weight: null pointer");
+  AS_CHECK_ARG((dy || dy_bf16) && (x || x_bf16) && dw, "conv bwd_weight: null pointer");
+  AS_CHECK_ARG((dy && x) || (dy_bf16 && x_bf16 && pl.g16 && !db && !use_thin(d, ADAPTSEG_CONV_BWD_WEIGHT) &&
+                             !tapgemm_eligible(d)),
+               "conv bwd_weight: this product needs the fp32 operands (no bf16-operand kernel / bias gradient)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
   hipStream_t s = as_stream(stream);
   int thin_st = ADAPTSEG_ERR_ARG;

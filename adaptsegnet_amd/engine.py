@@ -80,15 +80,35 @@ def bf16_operands() -> bool:
     return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
 
 
-def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False):
-    """bn_forward that also returns the bf16 copy of y (None unless ``bf16``)."""
+_BF16_SEL: dict = {}
+
+
+def bf16_only(g, n, h, w, ops) -> bool:
+    """True when every listed product of this conv runs on a bf16-operand LDS-DMA kernel
+    (selectors 94 / 97-99), which reads only the bf16 copy of its activation operand: the fp32
+    tensor then need not be written at all."""
+    for op in ops:
+        key = (g, n, h, w, op, K.get_conv_math())
+        v = _BF16_SEL.get(key)
+        if v is None:
+            kid, _ = K.conv_kernel_id(g, n, h, w, op)
+            v = _BF16_SEL[key] = kid // 10 % 10 == 9 and kid % 10 in (4, 7, 8, 9)
+        if not v:
+            return False
+    return True
+
+
+def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False, fp32=True):
+    """bn_forward that also returns the bf16 copy of y (None unless ``bf16``); fp32=False skips
+    the fp32 y (returned as None) when every consumer reads the copy."""
+    fp32 = fp32 or not bf16
     if training:
         if tiles is not None:
             r = K.bn_fwd_train_tiles(x, tiles, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                     bn.momentum, bn.eps, res=res, relu=relu, bf16_out=bf16)
+                                     bn.momentum, bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32)
         else:
             r = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
-                               bn.eps, res=res, relu=relu, bf16_out=bf16)
+                               bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32)
         y, mean, invstd = r[:3]
         return y, (mean, invstd, True), (r[3] if bf16 else None)
     r = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
@@ -104,7 +124,7 @@ def bn_forward(bn, x, res, relu, training, tiles=None):
     return y, st
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False, fp32=True):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
     mode instead of reading the saved output y (one activation read less per pass).
     bf16: return (dx, bf16 copy of dx) for the bf16-math data gradient that consumes dx."""
@@ -114,7 +134,7 @@ def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, b
     elif mask_from_x and relu:
         y = None
     return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train,
-                    bias=bn.bias, bf16_out=bf16)
+                    bias=bn.bias, bf16_out=bf16, fp32_out=fp32 or not bf16)
 
 
 # ---------------------------------------------------------------------------------------
@@ -142,10 +162,15 @@ def block_forward(blk, x, n, h, w, training, save, xb=None):
     oh, ow = g1.out_hw(h, w)
     conv = _conv_bn if training else _conv_plain
     sh = bf16_operands()
+    # train mode (the BN backward recomputes its ReLU mask from x): y1 / y2 are read only by the
+    # next conv's forward and weight gradient — with both on bf16-operand kernels, only their
+    # bf16 copies are written
+    thin1 = sh and training and bf16_only(g2, n, oh, ow, (0, 2))
+    thin2 = sh and training and bf16_only(g3, n, oh, ow, (0, 2))
     c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb)
-    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh)
+    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh, fp32=not thin1)
     c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b)
-    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh)
+    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
     c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b)
     cd = sd = None
     if blk.downsample is not None:
@@ -217,30 +242,43 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
     sh = bf16_operands()   # bf16 copies of each data-gradient operand (bf16 conv math)
-    r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh)
+    train = rec.s3[2]
+    # a BN-backward output read only by bf16-operand data / weight gradients: copy only
+    f3 = not (sh and train and bf16_only(g3, n, oh, ow, (1, 2)))
+    f2 = not (sh and train and bf16_only(g2, n, oh, ow, (1, 2)))
+    f1 = not (sh and train and rec.xb is not None and bf16_only(g1, n, h, w, (1, 2)))
+    r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
     dc3, dc3b = r if sh else (r, None)
     dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b)
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
-    r = bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, bf16=sh)
+    r = bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, bf16=sh,
+                    fp32=f2)
     dy2b = r[1] if sh else None
+    if not f2:
+        dy2 = None   # not written: its consumers read dy2b
     dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b)
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
-    r = bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, bf16=sh)
+    r = bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, bf16=sh,
+                    fp32=f1)
     dy1b = r[1] if sh else None
+    if not f1:
+        dy1 = None
     if need_w and blk.conv1.weight.grad is not None:
         _wgrad(ws, g1, dy1, rec.x, n, h, w, [blk.conv1.weight.grad], dyb=dy1b, xb=rec.xb)
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
-        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout, bf16=sh)
+        fd = not (sh and train and rec.xb is not None and bf16_only(gd, n, h, w, (1, 2)))
+        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout, bf16=sh, fp32=fd)
         goutb = r[1] if sh else None
+        gd_in = gout if fd else None   # gout keeps the residual gradient when not rewritten
         if need_w and dconv.weight.grad is not None:
-            _wgrad(ws, gd, gout, rec.x, n, h, w, [dconv.weight.grad], dyb=goutb, xb=rec.xb)
-        dx = K.conv_dgrad(gd, gout, n, h, w, [dconv.weight], dyb=goutb)
+            _wgrad(ws, gd, gd_in, rec.x, n, h, w, [dconv.weight.grad], dyb=goutb, xb=rec.xb)
+        dx = K.conv_dgrad(gd, gd_in, n, h, w, [dconv.weight], dyb=goutb)
         del goutb
         K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE, dyb=dy1b)
     else:

@@ -104,7 +104,7 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, bias
     strides = strides or nhwc_strides(n, h, w, g.cin)
     oh, ow = g.out_hw(h, w)
     if out is None:
-        out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
+        out = torch.empty((n, oh, ow, g.cout), device=(x if x is not None else xb).device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
     _OP.conv2d_fwd(x, xb, list(weights), list(biases) if biases is not None else [], res, out, (n, g.cin, h, w),
@@ -127,8 +127,9 @@ def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weigh
     if nt == 0:
         return conv_fwd(g, x, n, h, w, weights, strides=strides, xb=xb), None
     oh, ow = g.out_hw(h, w)
-    out = torch.empty((n, oh, ow, g.cout), device=x.device, dtype=torch.float32)
-    stats = torch.empty(nt * (1 + 2 * g.cout), device=x.device, dtype=torch.float32)
+    dev = (x if x is not None else xb).device
+    out = torch.empty((n, oh, ow, g.cout), device=dev, dtype=torch.float32)
+    stats = torch.empty(nt * (1 + 2 * g.cout), device=dev, dtype=torch.float32)
     _OP.conv2d_fwd_bnstats(x, xb, list(weights), out, stats, (n, g.cin, h, w), strides, _wshape(g), g.stride,
                            g.pads, g.dils, nt)
     return out, (stats, nt)
@@ -138,7 +139,7 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
                res=None, aux=None, flags: int = 0, dyb=None) -> torch.Tensor:
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD)."""
     if out is None:
-        out = torch.empty((n, h, w, g.cin), device=dy.device, dtype=torch.float32)
+        out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
     if aux is not None and not flags & EPI_RELU_GRAD:
@@ -167,12 +168,12 @@ def _bf16_like(t, want):
 
 
 def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                 relu=True, out=None, bf16_out=False):
+                 relu=True, out=None, bf16_out=False, fp32_out=True):
     """bf16_out: also return a bf16 (RNE) copy of y, the operand of a bf16-math conv: (y, mean,
-    invstd, yb)."""
+    invstd, yb).  fp32_out=False (with bf16_out): only the copy is written, y is None."""
     c = x.shape[-1]
-    y = torch.empty_like(x) if out is None else out
-    yb = _bf16_like(y, bf16_out)
+    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
     _OP.bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, float(momentum),
@@ -181,12 +182,12 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=
 
 
 def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                       relu=True, out=None, bf16_out=False):
+                       relu=True, out=None, bf16_out=False, fp32_out=True):
     """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles."""
     stats, ntiles = tiles
     c = x.shape[-1]
-    y = torch.empty_like(x) if out is None else out
-    yb = _bf16_like(y, bf16_out)
+    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
     _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, yb, mean,
@@ -195,21 +196,24 @@ def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, moment
 
 
 def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None,
-                 bf16_out=False):
-    y = torch.empty_like(x) if out is None else out
-    yb = _bf16_like(y, bf16_out)
+                 bf16_out=False, fp32_out=True):
+    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    yb = _bf16_like(x, bf16_out)
     _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, float(eps), int(relu))
     return (y, yb) if bf16_out else y
 
 
 def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None,
-           bf16_out=False):
+           bf16_out=False, fp32_out=True):
     """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy.
     y=None with relu (train mode): the mask is recomputed from x, weight and bias.
-    bf16_out: return (dx, dxb) with a bf16 (RNE) copy of dx (a bf16-math data-gradient operand)."""
-    if dx is None:
+    bf16_out: return (dx, dxb) with a bf16 (RNE) copy of dx (a bf16-math data-gradient operand);
+    fp32_out=False (with bf16_out): only the copy is written, dx is None."""
+    if not (fp32_out or not bf16_out):
+        dx = None
+    elif dx is None:
         dx = torch.empty_like(dy)
-    dxb = _bf16_like(dx, bf16_out)
+    dxb = _bf16_like(dy, bf16_out)
     _OP.bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
     return (dx, dxb) if bf16_out else dx
 

@@ -147,21 +147,21 @@ def _op(schema):
 
 
 # ---- convolution ------------------------------------------------------------------------
-@_op("conv2d_fwd(Tensor x, Tensor? xb, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, "
+@_op("conv2d_fwd(Tensor? x, Tensor? xb, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, "
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_fwd(x, xb, weight, bias, res, out, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    wp, wsz = _ws_args(ws[CONV_FWD], out.device)
     check(_lib.lib().adaptseg_conv2d_fwd_x(
         ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out),
         flags, wp, wsz, _stream()), "conv2d_fwd")
 
 
-@_op("conv2d_fwd_bnstats(Tensor x, Tensor? xb, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, "
+@_op("conv2d_fwd_bnstats(Tensor? x, Tensor? xb, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, "
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int ntiles) -> ()")
 def _conv2d_fwd_bnstats(x, xb, weight, out, stats, in_shape, in_stride, w_shape, stride, pad, dil, ntiles):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_FWD], x.device)
+    wp, wsz = _ws_args(ws[CONV_FWD], out.device)
     nt = ctypes.c_int(0)
     check(_lib.lib().adaptseg_conv2d_fwd_bnstats_x(
         ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(out), _p(stats), ctypes.c_size_t(stats.numel() * 4),
@@ -171,22 +171,22 @@ def _conv2d_fwd_bnstats(x, xb, weight, out, stats, in_shape, in_stride, w_shape,
                            f"{nt.value} (unaligned operand?)")
 
 
-@_op("conv2d_bwd_data(Tensor dy, Tensor? dyb, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, "
+@_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, "
      "int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_bwd_data(dy, dyb, weight, res, aux, dx, in_shape, w_shape, stride, pad, dil, flags):
     n, c, h, w = in_shape
     d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dy.device)
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dx.device)
     check(_lib.lib().adaptseg_conv2d_bwd_data_x(
         ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(res), _p(aux), _p(dx), flags, wp, wsz, _stream()),
         "conv2d_bwd_data")
 
 
-@_op("conv2d_bwd_weight(Tensor dy, Tensor? dyb, Tensor x, Tensor? xb, Tensor(a!)[] dw, Tensor(b!)[] db, "
+@_op("conv2d_bwd_weight(Tensor? dy, Tensor? dyb, Tensor? x, Tensor? xb, Tensor(a!)[] dw, Tensor(b!)[] db, "
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_bwd_weight(dy, dyb, x, xb, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dy.device)
+    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dw[0].device)
     check(_lib.lib().adaptseg_conv2d_bwd_weight_x(
         ctypes.byref(d), _p(dy), _p(dyb), _p(x), _p(xb), _ptrs(dw), _ptrs(db) if len(db) else None, flags, wp,
         wsz, _stream()), "conv2d_bwd_weight")
@@ -211,7 +211,7 @@ def _rc(t):
 
 
 @_op("bn_fwd_train(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-     "Tensor? res, Tensor(c!) y, Tensor(f!)? yb, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, "
+     "Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, "
      "int act) -> ()")
 def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, momentum, eps, act):
     rows, c = _rc(x)
@@ -222,7 +222,7 @@ def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, 
 
 
 @_op("bn_fwd_train_tiles(Tensor x, Tensor stats, int ntiles, Tensor? weight, Tensor? bias, "
-     "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!) y, Tensor(f!)? yb, "
+     "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, "
      "Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
 def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, yb, mean, invstd,
                         momentum, eps, act):
@@ -234,7 +234,7 @@ def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_va
 
 
 @_op("bn_fwd_infer(Tensor x, Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
-     "Tensor? res, Tensor(a!) y, Tensor(b!)? yb, float eps, int act) -> ()")
+     "Tensor? res, Tensor(a!)? y, Tensor(b!)? yb, float eps, int act) -> ()")
 def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, act):
     rows, c = _rc(x)
     check(_lib.lib().adaptseg_bn_fwd_infer_x(
@@ -243,7 +243,7 @@ def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, a
 
 
 @_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
-     "Tensor(a!) dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
+     "Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
 def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
     rows, c = _rc(dy)
     wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)

@@ -209,3 +209,25 @@ def test_bf16_operand_copies_are_bitwise_neutral(bf16_math):
     k.conv_wgrad(geom, gy, y, n, h, w, dw0, accumulate=False)
     k.conv_wgrad(geom, gy, y, n, h, w, dw1, accumulate=False, dyb=gy.to(torch.bfloat16), xb=yb)
     assert torch.equal(dw0[0], dw1[0])
+
+
+def test_bf16_train_step_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monkeypatch):
+    """Train-mode BN under the bf16 conv math: the BN passes whose outputs feed only
+    bf16-operand kernels write only the bf16 copy (engine.bf16_only).  Two iterations of the
+    multi-level LS step with and without that skipping give bitwise the same losses and
+    parameters (the skipped fp32 tensors are never read)."""
+    from test_model_gpu import _run_hip, R
+    from adaptsegnet_amd import engine
+    xs = torch.from_numpy(R.det_images((2, 3, 41, 57), 11))
+    lab = torch.from_numpy(R.det_labels((2, 41, 57), 12))
+    xt = torch.from_numpy(R.det_images((2, 3, 33, 49), 13))
+    cfg = dict(level="multi-level", gan="LS", input_size=(57, 41), input_size_target=(49, 33))
+    # the skipping is live on this geometry: layer3's conv2 reads only bf16 copies
+    assert engine.bf16_only(bf16_math.ConvGeom(256, 256, 3, 3, 1, (2,), (2,)), 2, 6, 8, (0, 1, 2))
+    m_a, d1_a, d2_a, got_a = _run_hip("multi-level", "LS", cfg, (xs, lab, xt), 2, bn_train=True)
+    monkeypatch.setattr(engine, "bf16_only", lambda *a, **kw: False)
+    m_b, d1_b, d2_b, got_b = _run_hip("multi-level", "LS", cfg, (xs, lab, xt), 2, bn_train=True)
+    assert got_a == got_b, (got_a, got_b)
+    for ma, mb in ((m_a, m_b), (d1_a, d1_b), (d2_a, d2_b)):
+        for (ka, va), (kb, vb) in zip(ma.state_dict().items(), mb.state_dict().items()):
+            assert ka == kb and torch.equal(va, vb), ka
