@@ -27,9 +27,10 @@ hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   int rows_pad, ktot;
   x3_pack_dims(pl, rows_pad, ktot);
-  const unsigned pg = (unsigned)std::min<int64_t>(ceil_div((int64_t)rows_pad * ktot, 256), 8192);
-  if (pl.mode == MODE_FWD) conv_wpack_x3_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)wpack, rows_pad, ktot);
-  else if (pl.mode == MODE_DGRAD) conv_wpack_x3_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, rows_pad, ktot);
+  // one thread per (row, 8-k chunk), 16-B stores (conv_wpack_x3v_kernel)
+  const dim3 pg((unsigned)(rows_pad / x3_bn(pl.mode)), (unsigned)(ktot / kX3BK));
+  if (pl.mode == MODE_FWD) conv_wpack_x3v_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
+  else if (pl.mode == MODE_DGRAD) conv_wpack_x3v_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
   return hipGetLastError();
 }
 

@@ -402,40 +402,46 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
 // Weight pack: the three bf16 terms of every weight of the GEMM's B operand (FWD: row n = Cout,
 // k = (seg, tap, ci); DGRAD: row n = Cin, k = (tap, co)) at the byte the kernel's LDS tile
 // wants: [n / 128][k / 16][term][kc16 image of 128 rows x 16 k]; rows >= N are zeros.
-// One thread per (row, k) of the padded operand, the source's contiguous axis fastest.
+// One thread per (row, 8-k chunk): eight weights gathered (FWD: two float4 of
+// a K-contiguous row; DGRAD: eight scalars, consecutive lanes on consecutive input channels
+// so every load is coalesced), split, and stored as one 16-B chunk per term image — a wave
+// writes 1 KB contiguous per term instead of 2-B elements 32 B apart.  grid = (rows_pad / 128,
+// ktot / 16), 256 threads: thread t -> row t >> 1, chunk t & 1.
 template <int MODE>
-__global__ void conv_wpack_x3_kernel(const ConvParams p, char *out, int rows_pad, int ktot) {
-  const int64_t total = (int64_t)rows_pad * ktot;
-  const int nkt = ktot / kX3BK;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int n, k;
-    float v = 0.f;
-    if constexpr (MODE == MODE_FWD) {  // W[co][seg*kseg + tk]: k fastest
-      n = (int)(i / ktot);
-      k = (int)(i - (int64_t)n * ktot);
-      if (n < p.k) {
-        const int seg = k / p.kseg;
-        v = seg_ptr(p, seg)[(size_t)n * p.kseg + (k - seg * p.kseg)];
-      }
-    } else {  // W_seg(tap)[co][t][ci]: ci (the row) fastest
-      k = (int)(i / rows_pad);
-      n = (int)(i - (int64_t)k * rows_pad);
-      if (n < p.c) {
-        const int tap = k / p.k, co = k - tap * p.k;
-        const int seg = tap / p.taps_per_seg, t = tap - seg * p.taps_per_seg;
-        v = seg_ptr(p, seg)[((size_t)co * p.taps_per_seg + t) * p.c + n];
-      }
+__global__ void __launch_bounds__(256) conv_wpack_x3v_kernel(const ConvParams p, char *out, int ktot) {
+  constexpr int TR = x3_bn(MODE), IMGB = TR * kX3BK * 2;
+  const int r = threadIdx.x >> 1, ch = threadIdx.x & 1;
+  const int n = blockIdx.x * TR + r;
+  const int ks = blockIdx.y, k0 = ks * kX3BK + 8 * ch;
+  float v[8];
+  if constexpr (MODE == MODE_FWD) {   // W_seg[co][tk], k = seg * kseg + tk (kseg % 16 == 0)
+    if (n < p.k) {
+      const int seg = k0 / p.kseg;
+      const float *src = seg_ptr(p, seg) + (size_t)n * p.kseg + (k0 - seg * p.kseg);
+      const float4 a = ld4(src), b = ld4(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
     }
-    constexpr int TR = x3_bn(MODE), IMGB = TR * kX3BK * 2;   // the kernel's column tile
-    const int r = n % TR, kk = k & (kX3BK - 1);
-    char *dst = out + ((size_t)(n / TR) * nkt + (k >> 4)) * 3 * IMGB + kc16_off(r, kk >> 3) + 2 * (kk & 7);
-    const __bf16 h = (__bf16)v;
-    const float r1 = v - (float)h;
-    const __bf16 m = (__bf16)r1;
-    *reinterpret_cast<__bf16 *>(dst) = h;
-    *reinterpret_cast<__bf16 *>(dst + IMGB) = m;
-    *reinterpret_cast<__bf16 *>(dst + 2 * IMGB) = (__bf16)(r1 - (float)m);
+  } else {   // W_seg(tap)[co][t][ci], k = tap * Cout + co (Cout % 16 == 0), row n = ci
+    const int tap = k0 / p.k, co = k0 - tap * p.k;
+    const int seg = tap / p.taps_per_seg, t = tap - seg * p.taps_per_seg;
+    const float *src = seg_ptr(p, seg) + ((size_t)co * p.taps_per_seg + t) * p.c + n;
+    const size_t cs = (size_t)p.taps_per_seg * p.c;   // stride between consecutive co
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = n < p.c ? src[j * cs] : 0.f;
   }
+  uint4 h, m, l;
+  split3_2(v[0], v[1], h.x, m.x, l.x);
+  split3_2(v[2], v[3], h.y, m.y, l.y);
+  split3_2(v[4], v[5], h.z, m.z, l.z);
+  split3_2(v[6], v[7], h.w, m.w, l.w);
+  const int nkt = ktot / kX3BK;
+  char *dst = out + ((size_t)blockIdx.x * nkt + ks) * 3 * IMGB + kc16_off(r, ch);
+  *reinterpret_cast<uint4 *>(dst) = h;
+  *reinterpret_cast<uint4 *>(dst + IMGB) = m;
+  *reinterpret_cast<uint4 *>(dst + 2 * IMGB) = l;
 }
 
 }  // namespace adaptseg
