@@ -69,6 +69,8 @@ BF16_CASES = [
     (4, 64, 64, 96, 64, 1, 1, (0,), (1,), True),         # wgrad, many K splits
     (2, 256, 96, 96, 256, 3, 1, (2,), (2,), False),      # large grid: 288 tiles, no K split
     (2, 256, 96, 96, 1024, 1, 1, (0,), (1,), False),     # large grid 1x1
+    (2, 256, 20, 22, 192, 3, 1, (1,), (1,), False),      # LDS-DMA 256x128 tile at K step 64 (fwd)
+    (1, 128, 12, 14, 384, 3, 1, (1,), (1,), False),      # dgrad 256x128 / K step 64; wgrad 256-row tile, half-empty
 ]
 
 
