@@ -53,11 +53,14 @@ __device__ __forceinline__ int g16_off(int r, int ch) {
 
 // BK 64: one block per CU (3 x 48 KB ring); BK 32: two (3 x 24 KB), so one block's epilogue and
 // prologue overlap the other's K loop (short-K 1x1 products).
-template <int MODE, int BM, int BN, int BK>
+// S2: the stride-2 data gradient by output-pixel parity class (blockIdx.z = 2 py + px), each a
+// dense stride-1 GEMM over its subgrid with only its taps, as igemm_x3_kernel / igemm_bf16_kernel.
+template <int MODE, int BM, int BN, int BK, bool S2 = false>
 __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(const ConvParams p,
                                                                               const __bf16 *__restrict__ ab,
                                                                               const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
+  static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
   static_assert(BK == 64 || BK == 32, "K step");
   constexpr int NT = 512;
   constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;  // 64x64 wave tiles
@@ -81,7 +84,20 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
   const int bm = tm * BM, bn = tn * BN;
   const SegRegs sr = seg_regs(p);
 
-  const int M = p.M, K = p.K;
+  int M = p.M, K = p.K, Hc = p.h, Wc = p.w, py = 0, px = 0, kh0 = 0, kw0 = 0, nkw = p.kw_;
+  if constexpr (S2) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (p.h - py + 1) >> 1;
+    Wc = (p.w - px + 1) >> 1;
+    kh0 = (py + p.pad_[0]) & 1;
+    kw0 = (px + p.pad_[0]) & 1;
+    const int nkh = (p.kh_ - kh0 + 1) >> 1;
+    nkw = (p.kw_ - kw0 + 1) >> 1;
+    M = p.n * Hc * Wc;
+    K = nkh * nkw * p.k;
+    if (bm >= M) return;
+  }
   const int nkt = (K + BK - 1) / BK;
   const int kt0 = split * p.ktiles_per_split;
   const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
@@ -100,7 +116,13 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
     const int m = bm + 8 * RPI * i + rsub;
     a_ok[i] = m < M;
     const int mm = min(m, M - 1);
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (S2) {   // row = (b, i, j) of the parity class's subgrid
+      const int j = mm % Wc, t2 = mm / Wc;
+      const int ii = t2 % Hc, b = t2 / Hc;
+      a_y[i] = ii;
+      a_x[i] = j;
+      a_pix[i] = ((b * p.oh + ii) * p.ow + j) * ca + chs;
+    } else if constexpr (MODE == MODE_FWD) {
       uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
       const int ow = mm - (int)t * p.ow;
       uint32_t b = fdiv(t, p.fd_oh);
@@ -142,6 +164,15 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
       dx = uni(dx);
       soff = uni((dy * p.w + dx) * ca + kbase - tap * p.c);
       wk = kbase;
+    } else if constexpr (S2) {   // tap (u, v) of the class: kernel row kh0 + 2u, column kw0 + 2v
+      const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
+      const int co0 = kbase - tap * p.k;
+      const int u = tap / nkw, v = tap - u * nkw;
+      const int kh = kh0 + 2 * u, kw = kw0 + 2 * v;
+      dy = uni((py + p.pad_[0] - kh) >> 1);   // dY row offset from subgrid row ii
+      dx = uni((px + p.pad_[0] - kw) >> 1);
+      soff = uni((dy * p.ow + dx) * ca + co0);
+      wk = uni((kh * p.kw_ + kw) * p.k + co0);   // packed row offset of (tap, co0)
     } else {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
       int seg, t;
@@ -226,8 +257,8 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
     __syncthreads();  // the epilogue reuses the LDS
   }
 
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, false>(p, acc, bm, bn, tm, tn, split, M, p.h, p.w, 0, 0,
-                                                         reinterpret_cast<float *>(lds));
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+                                                      reinterpret_cast<float *>(lds));
 }
 
 // Weight gradient on the same LDS-DMA ring: dW[co][tap, ci] = sum_pix dY[pix][co] x[pix+tap][ci]

@@ -473,7 +473,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     pl.bf16_bn = (w256 && op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 256) ? 256 : 128;
     // forward / stride-1 data gradients with N >= 128 on the LDS-DMA kernel (conv_bf16g.hpp):
     // 128x256 tiles when N >= 256 (the activation operand is fetched once per tap), else 256x128
-    if (op != ADAPTSEG_CONV_BWD_WEIGHT && !pl.s2 && p.N >= 128) {
+    if (op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 128) {   // stride-2 data gradients by parity class too
       pl.g16 = true;
       pl.g16_bm = p.N >= 256 ? 128 : 256;
       pl.g16_bn = p.N >= 256 ? 256 : 128;
@@ -481,7 +481,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // prologue / epilogue overlaps the other's loop on short-K products) — per shape
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
-      pl.g16_bk = p.K >= 2048 ? 64 : 32;
+      pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
     }
     // weight gradients with 16-B channel chunks (Cin % 8 == 0, Cout % 8 == 0) on the LDS-DMA
     // weight-gradient kernel: {128,256}x128 tiles, K steps of 32 output pixels
@@ -506,6 +506,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 
 int kernel_id(const Plan &pl, int mode) {
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
+  if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);

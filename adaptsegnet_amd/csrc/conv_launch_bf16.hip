@@ -118,7 +118,12 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(bf16_wpack_bytes(pl));
     const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext)
                                    : reinterpret_cast<const __bf16 *>(base);
-    dim3 grid(pl.tiles, p.splits), block(512);
+    dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(512);
+    if (pl.s2) {   // stride-2 data gradient: parity classes on grid.z, K step 32
+      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_DGRAD, 128, 256, 32, true><<<grid, block, 0, s>>>(p, act, wb);
+      else igemm_bf16g_kernel<MODE_DGRAD, 256, 128, 32, true><<<grid, block, 0, s>>>(p, act, wb);
+      return hipGetLastError();
+    }
     if (pl.mode == MODE_WGRAD) {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(

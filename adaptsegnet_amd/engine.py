@@ -85,14 +85,15 @@ _BF16_SEL: dict = {}
 
 def bf16_only(g, n, h, w, ops) -> bool:
     """True when every listed product of this conv runs on a bf16-operand LDS-DMA kernel
-    (selectors 94 / 97-99), which reads only the bf16 copy of its activation operand: the fp32
-    tensor then need not be written at all."""
+    (selectors 94 / 97-99, stride-2 data gradients 192 / 193), which reads only the bf16 copy of
+    its activation operand: the fp32 tensor then need not be written at all."""
     for op in ops:
         key = (g, n, h, w, op, K.get_conv_math())
         v = _BF16_SEL.get(key)
         if v is None:
             kid, _ = K.conv_kernel_id(g, n, h, w, op)
-            v = _BF16_SEL[key] = kid // 10 % 10 == 9 and kid % 10 in (4, 7, 8, 9)
+            sel = kid % 100   # 94 / 97-99: LDS-DMA kernels; 192 / 193: its stride-2 data gradient
+            v = _BF16_SEL[key] = sel in (94, 97, 98, 99) or (op == 1 and sel in (92, 93))
         if not v:
             return False
     return True

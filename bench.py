@@ -173,6 +173,9 @@ def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
     if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
+    if sel % 100 in (92, 93) and op == 1:   # bf16 LDS-DMA stride-2 data gradient (parity classes)
+        bm, bn = (128, 256) if var == 2 else (256, 128)
+        return f"igemm_bf16g_kernel<1, {bm}, {bn}, 32, true>"
     if sel % 100 in (94, 97, 98, 99):   # the bf16 LDS-DMA kernels (conv_bf16g.hpp)
         if op == 2:
             return f"igemm_bf16g_wgrad_kernel<{256 if var == 8 else 128}>"

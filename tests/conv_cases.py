@@ -71,6 +71,8 @@ BF16_CASES = [
     (2, 256, 96, 96, 1024, 1, 1, (0,), (1,), False),     # large grid 1x1
     (2, 256, 20, 22, 192, 3, 1, (1,), (1,), False),      # LDS-DMA 256x128 tile at K step 64 (fwd)
     (1, 128, 12, 14, 384, 3, 1, (1,), (1,), False),      # dgrad 256x128 / K step 64; wgrad 256-row tile, half-empty
+    (2, 128, 19, 25, 128, 3, 2, (1,), (1,), False),      # stride-2 3x3 data gradient, LDS-DMA parity classes 256x128
+    (2, 256, 16, 20, 128, 4, 2, (1,), (1,), True),       # D-style 4x4/2 (bias), parity classes on 128x256
 ]
 
 
