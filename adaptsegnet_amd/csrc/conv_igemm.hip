@@ -677,6 +677,7 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
+  AS_CHECK_ARG(x || pl.act_ext, "conv fwd: bf16 input copy must be 16-byte aligned when x is NULL");
   p.out = y;
   p.res = res;
   p.flags = flags;
@@ -735,6 +736,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
+  AS_CHECK_ARG(x || pl.act_ext, "conv fwd_bnstats: bf16 input copy must be 16-byte aligned when x is NULL");
   p.out = y;
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
@@ -784,6 +786,7 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(dy_bf16) ? dy_bf16 : nullptr;
+  AS_CHECK_ARG(dy || pl.act_ext, "conv bwd_data: bf16 dY copy must be 16-byte aligned when dy is NULL");
   p.out = dx;
   p.res = res;
   p.aux = aux;
@@ -830,6 +833,7 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
       pl.act_ext = dy_bf16;
       pl.act_ext2 = x_bf16;
     }
+    AS_CHECK_ARG((dy && x) || pl.act_ext, "conv bwd_weight: bf16 copies must be 16-byte aligned when dy / x is NULL");
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
     st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
   }
