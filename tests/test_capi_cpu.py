@@ -103,3 +103,31 @@ def test_kernels_use_no_scratch(tmp_path):
         assert not bad, f"kernels using scratch: {bad}"
         seen += len(names)
     assert seen > 50
+
+
+def test_bf16_operand_abi_checks_on_host():
+    """The _x entry points (bf16 operand copies): a NULL fp32 operand is accepted only when the
+    plan runs a bf16-operand LDS-DMA kernel that reads the copy instead — rejected on the host,
+    before any launch, otherwise; and the bf16 selectors of the step's shapes (host planning)."""
+    from adaptsegnet_amd import kernels as K
+    L = _lib.lib()
+    d = K._desc(K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,)), 4, 64, 128, K.nhwc_strides(4, 64, 128, 256))[0]
+    w = _lib.ptr_array([16])
+    # F32X3 math: no bf16-operand kernel, so the fp32 input is required
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, ctypes.c_void_p(256), w, None, None,
+                                 ctypes.c_void_p(512), 0, None, 0, None)
+    assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, ctypes.c_void_p(512), 0, None, 0, None)
+    assert st == 1
+    K.set_conv_math(K.MATH_BF16)
+    try:
+        g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
+        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
+        s2 = K.ConvGeom(256, 128, 1, 1, 2, (0,), (1,))
+        assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 192    # stride-2 parity classes, LDS-DMA
+        # weight gradient without the fp32 operands needs both copies (and no bias gradient)
+        st = L.adaptseg_conv2d_bwd_weight_x(ctypes.byref(d), None, ctypes.c_void_p(256), None, None,
+                                            _lib.ptr_array([1024]), None, 0, None, 0, None)
+        assert st == 1
+    finally:
+        K.set_conv_math(K.MATH_F32X3)
