@@ -117,8 +117,12 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
    LDS-DMA kernel (forward and stride-1 data gradient with N >= 128) then reads it instead of
    converting the operand itself, one pass over the activation less per call; every other
    kernel ignores it.  The results are bitwise those of the plain forms (the copy holds
-   exactly the values the kernel would have rounded).  Same interfaces otherwise
-   (model/deeplab_multi.py:83-103: the Bottleneck convs consume BN+ReLU outputs). */
+   exactly the values the kernel would have rounded).  The fp32 operand itself may then be
+   NULL — its producer skipped writing it — but only when the product runs on that kernel
+   (adaptseg_conv2d_kernel_id selector 100*op + 94 / 97-99, or 192 / 193 for the stride-2
+   data gradient); otherwise ADAPTSEG_ERR_ARG, checked on the host before any launch.  Same
+   interfaces otherwise (model/deeplab_multi.py:83-103: the Bottleneck convs consume BN+ReLU
+   outputs). */
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
                           const float *const *w, const float *const *bias, const float *res, float *y,
                           int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
@@ -173,7 +177,8 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                 adaptseg_stream_t stream);
 
 /* The forward BN passes with an optional bf16 (RNE) copy of y written beside it (y_bf16,
-   contiguous [rows][c], NULL = none): the operand of the next conv under bf16 conv math. */
+   contiguous [rows][c], NULL = none): the operand of the next conv under bf16 conv math.
+   y may be NULL when y_bf16 is given (only the copy is written). */
 int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
                             float *running_mean, float *running_var, float momentum, float eps,
                             float *save_mean, float *save_invstd, const float *res, float *y,
@@ -205,7 +210,8 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd with an optional bf16 (RNE) copy of dx (dx_bf16, NULL = none): the
-   data-gradient operand of the conv that produced x, under bf16 conv math. */
+   data-gradient operand of the conv that produced x, under bf16 conv math.  dx may be NULL
+   when dx_bf16 is given. */
 int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const float *x,
                       const float *weight, const float *bias, const float *save_mean,
                       const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu,
