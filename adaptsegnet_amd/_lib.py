@@ -58,10 +58,10 @@ _SIGS = {
     "adaptseg_conv2d_fwd": [_DESC, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data": [_DESC, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight": [_DESC, _P, _P, _PP, _PP, _I, _P, _SZ, _P],
-    "adaptseg_conv2d_fwd_x": [_DESC, _P, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
+    "adaptseg_conv2d_fwd_x": [_DESC, _P, _P, _PP, _PP, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_fwd_bnstats_x": [_DESC, _P, _P, _PP, _P, _P, _SZ, ctypes.POINTER(ctypes.c_int), _P, _SZ,
                                       _P],
-    "adaptseg_conv2d_bwd_data_x": [_DESC, _P, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
+    "adaptseg_conv2d_bwd_data_x": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight_x": [_DESC, _P, _P, _P, _P, _PP, _PP, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_train_x": [_L, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_train_tiles_x": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P],

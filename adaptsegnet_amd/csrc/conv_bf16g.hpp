@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
     const bool bv = rv & b_col & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
-      glds16(rv & a_col[i] ? dyb + (size_t)mm * p.k + bm + 128 * i + chs : zero, As + i * IMG);
+      glds16((rv & a_col[i]) ? dyb + (size_t)mm * p.k + bm + 128 * i + chs : zero, As + i * IMG);
     glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci : zero, As + NA * IMG);
   };
 

@@ -53,6 +53,7 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
       v = epi_act(v, p.flags);
       if (p.flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], p.flags);
       p.out[idx] = v;
+      if (p.outb) p.outb[idx] = (__bf16)v;
     }
   }
 }
@@ -132,6 +133,10 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
       }
     }
     *reinterpret_cast<float4 *>(o) = v;
+    if (mode != MODE_WGRAD && p.outb) {
+      __bf16 *ob = p.outb + (o - p.out);
+      ob[0] = (__bf16)v.x; ob[1] = (__bf16)v.y; ob[2] = (__bf16)v.z; ob[3] = (__bf16)v.w;
+    }
   }
 }
 
@@ -592,6 +597,20 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
 }
 
 
+// bf16 (RNE) copy of a finished fp32 output, for the paths whose kernels do not write one.
+__global__ void bf16_out_copy_kernel(const float *__restrict__ y, __bf16 *__restrict__ yb, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    yb[i] = (__bf16)y[i];
+}
+
+static int out_copy(const float *y, uint16_t *yb, int64_t n, hipStream_t s) {
+  if (!yb || n == 0) return ADAPTSEG_OK;
+  bf16_out_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 8192), 256, 0, s>>>(
+      y, reinterpret_cast<__bf16 *>(yb), n);
+  AS_CHECK_LAUNCH("bf16_out_copy");
+  return ADAPTSEG_OK;
+}
+
 // Thin convs (Cout <= 4) go to the vector-ALU kernels of conv_thin.hip.
 bool use_thin(const adaptseg_conv_desc *d, int op) { return thin_eligible(d, op); }
 
@@ -645,12 +664,12 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                         const float *const *bias, const float *res, float *y, int flags, void *ws,
                         size_t ws_bytes, adaptseg_stream_t stream) {
-  return adaptseg_conv2d_fwd_x(d, x, nullptr, w, bias, res, y, flags, ws, ws_bytes, stream);
+  return adaptseg_conv2d_fwd_x(d, x, nullptr, w, bias, res, y, nullptr, flags, ws, ws_bytes, stream);
 }
 
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
-                          const float *const *w, const float *const *bias, const float *res, float *y, int flags,
-                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                          const float *const *w, const float *const *bias, const float *res, float *y,
+                          uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
@@ -661,11 +680,14 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv fwd: residual flag without res");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd: null weight %d", s);
+  const int64_t ny = (int64_t)d->n * d->oh * d->ow * d->k;
   if (use_thin(d, ADAPTSEG_CONV_FWD) &&
       thin_fwd(d, x, w[0], bias ? bias[0] : nullptr, res, y, flags, as_stream(stream)) == ADAPTSEG_OK)
-    return ADAPTSEG_OK;
-  if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg))
-    return tapgemm_fwd(d, x, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
+    return out_copy(y, y_bf16, ny, as_stream(stream));
+  if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg)) {
+    st = tapgemm_fwd(d, x, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
+    return st ? st : out_copy(y, y_bf16, ny, as_stream(stream));
+  }
   ConvParams &p = pl.p;
   p.x = x;
   for (int s = 0; s < d->nseg; ++s) {
@@ -679,6 +701,7 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
   AS_CHECK_ARG(x || pl.act_ext, "conv fwd: bf16 input copy must be 16-byte aligned when x is NULL");
   p.out = y;
+  p.outb = reinterpret_cast<__bf16 *>(y_bf16);
   p.res = res;
   p.flags = flags;
   return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
@@ -726,7 +749,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
                "conv fwd_bnstats: this product needs the fp32 input (no bf16-operand kernel for it)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
   if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
-    return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, y, 0, ws, ws_bytes, stream);
+    return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, y, nullptr, 0, ws, ws_bytes, stream);
   ConvParams &p = pl.p;
   p.x = x;
   for (int s = 0; s < d->nseg; ++s) {
@@ -753,12 +776,12 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream) {
-  return adaptseg_conv2d_bwd_data_x(d, dy, nullptr, w, res, aux, dx, flags, ws, ws_bytes, stream);
+  return adaptseg_conv2d_bwd_data_x(d, dy, nullptr, w, res, aux, dx, nullptr, flags, ws, ws_bytes, stream);
 }
 
 int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
-                               const float *const *w, const float *res, const float *aux, float *dx, int flags,
-                               void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                               const float *const *w, const float *res, const float *aux, float *dx,
+                               uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
@@ -770,12 +793,15 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
   AS_CHECK_ARG((flags & kEpiActGrad) != kEpiActGrad, "conv bwd_data: LEAKY_GRAD and RELU_GRAD");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data: null weight %d", s);
+  const int64_t nx = (int64_t)d->n * d->h * d->w * d->c;
   if (use_thin(d, ADAPTSEG_CONV_BWD_DATA) &&
       thin_dgrad(d, dy, w[0], res, aux, dx, flags, as_stream(stream)) == ADAPTSEG_OK)
-    return ADAPTSEG_OK;
+    return out_copy(dx, dx_bf16, nx, as_stream(stream));
   if (tapgemm_eligible(d) && aligned16(dy) && aligned16(dx) && segs_aligned(w, d->nseg) &&
-      (!res || aligned16(res)) && (!aux || aligned16(aux)))
-    return tapgemm_bwd_data(d, dy, w, res, aux, dx, flags, ws, ws_bytes, as_stream(stream));
+      (!res || aligned16(res)) && (!aux || aligned16(aux))) {
+    st = tapgemm_bwd_data(d, dy, w, res, aux, dx, flags, ws, ws_bytes, as_stream(stream));
+    return st ? st : out_copy(dx, dx_bf16, nx, as_stream(stream));
+  }
   ConvParams &p = pl.p;
   p.dy = dy;
   for (int s = 0; s < d->nseg; ++s) {
@@ -788,6 +814,7 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   pl.act_ext = aligned16(dy_bf16) ? dy_bf16 : nullptr;
   AS_CHECK_ARG(dy || pl.act_ext, "conv bwd_data: bf16 dY copy must be 16-byte aligned when dy is NULL");
   p.out = dx;
+  p.outb = reinterpret_cast<__bf16 *>(dx_bf16);
   p.res = res;
   p.aux = aux;
   p.flags = flags;

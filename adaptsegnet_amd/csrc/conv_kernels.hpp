@@ -59,6 +59,7 @@ struct ConvParams {
   int kw_, kh_;                // kernel width / height (tap -> kh, kw)
   int pad_[4], dil_[4];        // per-segment padding / dilation
   FastDiv fd_taps, fd_kw;
+  __bf16 *outb;                // FWD / DGRAD: optional bf16 (RNE) copy of the final output (NULL: none)
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
@@ -548,6 +549,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_kernel(const Con
           v = epi_act(v, flags);
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           p.out[idx] = v;
+          if (p.outb) p.outb[idx] = (__bf16)v;
         }
     }
   }
@@ -733,6 +735,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
           v = epi_act(v, flags);
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           p.out[idx] = v;
+          if (p.outb) p.outb[idx] = (__bf16)v;
         }
     }
     if constexpr (MODE == MODE_FWD && !S2) {

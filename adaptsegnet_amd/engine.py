@@ -99,6 +99,12 @@ def bf16_only(g, n, h, w, ops) -> bool:
     return True
 
 
+def _copy_pays(g, n, h, w, ops) -> bool:
+    """True when one of the listed products of conv ``g`` reads a bf16 operand copy, so that
+    its producer should write one (the discriminator's conv -> LeakyReLU -> conv chain)."""
+    return any(bf16_only(g, n, h, w, (op,)) for op in ops)
+
+
 def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False, fp32=True):
     """bn_forward that also returns the bf16 copy of y (None unless ``bf16``); fp32=False skips
     the fp32 y (returned as None) when every consumer reads the copy."""
@@ -472,20 +478,24 @@ class _FCDiscriminatorFn(torch.autograd.Function):
         convs = model._convs()
         n, c, h, w = x.shape
         xs = _input_strides(x)
-        acts, dims = [], []
-        cur, ch, cw, cs = x, h, w, xs
+        sh = bf16_operands()   # bf16 conv math: each conv epilogue also writes the next conv's operand copy
+        acts, actsb, dims = [], [], []
+        cur, curb, ch, cw, cs = x, None, h, w, xs
         for i, conv in enumerate(convs):
             g = conv.geom()
             last = i == len(convs) - 1
+            oh, ow = g.out_hw(ch, cw)
+            nb = sh and not last and _copy_pays(convs[i + 1].geom(), n, oh, ow, (0, 2))
             out = K.conv_fwd(g, cur, n, ch, cw, [conv.weight], [conv.bias], strides=cs,
-                             flags=0 if last else K.EPI_LEAKY)
+                             flags=0 if last else K.EPI_LEAKY, xb=curb, bf16_out=nb)
             dims.append((ch, cw, cs))
             acts.append(cur)
-            cur = out
-            ch, cw = g.out_hw(ch, cw)
+            actsb.append(curb)
+            cur, curb = out if nb else (out, None)
+            ch, cw = oh, ow
             cs = K.nhwc_strides(n, ch, cw, g.cout)
         if save:
-            ctx.model, ctx.acts, ctx.dims, ctx.n = model, acts, dims, n
+            ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n = model, acts, actsb, dims, n
             ctx.need_w = anchor.requires_grad
         return K.as_nchw(cur)
 
@@ -493,8 +503,9 @@ class _FCDiscriminatorFn(torch.autograd.Function):
     def backward(ctx, gout):
         if gout is None:
             return None, None, None, None
-        model, acts, dims, n = ctx.model, ctx.acts, ctx.dims, ctx.n
+        model, acts, actsb, dims, n = ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n
         convs = model._convs()
+        sh = bf16_operands()
         need_w = ctx.need_w
         if need_w:
             model._arena.claim(model._pidx["all"])
@@ -502,7 +513,7 @@ class _FCDiscriminatorFn(torch.autograd.Function):
         if not g.is_contiguous():
             g = g.contiguous()
         ws = WgradStream(g.device) if need_w else None
-        dx = None
+        dx, gb = None, None
         for i in reversed(range(len(convs))):
             conv = convs[i]
             geo = conv.geom()
@@ -512,13 +523,16 @@ class _FCDiscriminatorFn(torch.autograd.Function):
                     _wgrad_padded(ws, geo, g, acts[i], n, ch, cw, conv.weight.grad, conv.bias.grad)
                 else:
                     _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
-                           strides=cs)
+                           strides=cs, dyb=gb, xb=actsb[i])
             if i > 0:
                 # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
-                g = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i])
+                ph, pw, _ = dims[i - 1]
+                nb = sh and _copy_pays(convs[i - 1].geom(), n, ph, pw, (1, 2) if need_w else (1,))
+                r = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i], dyb=gb, bf16_out=nb)
+                g, gb = r if nb else (r, None)
             elif ctx.needs_input_grad[1]:
-                dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight]))
-            acts[i] = None
+                dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], dyb=gb))
+            acts[i] = actsb[i] = None
         if ws is not None:
             ws.join()
         return None, dx, None, None

@@ -98,18 +98,20 @@ def _wshape(g: ConvGeom):
 
 
 def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, biases=None,
-             strides=None, out=None, res=None, flags: int = 0, xb=None) -> torch.Tensor:
+             strides=None, out=None, res=None, flags: int = 0, xb=None, bf16_out: bool = False):
     """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (EPI_LEAKY / EPI_RELU).
-    xb: optional bf16 copy of x (contiguous NHWC) for the bf16 conv math (bn_* ``bf16_out``)."""
+    xb: optional bf16 copy of x (contiguous NHWC) for the bf16 conv math (bn_* ``bf16_out``).
+    bf16_out: also return a bf16 copy of y written by the epilogue -> (y, yb)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
     oh, ow = g.out_hw(h, w)
     if out is None:
         out = torch.empty((n, oh, ow, g.cout), device=(x if x is not None else xb).device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
-    _OP.conv2d_fwd(x, xb, list(weights), list(biases) if biases is not None else [], res, out, (n, g.cin, h, w),
-                   strides, _wshape(g), g.stride, g.pads, g.dils, flags)
-    return out
+    outb = _bf16_like(out, bf16_out)
+    _OP.conv2d_fwd(x, xb, list(weights), list(biases) if biases is not None else [], res, out, outb,
+                   (n, g.cin, h, w), strides, _wshape(g), g.stride, g.pads, g.dils, flags)
+    return (out, outb) if bf16_out else out
 
 
 def conv_bnstats_tiles(g: ConvGeom, n: int, h: int, w: int, strides) -> int:
@@ -136,17 +138,19 @@ def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weigh
 
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
-               res=None, aux=None, flags: int = 0, dyb=None) -> torch.Tensor:
-    """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD)."""
+               res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False):
+    """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD).
+    bf16_out: also return a bf16 copy of dx written by the epilogue -> (dx, dxb)."""
     if out is None:
         out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
     if aux is not None and not flags & EPI_RELU_GRAD:
         flags |= EPI_LEAKY_GRAD
-    _OP.conv2d_bwd_data(dy, dyb, list(weights), res, aux, out, (n, g.cin, h, w), _wshape(g), g.stride, g.pads,
-                        g.dils, flags)
-    return out
+    outb = _bf16_like(out, bf16_out)
+    _OP.conv2d_bwd_data(dy, dyb, list(weights), res, aux, out, outb, (n, g.cin, h, w), _wshape(g), g.stride,
+                        g.pads, g.dils, flags)
+    return (out, outb) if bf16_out else out
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,

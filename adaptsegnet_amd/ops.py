@@ -148,13 +148,14 @@ def _op(schema):
 
 # ---- convolution ------------------------------------------------------------------------
 @_op("conv2d_fwd(Tensor? x, Tensor? xb, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, "
-     "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_fwd(x, xb, weight, bias, res, out, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+     "Tensor(b!)? outb, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, "
+     "int flags) -> ()")
+def _conv2d_fwd(x, xb, weight, bias, res, out, outb, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_FWD], out.device)
     check(_lib.lib().adaptseg_conv2d_fwd_x(
         ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out),
-        flags, wp, wsz, _stream()), "conv2d_fwd")
+        _p(outb), flags, wp, wsz, _stream()), "conv2d_fwd")
 
 
 @_op("conv2d_fwd_bnstats(Tensor? x, Tensor? xb, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, "
@@ -172,13 +173,14 @@ def _conv2d_fwd_bnstats(x, xb, weight, out, stats, in_shape, in_stride, w_shape,
 
 
 @_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, "
-     "int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_bwd_data(dy, dyb, weight, res, aux, dx, in_shape, w_shape, stride, pad, dil, flags):
+     "Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
+def _conv2d_bwd_data(dy, dyb, weight, res, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
     n, c, h, w = in_shape
     d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_DATA], dx.device)
     check(_lib.lib().adaptseg_conv2d_bwd_data_x(
-        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(res), _p(aux), _p(dx), flags, wp, wsz, _stream()),
+        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(res), _p(aux), _p(dx), _p(dxb), flags, wp, wsz,
+        _stream()),
         "conv2d_bwd_data")
 
 

@@ -122,16 +122,22 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
    (adaptseg_conv2d_kernel_id selector 100*op + 94 / 97-99, or 192 / 193 for the stride-2
    data gradient); otherwise ADAPTSEG_ERR_ARG, checked on the host before any launch.  Same
    interfaces otherwise (model/deeplab_multi.py:83-103: the Bottleneck convs consume BN+ReLU
-   outputs). */
+   outputs).
+   y_bf16 / dx_bf16 (optional, NULL = none): a bf16 (RNE) copy of the fp32 output, written by
+   the GEMM epilogue or split-K reduce beside y / dx (a separate pass on the thin and tap-GEMM
+   paths), so that a consumer conv's _x operand needs no conversion pass: the discriminator
+   convs (model/discriminator.py:14-27) chain conv -> LeakyReLU -> conv with no BatchNorm
+   between.  Contiguous NHWC like y; 2-byte alignment suffices. */
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
                           const float *const *w, const float *const *bias, const float *res, float *y,
-                          int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+                          uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
                                   const float *const *w, float *y, float *stats, size_t stats_bytes,
                                   int *ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                const float *const *w, const float *res, const float *aux, float *dx,
-                               int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+                               uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
+                               adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
    (Cin and Cout multiples of 8) reads them; other kernels ignore them. */

@@ -231,3 +231,65 @@ def test_bf16_train_step_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monk
     for ma, mb in ((m_a, m_b), (d1_a, d1_b), (d2_a, d2_b)):
         for (ka, va), (kb, vb) in zip(ma.state_dict().items(), mb.state_dict().items()):
             assert ka == kb and torch.equal(va, vb), ka
+
+
+@pytest.mark.parametrize("math", ["bf16", "f32x3"])
+def test_conv_bf16_output_copy_is_exact(math):
+    """conv_fwd / conv_dgrad ``bf16_out``: the epilogue (or split-K reduce, or the separate pass
+    of the thin and tap-GEMM paths) writes y.to(bfloat16) exactly beside y, and y itself is
+    bitwise the plain call's.  The discriminator's conv -> LeakyReLU -> conv chain
+    (model/discriminator.py:14-27) feeds these copies to the next conv's _x operand."""
+    k = K()
+    k.set_conv_math(k.MATH_BF16 if math == "bf16" else k.MATH_F32X3)
+    try:
+        g = torch.Generator().manual_seed(33)
+        cases = [  # (n, cin, h, w, cout, ks, stride, pads, dils): D convs (4x4/2), a split-K tail,
+            (2, 64, 40, 48, 128, 4, 2, (1,), (1,)),      # thin classifier, the ASPP tap-GEMM shape
+            (2, 128, 20, 24, 256, 4, 2, (1,), (1,)),
+            (1, 256, 5, 6, 512, 4, 2, (1,), (1,)),
+            (2, 512, 9, 11, 1, 4, 1, (1,), (1,)),
+            (1, 2048, 9, 11, 19, 3, 1, (6, 12), (6, 12)),
+        ]
+        for n, cin, h, w, cout, ks, st, pads, dils in cases:
+            geom = k.ConvGeom(cin, cout, ks, ks, st, pads, dils)
+            oh, ow = geom.out_hw(h, w)
+            x = torch.randn(n, h, w, cin, generator=g).to(DEV)
+            wt = [(torch.randn(cout, ks, ks, cin, generator=g) * 0.05).to(DEV) for _ in pads]
+            bs = [torch.randn(cout, generator=g).to(DEV) for _ in pads]
+            y0 = k.conv_fwd(geom, x, n, h, w, wt, bs, flags=k.EPI_LEAKY)
+            y1, yb = k.conv_fwd(geom, x, n, h, w, wt, bs, flags=k.EPI_LEAKY, bf16_out=True)
+            assert torch.equal(y0, y1) and torch.equal(yb, y1.to(torch.bfloat16)), (cin, cout)
+            gy = torch.randn(n, oh, ow, cout, generator=g).to(DEV)
+            aux = torch.randn(n, h, w, cin, generator=g).to(DEV)
+            d0 = k.conv_dgrad(geom, gy, n, h, w, wt, aux=aux)
+            d1, db = k.conv_dgrad(geom, gy, n, h, w, wt, aux=aux, bf16_out=True)
+            assert torch.equal(d0, d1) and torch.equal(db, d1.to(torch.bfloat16)), (cin, cout)
+    finally:
+        k.set_conv_math(k.MATH_F32X3)
+
+
+def test_discriminator_bf16_output_copies_are_bitwise_neutral(bf16_math, monkeypatch):
+    """The discriminator under the bf16 conv math with and without the epilogue-written operand
+    copies (engine._copy_pays): bitwise the same output, input gradient and parameter gradients."""
+    from adaptsegnet_amd import engine
+    from adaptsegnet_amd.model import FCDiscriminator
+    torch.manual_seed(3)
+    n, h, w = 2, 65, 97
+    x = torch.randn(n, 19, h, w, generator=torch.Generator().manual_seed(4)).softmax(1).to(DEV)
+    assert engine._copy_pays(bf16_math.ConvGeom(64, 128, 4, 4, 2, (1,), (1,)), n, 33, 49, (0, 2))
+
+    def run():
+        torch.manual_seed(3)
+        D = FCDiscriminator(num_classes=19).to(DEV)
+        xi = x.clone().requires_grad_(True)
+        out = D(xi)
+        out.backward(torch.ones_like(out))
+        torch.cuda.synchronize()
+        return out.detach(), xi.grad, [p.grad.clone() for p in D.parameters()]
+
+    a = run()
+    monkeypatch.setattr(engine, "_copy_pays", lambda *args, **kw: False)
+    b = run()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for ga, gb in zip(a[2], b[2]):
+        assert torch.equal(ga, gb)

@@ -115,9 +115,10 @@ def test_bf16_operand_abi_checks_on_host():
     w = _lib.ptr_array([16])
     # F32X3 math: no bf16-operand kernel, so the fp32 input is required
     st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, ctypes.c_void_p(256), w, None, None,
-                                 ctypes.c_void_p(512), 0, None, 0, None)
+                                 ctypes.c_void_p(512), None, 0, None, 0, None)
     assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
-    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, ctypes.c_void_p(512), 0, None, 0, None)
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, ctypes.c_void_p(512), None, 0, None, 0,
+                                 None)
     assert st == 1
     K.set_conv_math(K.MATH_BF16)
     try:

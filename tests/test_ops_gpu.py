@@ -557,9 +557,9 @@ def test_custom_ops_opcheck():
     y = torch.empty(n, h, w, cout, device=DEV)
     ops = torch.ops.adaptseg
     cases = [
-        (ops.conv2d_fwd.default, (x, None, [wt], [None], None, y, [n, cin, h, w], [h * w * cin, 1, w * cin, cin],
+        (ops.conv2d_fwd.default, (x, None, [wt], [None], None, y, None, [n, cin, h, w], [h * w * cin, 1, w * cin, cin],
                                   [cout, cin, 3, 3], 1, [1], [1], 0)),
-        (ops.conv2d_bwd_data.default, (r(n, h, w, cout), None, [wt], None, None, torch.empty_like(x), [n, cin, h, w],
+        (ops.conv2d_bwd_data.default, (r(n, h, w, cout), None, [wt], None, None, torch.empty_like(x), None, [n, cin, h, w],
                                        [cout, cin, 3, 3], 1, [1], [1], 0)),
         (ops.conv2d_bwd_weight.default, (r(n, h, w, cout), None, x, None, [torch.zeros_like(wt)], [], [n, cin, h, w],
                                          [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1, [1], [1], 2)),
@@ -587,7 +587,7 @@ def test_torch_ops_conv_and_ce_vs_oracle():
     ref = F.conv2d(x, wt, None, 1, 2, 2)
     y = torch.empty(n, h, w, cout, device=DEV)
     torch.ops.adaptseg.conv2d_fwd(nhwc(x), None, [wt.float().to(DEV).contiguous(memory_format=torch.channels_last)], [],
-                                  None, y, [n, cin, h, w], [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1,
+                                  None, y, None, [n, cin, h, w], [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1,
                                   [2], [2], 0)
     assert rel(nchw(y), ref) < 2e-5
     logits = torch.randn(n, 19, h, w, generator=g, dtype=torch.float64) * 3
