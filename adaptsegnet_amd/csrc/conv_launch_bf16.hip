@@ -37,6 +37,50 @@ __global__ void __launch_bounds__(256) conv_wpack_dgrad_kernel(const ConvParams 
   }
 }
 
+// Vector forms (the step's convs: kseg % 8 == 0 / Cin % 4 == 0 and Cout % 8 == 0, 16-B aligned
+// weights): every load a float4 and every store a 16-B chunk of eight bf16, 32-bit indexing.
+// FWD: one thread per 8-k chunk of a row, consecutive threads on consecutive chunks.
+__global__ void __launch_bounds__(256) conv_wpack_fwd_v_kernel(const ConvParams p, uint4 *__restrict__ out,
+                                                               uint32_t cpr, uint32_t total) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t co = i / cpr, k0 = (i - co * cpr) * 8;
+    int seg = 0;
+    uint32_t tk = k0;
+    while (tk >= (uint32_t)p.kseg) { tk -= p.kseg; ++seg; }
+    const float *src = seg_ptr(p, seg) + (size_t)co * p.kseg + tk;
+    const uint2 lo = cvt4_bf16(ld4(src)), hi = cvt4_bf16(ld4(src + 4));
+    out[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+
+// DGRAD: the 64 (co) x 64 (ci) tile of one tap read as float4 along ci, written as 16-B chunks
+// along co.  grid = (ceil(C/64), ceil(Cout/64), ntaps), 256 threads.
+__global__ void __launch_bounds__(256) conv_wpack_dgrad_v_kernel(const ConvParams p, __bf16 *out) {
+  __shared__ float tile[64][65];
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int seg = tap / p.taps_per_seg, t = tap - seg * p.taps_per_seg;
+  const float *w = seg_ptr(p, seg);
+  const int f = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = r0 + 16 * j, co = co0 + r, ci = ci0 + 4 * f;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (co < p.k && ci < p.c) v = ld4(w + ((size_t)co * p.taps_per_seg + t) * p.c + ci);
+    tile[r][4 * f] = v.x; tile[r][4 * f + 1] = v.y; tile[r][4 * f + 2] = v.z; tile[r][4 * f + 3] = v.w;
+  }
+  __syncthreads();
+  const size_t ktot = (size_t)p.ntaps * p.k;
+  const int c = threadIdx.x & 7, co = co0 + 8 * c;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rl = (threadIdx.x >> 3) + 32 * j, ci = ci0 + rl;
+    if (ci >= p.c || co >= p.k) continue;
+    const float *col = &tile[8 * c][rl];
+    const uint2 lo = cvt4_bf16(make_float4(col[0], col[65], col[130], col[195]));
+    const uint2 hi = cvt4_bf16(make_float4(col[260], col[325], col[390], col[455]));
+    *reinterpret_cast<uint4 *>(out + (size_t)ci * ktot + (size_t)tap * p.k + co) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
 
 // fp32 NHWC activations (pixel strides sxn / sxh / sxw, unit channel stride) -> contiguous
 // NHWC bf16 (RNE), 8 channels per thread: the activation operand of the LDS-DMA kernel.
@@ -84,12 +128,21 @@ size_t bf16_wpack_bytes(const Plan &pl) {
 hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
+  bool wal = true;   // weights 16-B aligned (the vector forms' float4 loads)
+  for (int g = 0; g < p.nseg; ++g) wal = wal && (reinterpret_cast<uintptr_t>(p.wt[g]) & 15) == 0;
   if (pl.mode == MODE_FWD) {
     const int64_t n = (int64_t)p.k * p.nseg * p.kseg;
-    conv_wpack_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, s>>>(p, wb);
+    if (wal && p.kseg % 8 == 0 && n / 8 < (int64_t)1 << 31) {
+      const uint32_t total = (uint32_t)(n / 8);
+      conv_wpack_fwd_v_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0, s>>>(
+          p, reinterpret_cast<uint4 *>(wb), (uint32_t)(p.nseg * p.kseg / 8), total);
+    } else {
+      conv_wpack_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, s>>>(p, wb);
+    }
   } else if (pl.mode == MODE_DGRAD) {
     dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
-    conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
+    if (wal && p.c % 4 == 0 && p.k % 8 == 0) conv_wpack_dgrad_v_kernel<<<g, 256, 0, s>>>(p, wb);
+    else conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
   if (pl.g16 && !pl.act_ext) {  // the activation operands' bf16 copies, after the (256-B aligned) weight pack
     char *base = reinterpret_cast<char *>(wpack) + al256(bf16_wpack_bytes(pl));
