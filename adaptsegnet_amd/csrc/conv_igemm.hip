@@ -357,7 +357,13 @@ void set_splits(Plan &pl) {
   // short BN / split-K kernels then wait for CU slots.  384 measured c2 +2.4 %, c3 +2.6 %
   // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2, tools/dbg/ab_bench_many.sh).
   constexpr int kX3WgradTarget = 384;
-  const int target = (pl.mode == MODE_WGRAD && pl.x3) ? kX3WgradTarget : kSplitTarget;
+  // The LDS-DMA bf16 weight gradient (side stream) to ~256 blocks: half the split-K slab
+  // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
+  // tools/dbg/ab_lib.sh).
+  constexpr int kG16WgradTarget = 256;
+  const int target = (pl.mode == MODE_WGRAD && pl.x3)    ? kX3WgradTarget
+                     : (pl.mode == MODE_WGRAD && pl.g16) ? kG16WgradTarget
+                                                         : kSplitTarget;
   // the LDS-DMA bf16 kernel runs one block per CU: split only grids under half the CUs
   const int split_below = pl.mode == MODE_WGRAD ? target : pl.g16 ? 128 : 257;
   int splits = 1;
@@ -685,7 +691,7 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
       thin_fwd(d, x, w[0], bias ? bias[0] : nullptr, res, y, flags, as_stream(stream)) == ADAPTSEG_OK)
     return out_copy(y, y_bf16, ny, as_stream(stream));
   if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg)) {
-    st = tapgemm_fwd(d, x, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
+    st = tapgemm_fwd(d, x, x_bf16, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
     return st ? st : out_copy(y, y_bf16, ny, as_stream(stream));
   }
   ConvParams &p = pl.p;
@@ -847,7 +853,7 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
   if (thin_st == ADAPTSEG_OK) {
     st = ADAPTSEG_OK;
   } else if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(dw, d->nseg)) {
-    st = tapgemm_bwd_weight(d, dy, x, dw, flags, ws, ws_bytes, s);
+    st = tapgemm_bwd_weight(d, dy, x, x_bf16, dw, flags, ws, ws_bytes, s);
   } else {
     ConvParams &p = pl.p;
     p.dy = dy;

@@ -1292,12 +1292,14 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s);
 bool tapgemm_eligible(const adaptseg_conv_desc *d);
 size_t tapgemm_workspace(const adaptseg_conv_desc *d, int op);
 int tapgemm_kernel_id(const adaptseg_conv_desc *d, int op, int *kid, int *splits);
-int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w, const float *const *bias,
-                const float *res, float *y, int flags, void *ws, size_t ws_bytes, hipStream_t s);
+// x_bf16: optional bf16 copy of x (contiguous NHWC, 16-B aligned) for the inner GEMM's bf16 kernel
+int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16, const float *const *w,
+                const float *const *bias, const float *res, float *y, int flags, void *ws, size_t ws_bytes,
+                hipStream_t s);
 int tapgemm_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w, const float *res,
                      const float *aux, float *dx, int flags, void *ws, size_t ws_bytes, hipStream_t s);
-int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x, float *const *dw,
-                       int flags, void *ws, size_t ws_bytes, hipStream_t s);
+int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x, const uint16_t *x_bf16,
+                       float *const *dw, int flags, void *ws, size_t ws_bytes, hipStream_t s);
 
 hipError_t launch_fwd(const Plan &pl, hipStream_t s);
 // bf16 conv math (adaptseg_conv_set_math): weight-pack bytes and launcher (conv_launch_bf16.hip)

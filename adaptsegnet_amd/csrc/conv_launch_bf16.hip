@@ -144,17 +144,20 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
     if (wal && p.c % 4 == 0 && p.k % 8 == 0) conv_wpack_dgrad_v_kernel<<<g, 256, 0, s>>>(p, wb);
     else conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
   }
-  if (pl.g16 && !pl.act_ext) {  // the activation operands' bf16 copies, after the (256-B aligned) weight pack
+  // the activation operands' bf16 copies the caller did not supply, after the (256-B aligned) weight pack
+  if (pl.g16) {
     char *base = reinterpret_cast<char *>(wpack) + al256(bf16_wpack_bytes(pl));
     uint4 *act = reinterpret_cast<uint4 *>(base);
     const int64_t n8 = (int64_t)g16_act_elems(pl) / 8;
     const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192);
-    if (pl.mode == MODE_FWD)
-      bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.x, p.n, p.h, p.w, p.c / 8, p.sxn, p.sxh, p.sxw, act);
-    else
-      bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.dy, p.n, p.oh, p.ow, p.k / 8, p.oh * p.ow * p.k, p.ow * p.k,
-                                              p.k, act);
-    if (pl.mode == MODE_WGRAD) {
+    if (!pl.act_ext) {
+      if (pl.mode == MODE_FWD)
+        bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.x, p.n, p.h, p.w, p.c / 8, p.sxn, p.sxh, p.sxw, act);
+      else
+        bf16_copy_kernel<<<blocks, 256, 0, s>>>(p.dy, p.n, p.oh, p.ow, p.k / 8, p.oh * p.ow * p.k, p.ow * p.k,
+                                                p.k, act);
+    }
+    if (pl.mode == MODE_WGRAD && !pl.act_ext2) {
       uint4 *act2 = reinterpret_cast<uint4 *>(base + al256(g16_act_elems(pl) * sizeof(__bf16)));
       const int64_t m8 = (int64_t)g16_act2_elems(pl) / 8;
       bf16_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(m8, 256), 8192), 256, 0, s>>>(

@@ -197,8 +197,9 @@ static int need_ws(const adaptseg_conv_desc *d, int op, size_t ws_bytes, void *w
   return ADAPTSEG_OK;
 }
 
-int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w, const float *const *bias,
-                const float *res, float *y, int flags, void *ws, size_t ws_bytes, hipStream_t s) {
+int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16, const float *const *w,
+                const float *const *bias, const float *res, float *y, int flags, void *ws, size_t ws_bytes,
+                hipStream_t s) {
   int st = need_ws(d, ADAPTSEG_CONV_FWD, ws_bytes, ws);
   if (st) return st;
   const size_t m = (size_t)d->n * d->h * d->w, nz = tap_nz(d);
@@ -216,6 +217,7 @@ int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const float *const 
   st = inner_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
   pl.p.x = x;
+  pl.act_ext = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;   // read by the bf16 kernels only
   pl.p.wt[0] = wp;
   pl.p.out = z;
   pl.p.flags = 0;
@@ -258,8 +260,8 @@ int tapgemm_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *
   return run_plan(pl, MODE_DGRAD, gws, gws_bytes, s);
 }
 
-int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x, float *const *dw,
-                       int flags, void *ws, size_t ws_bytes, hipStream_t s) {
+int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x, const uint16_t *x_bf16,
+                       float *const *dw, int flags, void *ws, size_t ws_bytes, hipStream_t s) {
   int st = need_ws(d, ADAPTSEG_CONV_BWD_WEIGHT, ws_bytes, ws);
   if (st) return st;
   const size_t m = (size_t)d->n * d->h * d->w, nz = tap_nz(d);
@@ -276,6 +278,7 @@ int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float
   if (st) return st;
   pl.p.dy = gbuf;
   pl.p.x = x;
+  pl.act_ext2 = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;   // x's copy; dY's is made here
   pl.p.dw[0] = dwp;
   pl.p.flags = 0;
   st = run_plan(pl, MODE_WGRAD, gws, gws_bytes, s);

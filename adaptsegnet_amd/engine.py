@@ -306,16 +306,18 @@ def aspp_geom(cls):
                       tuple(c.dilation for c in cls.conv2d_list))
 
 
-def aspp_forward(cls, x, n, h, w):
+def aspp_forward(cls, x, n, h, w, xb=None):
+    """xb: bf16 copy of x (the last block's output copy, bf16 conv math): the tap-GEMM's inner
+    GEMM reads it instead of converting x per call."""
     return K.conv_fwd(aspp_geom(cls), x, n, h, w, [c.weight for c in cls.conv2d_list],
-                      [c.bias for c in cls.conv2d_list])
+                      [c.bias for c in cls.conv2d_list], xb=xb)
 
 
-def aspp_backward(cls, gy, x, n, h, w, need_w, gx_out=None, ws=None):
+def aspp_backward(cls, gy, x, n, h, w, need_w, gx_out=None, ws=None, xb=None):
     g = aspp_geom(cls)
     if need_w and cls.conv2d_list[0].weight.grad is not None:
         _wgrad(ws, g, gy, x, n, h, w, [c.weight.grad for c in cls.conv2d_list],
-               [c.bias.grad for c in cls.conv2d_list])
+               [c.bias.grad for c in cls.conv2d_list], xb=xb)
     if gx_out is None:
         return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list])
     return K.conv_dgrad(g, gy, n, h, w, [c.weight for c in cls.conv2d_list], out=gx_out,
@@ -357,14 +359,15 @@ class _DeeplabMultiFn(torch.autograd.Function):
                 recs.append(rec)
                 ch, cw = nh, nw
         p3, h3, w3 = cur, ch, cw
-        x1 = aspp_forward(model.layer5, p3, n, h3, w3)
-        q, qb = p3, curb
+        p3b = curb
+        x1 = aspp_forward(model.layer5, p3, n, h3, w3, xb=p3b)
+        q, qb = p3, p3b
         recs4 = []
         for blk in model.layer4:
             q, rec, qb = block_forward(blk, q, n, h3, w3, training, save, xb=qb)
             recs4.append(rec)
-        del curb, qb
-        x2 = aspp_forward(model.layer6, q, n, h3, w3)
+        del curb
+        x2 = aspp_forward(model.layer6, q, n, h3, w3, xb=qb)
         x1_up = K.upsample_fwd(x1, out_h, out_w)
         x2_up = K.upsample_fwd(x2, out_h, out_w)
         if save:
@@ -375,6 +378,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             ctx.stem = (c0, y0, s0, am)
             ctx.recs, ctx.recs4 = recs, recs4
             ctx.p3, ctx.q = p3, q
+            ctx.p3b, ctx.qb = p3b, qb   # bf16 copies for the classifiers' weight gradients (or None)
             ctx.need_w = anchor.requires_grad
         return K.as_nchw(x1_up), K.as_nchw(x2_up)
 
@@ -404,10 +408,10 @@ class _DeeplabMultiFn(torch.autograd.Function):
         gp3 = None
         if g2_up is not None:
             gx2 = K.upsample_bwd(K.nhwc_view(g2_up), h3, w3)
-            gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w, ws=ws)
+            gq = aspp_backward(model.layer6, gx2, ctx.q, n, h3, w3, need_w, ws=ws, xb=ctx.qb)
             done(0)
             del gx2
-            ctx.q = None
+            ctx.q = ctx.qb = None
             for i in reversed(range(n4)):
                 gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w, ws)
                 done(n4 - i)
@@ -415,10 +419,10 @@ class _DeeplabMultiFn(torch.autograd.Function):
             gp3 = gq
         if g1_up is not None:
             gx1 = K.upsample_bwd(K.nhwc_view(g1_up), h3, w3)
-            gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3, ws=ws)
+            gp3 = aspp_backward(model.layer5, gx1, ctx.p3, n, h3, w3, need_w, gx_out=gp3, ws=ws, xb=ctx.p3b)
             done(n4 + 1)
             del gx1
-        ctx.p3 = None
+        ctx.p3 = ctx.p3b = None
         if gp3 is None:
             done(None)
             if ws is not None:

@@ -155,11 +155,10 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
                dbs=None, strides=None, accumulate: bool = True, dyb=None, xb=None) -> None:
-    """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy.  dyb / xb: bf16 copies of both
-    operands (bf16 conv math; used only together)."""
+    """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy.  dyb / xb: bf16 copies of the
+    operands (bf16 conv math): the LDS-DMA weight-gradient kernel uses them together; the
+    tap-GEMM (ASPP) path uses xb alone (its dY operand is its own scattered buffer)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
-    if dyb is None or xb is None:
-        dyb = xb = None
     _OP.conv2d_bwd_weight(dy, dyb, x, xb, list(dws), list(dbs) if dbs is not None else [], (n, g.cin, h, w), strides,
                           _wshape(g), g.stride, g.pads, g.dils, EPI_ACCUMULATE if accumulate else 0)
 

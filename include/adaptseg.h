@@ -140,7 +140,9 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
-   (Cin and Cout multiples of 8) reads them; other kernels ignore them. */
+   (Cin and Cout multiples of 8) reads them; other kernels ignore them.  Exception: the
+   tap-GEMM path of the multi-branch dilated classifier (model/deeplab_multi.py:112-121; its dY
+   operand is a buffer it builds itself) uses x_bf16 alone, as adaptseg_conv2d_fwd_x does. */
 int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                  const float *x, const uint16_t *x_bf16, float *const *dw,
                                  float *const *db, int flags, void *ws, size_t ws_bytes,

@@ -293,3 +293,26 @@ def test_discriminator_bf16_output_copies_are_bitwise_neutral(bf16_math, monkeyp
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for ga, gb in zip(a[2], b[2]):
         assert torch.equal(ga, gb)
+
+
+def test_aspp_tap_gemm_reads_the_bf16_copy_bitwise(bf16_math):
+    """The multi-branch dilated classifier (model/deeplab_multi.py:112-121) on the tap-GEMM path
+    with the bf16 copy of its input (the last block's output copy): forward and weight gradient
+    bitwise the plain calls', the weight gradient taking ``xb`` alone."""
+    k = bf16_math
+    g = torch.Generator().manual_seed(41)
+    n, h, w, c, cout = 1, 65, 129, 1024, 19
+    geom = k.ConvGeom(c, cout, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24))
+    x = torch.randn(n, h, w, c, generator=g).to(DEV)
+    xb = x.to(torch.bfloat16)
+    wt = [(torch.randn(cout, 3, 3, c, generator=g) * 0.02).to(DEV) for _ in range(4)]
+    bs = [torch.randn(cout, generator=g).to(DEV) for _ in range(4)]
+    assert k.conv_kernel_id(geom, n, h, w, 0)[0] % 100 in (94, 97, 98, 99)   # inner GEMM on the LDS-DMA kernel
+    assert torch.equal(k.conv_fwd(geom, x, n, h, w, wt, bs, xb=xb), k.conv_fwd(geom, x, n, h, w, wt, bs))
+    gy = torch.randn(n, h, w, cout, generator=g).to(DEV)
+    dw0 = [torch.zeros_like(t) for t in wt]
+    dw1 = [torch.zeros_like(t) for t in wt]
+    k.conv_wgrad(geom, gy, x, n, h, w, dw0, accumulate=False)
+    k.conv_wgrad(geom, gy, x, n, h, w, dw1, accumulate=False, xb=xb)
+    for a, b in zip(dw0, dw1):
+        assert torch.equal(a, b)
