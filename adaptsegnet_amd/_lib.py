@@ -12,7 +12,9 @@ import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libadaptseg.so")
+# ADAPTSEG_LIBRARY: path of another build of the same library (A/B of two builds on one box,
+# experiments/ab_*.sh); default the in-tree build
+LIB_PATH = os.environ.get("ADAPTSEG_LIBRARY") or os.path.join(_HERE, "lib", "libadaptseg.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "adaptseg.h")
 
 ADAPTSEG_OK = 0
@@ -23,7 +25,7 @@ EPI_RESIDUAL = 8
 EPI_RELU = 16
 EPI_RELU_GRAD = 32
 CONV_FWD, CONV_BWD_DATA, CONV_BWD_WEIGHT = 0, 1, 2
-MATH_F32, MATH_BF16, MATH_BF16_WIDE, MATH_F32X3 = 0, 1, 2, 3
+MATH_F32, MATH_BF16, MATH_BF16_WIDE, MATH_F32X3, MATH_F32X3_PRESPLIT = 0, 1, 2, 3, 4
 
 
 class AdaptSegLibraryError(RuntimeError):
@@ -55,6 +57,7 @@ _SIGS = {
     "adaptseg_version": [],
     "adaptseg_conv2d_workspace_size": [_DESC, _I, ctypes.POINTER(_SZ)],
     "adaptseg_conv2d_kernel_id": [_DESC, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
+    "adaptseg_conv2d_copy_operand_only": [_DESC, _I, ctypes.POINTER(_I)],
     "adaptseg_conv2d_fwd": [_DESC, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data": [_DESC, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight": [_DESC, _P, _P, _PP, _PP, _I, _P, _SZ, _P],

@@ -325,7 +325,7 @@ double conv_flops(const adaptseg_conv_desc *d) {
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.g16 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.x3g = pl.g16 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
   const int bm = pl.g16 ? pl.g16_bm : (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
   const int bn = pl.g16 ? pl.g16_bn : pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
@@ -378,7 +378,7 @@ void set_splits(Plan &pl) {
   p.ktiles_per_split = per;
   pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
   if (pl.bf16) pl.slab_bytes += bf16_pre_bytes(pl);
-  if (pl.x3) pl.slab_bytes += (x3_wpack_bytes(pl) + 255) / 256 * 256;
+  if (pl.x3) pl.slab_bytes += x3_pre_bytes(pl);
 }
 
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
@@ -469,11 +469,16 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.bf16 = true;
   }
   // F32X3 conv math: the vector FAST cases whose 16-deep K tiles stay inside one tap
-  pl.x3 = false;
-  if (conv_math() == ADAPTSEG_MATH_F32X3 && pl.fast && !pl.ae && !pl.be) {
+  pl.x3 = pl.x3g = false;
+  const bool x3_math = conv_math() == ADAPTSEG_MATH_F32X3 || conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT;
+  if (x3_math && pl.fast && !pl.ae && !pl.be) {
     if (op == ADAPTSEG_CONV_FWD) pl.x3 = d->c % kX3BK == 0;
     else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3 = d->k % kX3BK == 0;
     else pl.x3 = true;
+    // pre-split operand images by LDS-DMA (conv_x3g.hpp): 16-B chunks of both weight-gradient
+    // operands (Cin, Cout multiples of 8); every F32X3 forward / data gradient qualifies
+    if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT)
+      pl.x3g = op != ADAPTSEG_CONV_BWD_WEIGHT || (d->c % 8 == 0 && d->k % 8 == 0);
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
@@ -516,6 +521,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
+  if (pl.x3g) return 100 * mode + 86 + (pl.s2 ? 1 : 0);
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
@@ -538,7 +544,7 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   hipError_t e;
   int slot;
   if (pl.bf16 || pl.x3) {  // [bf16 weight pack(s)][slabs]
-    const size_t wb = pl.x3 ? (x3_wpack_bytes(pl) + 255) / 256 * 256 : bf16_pre_bytes(pl);
+    const size_t wb = pl.x3 ? x3_pre_bytes(pl) : bf16_pre_bytes(pl);
     if (!ws || ws_bytes < pl.slab_bytes) {
       set_error("conv (%s): workspace %zu < required %zu", pl.x3 ? "f32x3" : "bf16", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
@@ -667,6 +673,17 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
   return ADAPTSEG_OK;
 }
 
+int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *only) {
+  AS_CHECK_ARG(only, "conv2d_copy_operand_only: null");
+  *only = 0;
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  // the conditions the _x entry points accept a NULL fp32 operand under (aligned operands)
+  *only = pl.g16 && !use_thin(d, op) && !tapgemm_eligible(d) ? 1 : 0;
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                         const float *const *bias, const float *res, float *y, int flags, void *ws,
                         size_t ws_bytes, adaptseg_stream_t stream) {
@@ -705,7 +722,10 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
-  AS_CHECK_ARG(x || pl.act_ext, "conv fwd: bf16 input copy must be 16-byte aligned when x is NULL");
+  // a misaligned weight clears pl.fast and, in set_splits, the bf16-operand kernel: only that
+  // kernel reads the copy, so a NULL x needs it to survive the alignment checks too
+  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext),
+               "conv fwd: x is NULL but the plan (after the alignment checks) needs the fp32 input");
   p.out = y;
   p.outb = reinterpret_cast<__bf16 *>(y_bf16);
   p.res = res;
@@ -765,7 +785,8 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
-  AS_CHECK_ARG(x || pl.act_ext, "conv fwd_bnstats: bf16 input copy must be 16-byte aligned when x is NULL");
+  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext),
+               "conv fwd_bnstats: x is NULL but the plan (after the alignment checks) needs the fp32 input");
   p.out = y;
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
@@ -818,7 +839,8 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(dy_bf16) ? dy_bf16 : nullptr;
-  AS_CHECK_ARG(dy || pl.act_ext, "conv bwd_data: bf16 dY copy must be 16-byte aligned when dy is NULL");
+  AS_CHECK_ARG(dy || (pl.g16 && pl.act_ext),
+               "conv bwd_data: dy is NULL but the plan (after the alignment checks) needs the fp32 dY");
   p.out = dx;
   p.outb = reinterpret_cast<__bf16 *>(dx_bf16);
   p.res = res;
@@ -866,7 +888,8 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
       pl.act_ext = dy_bf16;
       pl.act_ext2 = x_bf16;
     }
-    AS_CHECK_ARG((dy && x) || pl.act_ext, "conv bwd_weight: bf16 copies must be 16-byte aligned when dy / x is NULL");
+    AS_CHECK_ARG((dy && x) || (pl.g16 && pl.act_ext),
+                 "conv bwd_weight: dy / x is NULL but the plan (after the alignment checks) needs the fp32 operands");
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
     st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
   }
@@ -898,7 +921,7 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
 
 int adaptseg_conv_set_math(int math) {
   AS_CHECK_ARG(math == ADAPTSEG_MATH_F32 || math == ADAPTSEG_MATH_BF16 || math == ADAPTSEG_MATH_BF16_WIDE ||
-                   math == ADAPTSEG_MATH_F32X3,
+                   math == ADAPTSEG_MATH_F32X3 || math == ADAPTSEG_MATH_F32X3_PRESPLIT,
                "conv_set_math: bad math %d", math);
   g_conv_math.store(math);
   return ADAPTSEG_OK;

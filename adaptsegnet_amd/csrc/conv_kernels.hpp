@@ -1256,6 +1256,7 @@ struct Plan {
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
   bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
   bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
+  bool x3g;    // ... on pre-split operand images by LDS-DMA (conv_x3g.hpp), MATH_F32X3_PRESPLIT
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
   int g16_bm, g16_bn, g16_bk;
@@ -1310,6 +1311,7 @@ hipError_t prep_bf16(Plan &pl, void *ws, hipStream_t s);   // the weight pack
 hipError_t launch_bf16(const Plan &pl, void *ws, hipStream_t s);
 // F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)
 size_t x3_wpack_bytes(const Plan &pl);
+size_t x3_pre_bytes(const Plan &pl);   // workspace ahead of the slabs: weight pack + x3g term images
 hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s);    // the weight pack
 hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s);  // the GEMM
 hipError_t launch_dgrad(const Plan &pl, hipStream_t s);

@@ -1,6 +1,6 @@
-// Kernel instantiations and host launcher of the F32X3 conv math (conv_x3.hpp): fp32 convs on
-// the bf16 MFMA through exact three-term bf16 splits.
-#include "conv_x3.hpp"
+// Kernel instantiations and host launcher of the F32X3 conv math (conv_x3.hpp, conv_x3g.hpp):
+// fp32 convs on the bf16 MFMA through exact three-term bf16 splits.
+#include "conv_x3g.hpp"
 
 namespace adaptseg {
 
@@ -23,6 +23,33 @@ size_t x3_wpack_bytes(const Plan &pl) {
   return 3 * (size_t)rows_pad * ktot * sizeof(__bf16);
 }
 
+// elements of ONE term image of the x3g kernel's activation operand (FWD: x, DGRAD / WGRAD:
+// dY) and, for the weight gradient, of x
+size_t x3g_act_elems(const Plan &pl) {
+  const ConvParams &p = pl.p;
+  if (!pl.x3g) return 0;
+  return pl.mode == MODE_FWD ? (size_t)p.n * p.h * p.w * p.c : (size_t)p.n * p.oh * p.ow * p.k;
+}
+size_t x3g_act2_elems(const Plan &pl) {
+  const ConvParams &p = pl.p;
+  return pl.x3g && pl.mode == MODE_WGRAD ? (size_t)p.n * p.h * p.w * p.c : 0;
+}
+static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+
+// workspace ahead of the split-K slabs: [weight pack][three term images of the activation
+// operand (+ of x for the weight gradient) when the caller supplied none]
+size_t x3_pre_bytes(const Plan &pl) {
+  return al256(x3_wpack_bytes(pl)) + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)) +
+         al256(3 * x3g_act2_elems(pl) * sizeof(__bf16));
+}
+
+static void split_copy(const float *x, int n, int h, int w, int c, int sxn, int sxh, int sxw, void *out,
+                       hipStream_t s) {
+  const int64_t n8 = (int64_t)n * h * w * c / 8;
+  x3_split_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192), 256, 0, s>>>(
+      x, n, h, w, c / 8, sxn, sxh, sxw, reinterpret_cast<uint4 *>(out), n8);
+}
+
 hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   int rows_pad, ktot;
@@ -31,6 +58,16 @@ hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const dim3 pg((unsigned)(rows_pad / x3_bn(pl.mode)), (unsigned)(ktot / kX3BK));
   if (pl.mode == MODE_FWD) conv_wpack_x3v_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
   else if (pl.mode == MODE_DGRAD) conv_wpack_x3v_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
+  if (pl.x3g) {   // the operands' term images the caller did not supply
+    char *base = reinterpret_cast<char *>(wpack) + al256(x3_wpack_bytes(pl));
+    if (!pl.act_ext) {
+      if (pl.mode == MODE_FWD) split_copy(p.x, p.n, p.h, p.w, p.c, p.sxn, p.sxh, p.sxw, base, s);
+      else split_copy(p.dy, p.n, p.oh, p.ow, p.k, p.oh * p.ow * p.k, p.ow * p.k, p.k, base, s);
+    }
+    if (pl.mode == MODE_WGRAD && !pl.act_ext2)
+      split_copy(p.x, p.n, p.h, p.w, p.c, p.sxn, p.sxh, p.sxw, base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)),
+                 s);
+  }
   return hipGetLastError();
 }
 
@@ -38,6 +75,20 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(x3_threads(pl.mode));
+  if (pl.x3g) {
+    const char *base = reinterpret_cast<const char *>(wpack) + al256(x3_wpack_bytes(pl));
+    const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext) : reinterpret_cast<const __bf16 *>(base);
+    const uint32_t img = (uint32_t)x3g_act_elems(pl);
+    if (pl.mode == MODE_FWD) igemm_x3g_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, act, img, wb);
+    else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3g_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, act, img, wb);
+    else if (pl.mode == MODE_DGRAD) igemm_x3g_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, act, img, wb);
+    else {
+      const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
+                                       : reinterpret_cast<const __bf16 *>(base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)));
+      igemm_x3g_wgrad_kernel<<<grid, block, 0, s>>>(p, act, img, act2, (uint32_t)x3g_act2_elems(pl));
+    }
+    return hipGetLastError();
+  }
   if (pl.mode == MODE_FWD) igemm_x3_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, wb);
   else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, wb);
   else if (pl.mode == MODE_DGRAD) igemm_x3_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, wb);

@@ -84,16 +84,14 @@ _BF16_SEL: dict = {}
 
 
 def bf16_only(g, n, h, w, ops) -> bool:
-    """True when every listed product of this conv runs on a bf16-operand LDS-DMA kernel
-    (selectors 94 / 97-99, stride-2 data gradients 192 / 193), which reads only the bf16 copy of
-    its activation operand: the fp32 tensor then need not be written at all."""
+    """True when every listed product of this conv runs on a kernel that reads only the bf16
+    copy of its activation operand (the LDS-DMA kernels; the library's own plan,
+    adaptseg_conv2d_copy_operand_only): the fp32 tensor then need not be written at all."""
     for op in ops:
         key = (g, n, h, w, op, K.get_conv_math())
         v = _BF16_SEL.get(key)
         if v is None:
-            kid, _ = K.conv_kernel_id(g, n, h, w, op)
-            sel = kid % 100   # 94 / 97-99: LDS-DMA kernels; 192 / 193: its stride-2 data gradient
-            v = _BF16_SEL[key] = sel in (94, 97, 98, 99) or (op == 1 and sel in (92, 93))
+            v = _BF16_SEL[key] = K.conv_copy_operand_only(g, n, h, w, op)
         if not v:
             return False
     return True
@@ -213,9 +211,6 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None, dyb=None, xb=None
 # ---------------------------------------------------------------------------------------
 def _round_up(v, m):
     return (v + m - 1) // m * m
-
-
-_PAD_THIN_CONVS = True   # the channel-padded thin-conv paths below (False: A/B reference only)
 
 
 def _wgrad_padded(ws, g, dy, x, n, h, w, dw, db=None):
@@ -441,7 +436,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
         bn_backward(model.bn1, dy0, y0, c0, s0, relu=True, dx=dy0, mask_from_x=True)
         gs = model.conv1.geom()
         if need_w and model.conv1.weight.grad is not None:
-            if gs.cin % 4 and _PAD_THIN_CONVS:   # Cin 3: on a 4-channel padded copy of the input
+            if gs.cin % 4:   # Cin 3: on a 4-channel padded copy of the input
                 _wgrad_padded(ws, gs, dy0, ctx.x, n, h, w, model.conv1.weight.grad)
             else:
                 _wgrad(ws, gs, dy0, ctx.x, n, h, w, [model.conv1.weight.grad], strides=ctx.xs)
@@ -523,7 +518,7 @@ class _FCDiscriminatorFn(torch.autograd.Function):
             geo = conv.geom()
             ch, cw, cs = dims[i]
             if need_w and conv.weight.grad is not None:
-                if geo.cin % 4 and _PAD_THIN_CONVS:   # D.conv1 (Cin 19): on a 20-channel padded copy
+                if geo.cin % 4:   # D.conv1 (Cin 19): on a 20-channel padded copy
                     _wgrad_padded(ws, geo, g, acts[i], n, ch, cw, conv.weight.grad, conv.bias.grad)
                 else:
                     _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
@@ -623,7 +618,7 @@ class _DeeplabVGGFn(torch.autograd.Function):
             geo = conv.geom()
             xin, ih, iw, cs, _ = acts[i]
             if need_w and conv.weight.grad is not None:
-                if geo.cin % 4 and _PAD_THIN_CONVS:   # conv1_1 (Cin 3): on a 4-channel padded copy
+                if geo.cin % 4:   # conv1_1 (Cin 3): on a 4-channel padded copy
                     _wgrad_padded(ws, geo, g, xin, n, ih, iw, conv.weight.grad, conv.bias.grad)
                 else:
                     _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)

@@ -17,11 +17,11 @@ import torch
 from . import _lib
 from . import ops as _ops
 from ._lib import (CONV_BWD_DATA, CONV_BWD_WEIGHT, CONV_FWD, EPI_ACCUMULATE, EPI_LEAKY,
-                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_BF16_WIDE, MATH_F32, MATH_F32X3,
+                   EPI_LEAKY_GRAD, EPI_RELU, EPI_RELU_GRAD, EPI_RESIDUAL, MATH_BF16, MATH_BF16_WIDE, MATH_F32, MATH_F32X3, MATH_F32X3_PRESPLIT,
                    ConvDesc, check)
 
 __all__ = [
-    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "MATH_BF16_WIDE", "MATH_F32X3", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
+    "ConvGeom", "set_conv_math", "get_conv_math", "MATH_F32", "MATH_BF16", "MATH_BF16_WIDE", "MATH_F32X3", "MATH_F32X3_PRESPLIT", "conv_fwd", "conv_fwd_bnstats", "conv_dgrad", "conv_wgrad", "bn_fwd_train",
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
@@ -72,7 +72,8 @@ class ConvGeom:
 
 def set_conv_math(math: int) -> None:
     """Process-wide conv arithmetic: MATH_F32X3 (default: fp32 through exact three-term bf16
-    splits on the bf16 MFMA, fp32-accurate, conv_x3.hpp), MATH_F32 (the fp32-input MFMA
+    splits on the bf16 MFMA, fp32-accurate, conv_x3.hpp / conv_x3g.hpp), MATH_F32X3_PRESPLIT (the
+    same arithmetic, every operand split while staged: conv_x3.hpp only), MATH_F32 (the fp32-input MFMA
     kernels) or MATH_BF16 (operands rounded to bf16, fp32 accumulate: BASELINE config c5).  Workspace sizes depend on it,
     so the descriptor cache is keyed on it."""
     _ops.set_math(math)
@@ -126,7 +127,9 @@ def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weigh
     produce them: returns (y, (stats, ntiles)) or (y, None)."""
     strides = tuple(strides or nhwc_strides(n, h, w, g.cin))
     nt = conv_bnstats_tiles(g, n, h, w, strides)
-    if nt == 0:
+    # the tile count is planned for 16-byte aligned operands; an unaligned view (a storage
+    # offset) takes a kernel without fused statistics, so plan the plain forward for it
+    if nt == 0 or not _aligned16(x, *weights):
         return conv_fwd(g, x, n, h, w, weights, strides=strides, xb=xb), None
     oh, ow = g.out_hw(h, w)
     dev = (x if x is not None else xb).device
@@ -135,6 +138,10 @@ def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weigh
     _OP.conv2d_fwd_bnstats(x, xb, list(weights), out, stats, (n, g.cin, h, w), strides, _wshape(g), g.stride,
                            g.pads, g.dils, nt)
     return out, (stats, nt)
+
+
+def _aligned16(*ts) -> bool:
+    return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
@@ -424,6 +431,18 @@ def conv_kernel_id(g: ConvGeom, n, h, w, op, strides=None):
     check(_lib.lib().adaptseg_conv2d_kernel_id(ctypes.byref(d), op, ctypes.byref(kid), ctypes.byref(sp)),
           "conv2d_kernel_id")
     return kid.value, sp.value
+
+
+def conv_copy_operand_only(g: ConvGeom, n, h, w, op, strides=None) -> bool:
+    """True when this conv product (aligned operands) runs on a kernel that reads only the
+    operand copies of the _x forms, so its fp32 operand need not be written
+    (adaptseg_conv2d_copy_operand_only: the plan the entry points check against)."""
+    strides = strides or nhwc_strides(n, h, w, g.cin)
+    d = _desc(g, n, h, w, tuple(strides))[0]
+    only = ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv2d_copy_operand_only(ctypes.byref(d), op, ctypes.byref(only)),
+          "conv2d_copy_operand_only")
+    return bool(only.value)
 
 
 def timing_enable(selector: int = -1, enable: bool = True):

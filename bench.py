@@ -162,7 +162,7 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
 
 def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
-    if sel % 100 in (95, 96):
+    if sel % 100 in (86, 87, 95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
     if sel % 100 >= 90:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
@@ -173,6 +173,8 @@ def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
     if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
+    if sel % 100 in (86, 87):   # F32X3 on pre-split operand images by LDS-DMA (conv_x3g.hpp)
+        return "igemm_x3g_wgrad_kernel" if op == 2 else f"igemm_x3g_kernel<{op}, {'true' if var == 7 else 'false'}>"
     if sel % 100 in (92, 93) and op == 1:   # bf16 LDS-DMA stride-2 data gradient (parity classes)
         bm, bn = (128, 256) if var == 2 else (256, 128)
         return f"igemm_bf16g_kernel<1, {bm}, {bn}, 32, true>"
@@ -213,7 +215,7 @@ def cpu_baseline(threads):
     * c2 shape (single-level Vanilla, 1024x512 source and target): 1 warm-up + 2 timed steps,
       `value` = images/s of the timed steps;
     * c3 shape (multi-level Vanilla, source 1280x720, target 1024x512, D1 + D2): 1 warm-up +
-      1 timed step, reported as `c3_step_s`;
+      2 timed steps, reported as `c3_step_s`;
     * BASELINE config c1 (forward + CrossEntropy2d, 1x3x321x321): 1 warm-up + 1 timed.
     The warm-up keeps oneDNN primitive creation out of the timed steps.
     """
@@ -238,7 +240,7 @@ def cpu_baseline(threads):
         return (time.perf_counter() - t0) / n_timed, G
 
     c2_s, G = run("single-level", (1024, 512), (1024, 512), 2)
-    c3_s, _ = run("multi-level", (1280, 720), (1024, 512), 1)
+    c3_s, _ = run("multi-level", (1280, 720), (1024, 512), 2)
     x1 = torch.from_numpy(R.det_images((1, 3, 321, 321), 5)).float()
     l1 = torch.from_numpy(R.det_labels((1, 321, 321), 6))
     times = []
@@ -252,11 +254,29 @@ def cpu_baseline(threads):
                       f"single-level 1024x512, 1 warm-up + 2 timed, {c2_s:.2f} s/step",
             "c3_step_s": c3_s,
             "c3_sample": "multi-level Vanilla, source 1280x720 + target 1024x512, batch 1, "
-                         "1 warm-up + 1 timed",
+                         "1 warm-up + 2 timed",
             "c3_images_per_s": 1.0 / c3_s,
             "c1_forward_ce_s": times[-1],
             "calibration": "the port times within +6 % (step) / -12 % (c1) of the reference's own "
                            "modules on the same cores (profiles/r1/cpu_calibration.json)"}
+
+
+def init_distributed(backend, local, init=None, set_device=None):
+    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_*): bind the local GPU and create the process group.  ``nccl`` (= RCCL over xGMI)
+    runs its collectives on a HIGH-priority stream, like the step's main chain
+    (StepConfig.main_priority): the generator's bucketed all-reduces, launched from inside its
+    backward, must not queue behind the weight-gradient / discriminator kernels.  ``gloo`` only
+    rehearses the multi-rank path on one GPU.  ``init`` / ``set_device`` default to
+    torch.distributed.init_process_group / torch.cuda.set_device (tests pass stubs)."""
+    init = init or dist.init_process_group
+    (set_device or torch.cuda.set_device)(local)
+    if backend == "nccl":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        init("nccl", device_id=torch.device("cuda", local), pg_options=opts)
+    else:
+        init("gloo")
 
 
 def main():
@@ -287,15 +307,7 @@ def main():
     if args.backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        if args.backend == "nccl":
-            # RCCL on a high-priority stream, like the step's main chain (StepConfig.main_priority):
-            # the G all-reduce launched mid-step must not queue behind the discriminator kernels
-            opts = dist.ProcessGroupNCCL.Options()
-            opts.is_high_priority_stream = True
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
-        else:
-            dist.init_process_group("gloo")
+        init_distributed(args.backend, local)
     dev = torch.device("cuda", local)
 
     from adaptsegnet_amd import kernels as K
@@ -345,12 +357,26 @@ def main():
         # ~400 launches per step, over ONE extra untimed step — inside the timed region those
         # event pairs cost ~2 % of the step.  The timed region keeps only the dominant conv
         # kernel's events (the roofline below).
-        K.timing_enable(dom)
-        K.timing_enable(dom, enable=False)   # resets the record, conv timing off
+        # The same untimed step also brackets EVERY conv launch, for the per-kernel rooflines
+        # of the largest symbols (roofline.by_kernel); the timed region records only `dom`.
+        K.timing_enable(-1)
         K.timing_enable_mem(True)
         trainer.step(args.warmup, batches)
         torch.cuda.synchronize()
         K.timing_enable_mem(False)
+        K.timing_enable(-1, enable=False)
+        by_kernel = []
+        for sel in sorted(inv, key=inv.get, reverse=True)[:6]:
+            ms_, _fl, n_ = K.timing_read_id(sel)
+            if not n_:
+                continue
+            pk, fam = kernel_peak(sel)
+            a_ = inv[sel] / (ms_ / 1e3) / 1e12   # algorithmic FLOPs of one step / summed launch time
+            by_kernel.append({"kernel": selector_symbol(sel), "selector": sel, "achieved": a_, "peak": pk,
+                              "unit": "TFLOP/s", "frac": a_ / pk, "kernel_family": fam,
+                              "launches_per_step": n_, "avg_launch_ms": ms_ / n_,
+                              "algorithmic_tflop_per_step": inv[sel] / 1e12,
+                              "flop_share_of_step": inv[sel] / step_flops})
         for kid, name in K.MEM_KERNELS.items():
             ms_, by_, n_ = K.timing_read_id(kid)
             if n_:
@@ -399,6 +425,9 @@ def main():
                    "conv_math": conv_math,
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
+                   # the same against a fixed denominator (the fp32 MFMA peak), comparable across
+                   # conv maths and rounds (the line above divides by the dominant family's peak)
+                   "step_conv_frac_of_fp32_peak": step_flops / (ms_per_step / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
                    "losses_last_step": losses},
     }
     if not args.no_roofline and k_launches:
@@ -421,7 +450,11 @@ def main():
                            "kernel": selector_symbol(dom), "selector": dom,
                            "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,
-                           "flop_share_of_step": inv[dom] / step_flops}
+                           "flop_share_of_step": inv[dom] / step_flops,
+                           # every large conv symbol (forward / data gradient / weight gradient
+                           # carry similar FLOPs), live over the untimed step before the timed one
+                           "by_kernel": by_kernel,
+                           "by_kernel_source": "hipEvents around every conv launch of one untimed step"}
         # north_star: HBM GB/s of the interp / loss kernels (and the BN passes) vs the peak,
         # live hipEvents over one untimed step right before the timed region
         out["hbm_kernels"] = hbm

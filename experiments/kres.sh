@@ -1,7 +1,7 @@
 #!/bin/bash
-# Register / LDS / spill usage of the kernels in one built object: bash tools/dbg/kres.sh conv_launch_x3 [name-regex]
+# Register / LDS / spill usage of the kernels in one built object: bash experiments/kres.sh conv_launch_x3 [name-regex]
 set -e
-OBJ=$(dirname "$0")/../../adaptsegnet_amd/csrc/build/$1.o
+OBJ=$(dirname "$0")/../adaptsegnet_amd/csrc/build/$1.o
 D=$(mktemp -d)
 LLVM=/opt/rocm/lib/llvm/bin
 $LLVM/llvm-objcopy --dump-section=.hip_fatbin=$D/fat.bin "$OBJ"

@@ -80,8 +80,11 @@ enum adaptseg_conv_math {
   ADAPTSEG_MATH_F32 = 0,
   ADAPTSEG_MATH_BF16 = 1,
   ADAPTSEG_MATH_BF16_WIDE = 2, /* BF16 with 128x256 tiles for fwd / data-grad products with N >= 256 */
-  ADAPTSEG_MATH_F32X3 = 3      /* fp32 on the bf16 MFMA: exact 3-term bf16 splits of both operands,
+  ADAPTSEG_MATH_F32X3 = 3,     /* fp32 on the bf16 MFMA: exact 3-term bf16 splits of both operands,
                                   the 6 products above 2^-23 relative (fp32-accurate; conv_x3.hpp) */
+  ADAPTSEG_MATH_F32X3_PRESPLIT = 4 /* F32X3 arithmetic (bitwise the same results) with the products
+                                  whose operands come in 16-B chunks on the LDS-DMA kernel of
+                                  conv_x3g.hpp, fed PRE-SPLIT bf16 term images (made per call) */
 };
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);
@@ -128,6 +131,12 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
    paths), so that a consumer conv's _x operand needs no conversion pass: the discriminator
    convs (model/discriminator.py:14-27) chain conv -> LeakyReLU -> conv with no BatchNorm
    between.  Contiguous NHWC like y; 2-byte alignment suffices. */
+/* *only = 1 when product `op` of `d` (16-byte aligned operands) runs on a kernel that reads
+   ONLY the operand copies of the _x forms (the LDS-DMA kernels), so the fp32 operand may be
+   NULL and its producer need not write it; 0 otherwise (thin, tap-GEMM, per-element and
+   register-staged kernels read the fp32 operand).  Host-side planning, no GPU.  The same plan
+   the _x entry points check against. */
+int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *only);
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
                           const float *const *w, const float *const *bias, const float *res, float *y,
                           uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);

@@ -29,7 +29,9 @@ def test_version_and_error_paths_without_gpu():
 def test_default_conv_math_selects_f32x3():
     """The library's default conv math is F32X3: the vector products of the step run on the
     split-bf16 kernel (selector 100*op + 95, +1 for the stride-2 parity path); thin and
-    per-element products keep their fp32 kernels."""
+    per-element products keep their fp32 kernels.  F32X3_PRESPLIT moves the products whose
+    operands come in 16-B chunks to the LDS-DMA kernel on pre-split images (100*op + 86 / 87);
+    the stem's channel-padded weight gradient (Cin 4) stays on the staged one."""
     from adaptsegnet_amd import kernels as K
     assert K.get_conv_math() == K.MATH_F32X3
     g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
@@ -40,6 +42,14 @@ def test_default_conv_math_selects_f32x3():
     assert K.conv_kernel_id(stem, 4, 512, 1024, 0, (3 * 512 * 1024, 512 * 1024, 1024, 1))[0] % 100 < 90
     d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))
     assert K.conv_kernel_id(d5, 4, 32, 64, 0)[0] == 80
+    stem4 = K.ConvGeom(4, 64, 7, 7, 2, (3,), (1,))
+    K.set_conv_math(K.MATH_F32X3_PRESPLIT)
+    try:
+        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [86, 186, 286]
+        assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 187
+        assert K.conv_kernel_id(stem4, 4, 512, 1024, 2, (4 * 512 * 1024, 1, 4 * 1024, 4))[0] == 295
+    finally:
+        K.set_conv_math(K.MATH_F32X3)
 
 
 def test_workspace_and_kernel_selection_on_host():

@@ -52,7 +52,7 @@ def _sd(specs, seed):
             for k, v in R.det_state(specs, seed).items()}
 
 
-def _hip_trainer(level, src, tgt, bn_train):
+def _hip_trainer(level, src, tgt, bn_train, gan="Vanilla"):
     from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
     m = DeeplabMulti(num_classes=19)
@@ -64,7 +64,7 @@ def _hip_trainer(level, src, tgt, bn_train):
     d2.load_state_dict(_sd(R.d_specs(), 2002))
     d1, d2 = d1.to(DEV), d2.to(DEV)
     tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2,
-                         StepConfig(level=level, gan="Vanilla", input_size=src, input_size_target=tgt))
+                         StepConfig(level=level, gan=gan, input_size=src, input_size_target=tgt))
     return tr, m, d1, d2
 
 
@@ -75,10 +75,91 @@ def _cos(a, b):
 @pytest.mark.parametrize("bn_train", [True, False], ids=["trainBN", "evalBN"])
 @pytest.mark.parametrize("geom", ["c2", "c3"])
 def test_fullres_step_vs_oracle(geom, bn_train):
+    _step_vs_oracle(geom, bn_train, "Vanilla", 1e-3)
+
+
+@pytest.fixture
+def bf16_math():
+    from adaptsegnet_amd import kernels as K
+    K.set_conv_math(K.MATH_BF16)
+    yield K
+    K.set_conv_math(K.MATH_F32X3)   # the library default
+
+
+@pytest.mark.parametrize("bn_train", [True, False], ids=["trainBN", "evalBN"])
+def test_fullres_c5_bf16_step_vs_oracle(bf16_math, bn_train):
+    """BASELINE config c5's program (multi-level LS-GAN, bf16 conv math, train:578-679) at its own
+    geometry — source 1280x720, target 1024x512, batch 1 — against the fp32 oracle: the bf16
+    LDS-DMA kernels on the producer-written operand copies, with the fp32 activations that only
+    those kernels read never written (engine.bf16_only), run unsplit at this size.  Losses within
+    2e-2 relative (bf16 operand rounding, ~2^-9 per operand through ~100 layers); eval BN: every
+    update cosine >= 0.99.  Train BN: the trunk update is not comparable with the fp32 oracle's
+    at all — the reference's OWN arithmetic with bf16 conv operands moves it to cosine -0.002
+    (experiments/bf16_trainbn_sensitivity.py, profiles/r3/bf16_trainbn_sensitivity.txt: the
+    random-init train-BN trunk gradient is chaotic under bf16 rounding, the losses and heads are
+    not), so the train-BN check is the losses, the heads' update (>= 0.97; the emulation: 0.9998)
+    and the discriminators' (>= 0.85: Adam's first step is nearly sign(g); the emulation 0.92)."""
+    _step_vs_oracle("c3", bn_train, "LS", 2e-2, trunk=not bn_train, d_bound=0.85 if bn_train else None)
+
+
+def test_fullres_c5_bf16_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monkeypatch):
+    """engine.bf16_only at the c5 geometry: one train-BN multi-level LS step with and without the
+    skipping of fp32 activations gives bitwise the same losses and parameters (a skipped tensor is
+    never read by the full-size kernel variants: tests/test_copy_plan_cpu.py lists those)."""
+    from adaptsegnet_amd import engine
+    level, src, tgt = GEOMS["c3"]
+    xs, lab, xt = _batch(src, tgt)
+    b = [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]
+    g = bf16_math.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
+    assert engine.bf16_only(g, 1, 90, 160, (0, 1, 2))   # layer3.conv2 at 1280x720 reads only copies
+    runs = []
+    for skip in (True, False):
+        if not skip:
+            monkeypatch.setattr(engine, "bf16_only", lambda *a, **kw: False)
+        tr, m, d1, d2 = _hip_trainer(level, src, tgt, True, gan="LS")
+        vals = tr.step(0, b).values()
+        torch.cuda.synchronize()
+        runs.append((vals, [{k: v.detach().cpu().clone() for k, v in mm.state_dict().items()} for mm in (m, d1, d2)]))
+    (va, sa), (vb, sb) = runs
+    assert va == vb, (va, vb)
+    for da, db in zip(sa, sb):
+        for k in da:
+            assert torch.equal(da[k], db[k]), k
+
+
+def test_c1_forward_crossentropy2d_vs_oracle():
+    """BASELINE config c1 at its own shape: DeeplabMulti forward (train-mode BN, single head)
+    + utils/loss.py CrossEntropy2d on one 1x3x321x321 tensor (model/deeplab_multi.py:174-194,
+    utils/loss.py:14-36) against the fp64 oracle: outputs within 1e-3 of max|ref|, loss within
+    1e-3 relative; the same with eval-mode BN."""
+    from adaptsegnet_amd.model import DeeplabMulti
+    from adaptsegnet_amd.utils.loss import CrossEntropy2d
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    x = torch.from_numpy(R.det_images((1, 3, 321, 321), 5))
+    lab = torch.from_numpy(R.det_labels((1, 321, 321), 6))
+    G = R.to_torch(R.det_state(R.g_specs(), 1338), trainable=R.g_trainable)
+    m = DeeplabMulti(num_classes=19)
+    m.load_state_dict(_sd(R.g_specs(), 1338))
+    m = m.to(DEV)
+    for train in (True, False):
+        with torch.no_grad():
+            _, p2 = R.g_forward(G, x, (321, 321), train=train)
+            l_ref = float(R.cross_entropy2d(p2, lab))
+            m.train(train)
+            _, q2 = m(x.float().to(DEV), (321, 321))
+            loss = float(CrossEntropy2d()(q2, lab.to(DEV)))
+        err = float((q2.double().cpu() - p2).abs().max() / p2.abs().max())
+        print(f"c1 train={train}: forward rel err {err:.2e}, loss hip={loss:.6f} oracle={l_ref:.6f}")
+        assert q2.shape == p2.shape == (1, 19, 321, 321)
+        assert err < 1e-3
+        assert abs(loss - l_ref) <= 1e-3 * abs(l_ref)
+
+
+def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None):
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     level, src, tgt = GEOMS[geom]
     xs, lab, xt = _batch(src, tgt)
-    cfg = dict(level=level, gan="Vanilla", input_size=src, input_size_target=tgt)
+    cfg = dict(level=level, gan=gan, input_size=src, input_size_target=tgt)
     # oracle, fp32 on the host cores
     G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
     D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=torch.float32, trainable=lambda k: True)
@@ -86,11 +167,11 @@ def test_fullres_step_vs_oracle(geom, bn_train):
     opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
     ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
     # HIP engine
-    tr, m, d1, d2 = _hip_trainer(level, src, tgt, bn_train)
+    tr, m, d1, d2 = _hip_trainer(level, src, tgt, bn_train, gan=gan)
     got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()
     for k, v in ref.items():
-        print(f"{geom} bn_train={bn_train} {k}: hip={got[k]:.6f} oracle={v:.6f}")
-        assert abs(got[k] - v) <= 1e-3 * abs(v) + 1e-6, (k, got[k], v)
+        print(f"{geom} {gan} bn_train={bn_train} {k}: hip={got[k]:.6f} oracle={v:.6f}")
+        assert abs(got[k] - v) <= tol * abs(v) + 1e-6, (k, got[k], v)
     # parameter updates (new - initial), per group
     g0 = R.det_state(R.g_specs(), 1338)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
@@ -102,6 +183,8 @@ def test_fullres_step_vs_oracle(geom, bn_train):
             groups["heads" if k.startswith(("layer5", "layer6")) else "trunk"].append(k)
     bound = 0.97 if bn_train else 0.99
     for gname, keys in groups.items():
+        if gname == "trunk" and not trunk:
+            continue
         u_ref = torch.cat([(G[k].detach().double() - torch.from_numpy(g0[k])).flatten() for k in keys])
         u_hip = torch.cat([(sd[k].double() - torch.from_numpy(g0[k])).flatten() for k in keys])
         c = _cos(u_hip, u_ref)
@@ -116,7 +199,7 @@ def test_fullres_step_vs_oracle(geom, bn_train):
         u_hip = torch.cat([(dsd[k].double().cpu() - torch.from_numpy(d0[k])).flatten() for k in DD])
         c = _cos(u_hip, u_ref)
         print(f"{geom} bn_train={bn_train} {dname} update cosine {c:.6f}")
-        assert c >= bound, (dname, c)
+        assert c >= (d_bound or bound), (dname, c)
 
 
 TRAJ_RUNS = {"c2_train": ("c2", True), "c2_eval": ("c2", False), "c3_train": ("c3", True)}

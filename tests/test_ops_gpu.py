@@ -86,12 +86,14 @@ def _ref_conv(x, ws, bs, stride, pads, dils):
     return out
 
 
-@pytest.fixture(params=["f32", "f32x3"])
+@pytest.fixture(params=["f32", "f32x3", "f32x3_presplit"])
 def conv_math(request):
-    """The two fp32 conv maths: exact fp32 MFMA and F32X3 (fp32 through exact 3-term bf16
-    splits on the bf16 MFMA, conv_x3.hpp) — both held to the same fp64 tolerance."""
+    """The fp32 conv maths: exact fp32 MFMA, F32X3 (fp32 through exact 3-term bf16 splits on the
+    bf16 MFMA, every operand split while staged, conv_x3.hpp) and F32X3_PRESPLIT (the same
+    arithmetic on pre-split operand images by LDS-DMA where the operands allow, conv_x3g.hpp) —
+    all held to the same fp64 tolerance."""
     k = K()
-    k.set_conv_math(k.MATH_F32 if request.param == "f32" else k.MATH_F32X3)
+    k.set_conv_math({"f32": k.MATH_F32, "f32x3": k.MATH_F32X3, "f32x3_presplit": k.MATH_F32X3_PRESPLIT}[request.param])
     yield request.param
     k.set_conv_math(k.MATH_F32X3)   # the library default
 
@@ -603,8 +605,9 @@ def test_torch_ops_conv_and_ce_vs_oracle():
 def test_f32x3_accuracy_matches_fp32_mfma(op):
     """F32X3 is fp32-accurate: on a layer3-shaped atrous conv (K = 2304) and a wide 1x1 (K =
     1024) its max error vs fp64 stays within 1.5x that of the exact fp32-MFMA kernel (the dropped
-    split terms are below one fp32 rounding per product), and the F32X3 kernel is the one
-    selected (selector 100*op + 95)."""
+    split terms are below one fp32 rounding per product), for both F32X3 kernels (the
+    register-staged one, selector 100*op + 95, and the pre-split LDS-DMA one under
+    F32X3_PRESPLIT, + 86)."""
     k = K()
     g = torch.Generator().manual_seed(77)
     errs = {}
@@ -619,11 +622,11 @@ def test_f32x3_accuracy_matches_fp32_mfma(op):
             ref = torch.nn.grad.conv2d_input(x.shape, wt, gy, 1, geom.pads[0], dil)
         else:
             ref = torch.nn.grad.conv2d_weight(x, wt.shape, gy, 1, geom.pads[0], dil)
-        for math in ("f32", "f32x3"):
-            k.set_conv_math(k.MATH_F32 if math == "f32" else k.MATH_F32X3)
+        for math in ("f32", "f32x3", "f32x3_presplit"):
+            k.set_conv_math({"f32": k.MATH_F32, "f32x3": k.MATH_F32X3, "f32x3_presplit": k.MATH_F32X3_PRESPLIT}[math])
             try:
                 sel, _ = k.conv_kernel_id(geom, n, h, w, op)
-                assert (sel % 100 in (95, 96)) == (math == "f32x3"), (math, sel)
+                assert sel % 100 == {"f32": sel % 100 if sel % 100 < 80 else -1, "f32x3": 95, "f32x3_presplit": 86}[math], (math, sel)
                 if op == 0:
                     out = nchw(k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)]))
                 elif op == 1:
@@ -635,14 +638,16 @@ def test_f32x3_accuracy_matches_fp32_mfma(op):
             finally:
                 k.set_conv_math(k.MATH_F32X3)   # the library default
             errs[math] = rel(out, ref)
-        print(f"op {op} K={cin * ks * ks}: max rel err f32 {errs['f32']:.3e}  f32x3 {errs['f32x3']:.3e}")
+        print(f"op {op} K={cin * ks * ks}: max rel err f32 {errs['f32']:.3e}  f32x3 {errs['f32x3']:.3e}  "
+              f"f32x3_presplit {errs['f32x3_presplit']:.3e}")
         assert errs["f32x3"] <= 1.5 * errs["f32"] + 1e-7, errs
+        assert errs["f32x3_presplit"] <= 1.5 * errs["f32"] + 1e-7, errs
 
 
 @pytest.mark.parametrize("op", [0, 1, 2])
 def test_f32x3_is_unbiased(op):
     """The bf16 MFMA's internal sum does not round to nearest: addends far below the largest one
-    lose their low bits (a downward bias, tools/dbg/mfma_round.hip).  With the five cross terms
+    lose their low bits (a downward bias, experiments/mfma_round.hip).  With the five cross terms
     in the same accumulator as a0*b0 that bias piled up to a mean signed error of -1.1e-8 x
     max|y| on this conv (positive data; fp32 MFMA: +-1e-10); conv_x3.hpp keeps them in their own
     accumulator.  Guard: |mean signed error| <= 1e-9 x max|ref| on all-positive operands, the

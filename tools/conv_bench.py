@@ -78,9 +78,10 @@ def main():
     ap.add_argument("--filter", default="")
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=512)
-    ap.add_argument("--math", choices=("f32", "f32x3", "bf16"), default="f32")
+    ap.add_argument("--math", choices=("f32", "f32x3", "f32x3_presplit", "bf16"), default="f32")
     args = ap.parse_args()
-    K.set_conv_math({"f32": K.MATH_F32, "f32x3": K.MATH_F32X3, "bf16": K.MATH_BF16}[args.math])
+    K.set_conv_math({"f32": K.MATH_F32, "f32x3": K.MATH_F32X3, "f32x3_presplit": K.MATH_F32X3_PRESPLIT,
+                     "bf16": K.MATH_BF16}[args.math])
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     tot_ms, tot_fl = 0.0, 0.0
