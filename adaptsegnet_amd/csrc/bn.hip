@@ -47,6 +47,17 @@ __device__ __forceinline__ float4 act_mask_o(float4 g, int rmode, float4 o, floa
   return g;
 }
 
+// Activation operands (x, the residual, the saved output y) are fp32 or — under the bf16 conv
+// math with bf16 activation storage (config c5) — bf16: four of them as a float4.
+__device__ __forceinline__ float4 lda4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 lda4(const __bf16 *p) {
+  const uint2 u = *reinterpret_cast<const uint2 *>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float lda1(const float *p) { return *p; }
+__device__ __forceinline__ float lda1(const __bf16 *p) { return (float)*p; }
+
 constexpr int kReduceUnroll = 4;
 // ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
 // GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
@@ -61,10 +72,10 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
 
 // Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
 // Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
-template <int MODE>  // 0: stats (shifted by pivot x[0][c]), 1: backward sums
+template <int MODE, typename TX>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
 __global__ void __launch_bounds__(256)
-bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const float *__restrict__ dy,
-                 const float *__restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
+bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
+                 const TX *__restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
                  int64_t rows_per_split, float *__restrict__ partial) {
   const int tr = 256 / tc;
@@ -78,7 +89,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
   float4 piv = make_float4(0, 0, 0, 0);
   float4 is = make_float4(0, 0, 0, 0), ww = is, bb = is;
   if (cok) {
-    if (MODE == 0) piv = *reinterpret_cast<const float4 *>(x + c0);
+    if (MODE == 0) piv = lda4(x + c0);
     else piv = *reinterpret_cast<const float4 *>(mean + c0);
     if (MODE == 1 && (relu == 2 || relu == 4)) {
       is = *reinterpret_cast<const float4 *>(invstd + c0);
@@ -95,10 +106,10 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const float *__restrict__ x, const
       for (int u = 0; u < U; ++u) {
         const int64_t ru = r + (int64_t)u * tr;
         const int64_t e = (ru < r1 ? ru : r) * C + c0;
-        v[u] = *reinterpret_cast<const float4 *>(x + e);
+        v[u] = lda4(x + e);
         if (MODE == 1) {
           g[u] = *reinterpret_cast<const float4 *>(dy + e);
-          if (relu == 1 || relu == 3) o[u] = *reinterpret_cast<const float4 *>(y + e);
+          if (relu == 1 || relu == 3) o[u] = lda4(y + e);
         }
       }
 #pragma unroll
@@ -154,7 +165,8 @@ __device__ __forceinline__ void wave_sum2(const float *p1, const float *p2, int 
 }
 
 // Finalise forward statistics: mean, invstd, running-stat update.  Block = 256 = 4 channels.
-__global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const float *__restrict__ x,
+template <typename TX>
+__global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const TX *__restrict__ x,
                                       const float *__restrict__ partial, float *mean_out,
                                       float *invstd_out, float *running_mean, float *running_var,
                                       float momentum, float eps) {
@@ -167,7 +179,7 @@ __global__ void bn_stats_final_kernel(int64_t rows, int C, int splits, const flo
   double dm = s1 / n;
   double var = s2 / n - dm * dm;
   if (var < 0) var = 0;
-  double mean = (double)x[c] + dm;
+  double mean = (double)lda1(x + c) + dm;
   mean_out[c] = (float)mean;
   invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
@@ -252,18 +264,19 @@ __device__ __forceinline__ uint2 bf16x4_rne(float4 v) {
   return __builtin_bit_cast(uint2, __builtin_convertvector(f, b4v));
 }
 
-__global__ void bn_infer_apply_kernel(int64_t total4, int C, const float *__restrict__ x,
+template <typename TX>
+__global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restrict__ x,
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
-                                      const float *__restrict__ res, float *__restrict__ y, uint2 *yb, int relu) {
+                                      const TX *__restrict__ res, float *__restrict__ y, uint2 *yb, int relu) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
-    float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float4 v = lda4(x + 4 * i);
     float o[4] = {v.x, v.y, v.z, v.w};
     float r4[4] = {0, 0, 0, 0};
     if (res) {
-      float4 r = reinterpret_cast<const float4 *>(res)[i];
+      float4 r = lda4(res + 4 * i);
       r4[0] = r.x; r4[1] = r.y; r4[2] = r.z; r4[3] = r.w;
     }
 #pragma unroll
@@ -287,10 +300,11 @@ constexpr int kApplyUnroll = 4;
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
+template <typename TX>
 __global__ void __launch_bounds__(256)
-bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, const float *__restrict__ mean,
+bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
-                  const float *res, float *y, uint2 *yb, int act) {
+                  const TX *res, float *y, uint2 *yb, int act) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -306,8 +320,8 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, cons
       const int64_t ru = r + (int64_t)u * tr;
       const bool ok = ru < r1;
       const int64_t e = (ok ? ru : r) * C + c0;
-      v[u] = ld4c(x + e);
-      q[u] = res ? ld4c(res + e) : make_float4(0, 0, 0, 0);
+      v[u] = lda4(x + e);
+      q[u] = res ? lda4(res + e) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -324,8 +338,9 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *x, cons
   }
 }
 
+template <typename TX>
 __global__ void __launch_bounds__(256)
-bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, const float *y, const float *x,
+bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, const TX *y, const TX *x,
                       const float *__restrict__ w, const float *__restrict__ b, const float *__restrict__ mean,
                       const float *__restrict__ invstd, const float *__restrict__ coef, float *dx, uint2 *dxb,
                       float *dres, int rmode, int train) {
@@ -348,8 +363,8 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
       const int64_t ru = r + (int64_t)u * tr;
       const int64_t e = (ru < r1 ? ru : r) * C + c0;
       g[u] = ld4c(dy + e);
-      v[u] = train ? ld4c(x + e) : z4;
-      o4[u] = need_y ? ld4c(y + e) : z4;
+      v[u] = train ? lda4(x + e) : z4;
+      o4[u] = need_y ? lda4(y + e) : z4;
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -444,128 +459,16 @@ static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(tot
 
 }  // namespace adaptseg
 
-using namespace adaptseg;
+namespace adaptseg {
 
-extern "C" {
-
-int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes) {
-  AS_CHECK_ARG(bytes && rows > 0 && c > 0, "bn_workspace_size: bad args");
-  *bytes = bn_ws_bytes(rows, c);
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                            float *running_mean, float *running_var, float momentum, float eps,
-                            float *save_mean, float *save_invstd, const float *res, float *y, uint16_t *y_bf16,
-                            int relu, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
-  AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
-  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
-  AS_CHECK_ARG(x && (y || y_bf16) && save_mean && save_invstd, "bn_fwd_train: null pointer");
-  size_t need = bn_ws_bytes(rows, c);
-  if (!ws || ws_bytes < need) {
-    set_error("bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
-    return ADAPTSEG_ERR_WORKSPACE;
-  }
-  hipStream_t s = as_stream(stream);
-  ReducePlan r = reduce_plan(rows, c);
-  float *partial = reinterpret_cast<float *>(ws);
-  int slot;  // x in
-  timing_begin(kTBnReduceStats, s, 4.0 * rows * c, &slot);
-  bn_reduce_kernel<0><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
-                                                                nullptr, nullptr, nullptr, 0, r.per, partial);
-  timing_end(slot, s);
-  AS_CHECK_LAUNCH("bn_reduce<stats>");
-  bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean,
-                                                                   save_invstd, running_mean, running_var,
-                                                                   momentum, eps);
-  AS_CHECK_LAUNCH("bn_stats_final");
-  const ApplyPlan ap = apply_plan(rows, c);
-  timing_begin(kTBnApply, s, 4.0 * rows * c * ((res ? 2 : 1) + (y ? 1 : 0)) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
-  bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                 weight, bias, res, y,
-                                                                 reinterpret_cast<uint2 *>(y_bf16), relu);
-  timing_end(slot, s);
-  AS_CHECK_LAUNCH("bn_apply");
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                          float *running_mean, float *running_var, float momentum, float eps,
-                          float *save_mean, float *save_invstd, const float *res, float *y, int relu,
-                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  return adaptseg_bn_fwd_train_x(rows, c, x, weight, bias, running_mean, running_var, momentum, eps, save_mean,
-                                 save_invstd, res, y, nullptr, relu, ws, ws_bytes, stream);
-}
-
-int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
-                                  const float *weight, const float *bias, float *running_mean, float *running_var,
-                                  float momentum, float eps, float *save_mean, float *save_invstd,
-                                  const float *res, float *y, uint16_t *y_bf16, int relu,
-                                  adaptseg_stream_t stream) {
-  AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
-  AS_CHECK_ARG(stats && ntiles > 0 && x && (y || y_bf16) && save_mean && save_invstd,
-               "bn_fwd_train_tiles: null pointer");
-  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
-  hipStream_t s = as_stream(stream);
-  bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
-                                                                   running_mean, running_var, momentum, eps);
-  AS_CHECK_LAUNCH("bn_tiles_final");
-  const ApplyPlan ap = apply_plan(rows, c);
-  int slot;  // x (+res) in, y out
-  timing_begin(kTBnApply, s, 4.0 * rows * c * ((res ? 2 : 1) + (y ? 1 : 0)) + (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
-  bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                 weight, bias, res, y,
-                                                                 reinterpret_cast<uint2 *>(y_bf16), relu);
-  timing_end(slot, s);
-  AS_CHECK_LAUNCH("bn_apply");
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
-                                const float *weight, const float *bias, float *running_mean, float *running_var,
-                                float momentum, float eps, float *save_mean, float *save_invstd, const float *res,
-                                float *y, int relu, adaptseg_stream_t stream) {
-  return adaptseg_bn_fwd_train_tiles_x(rows, c, stats, ntiles, x, weight, bias, running_mean, running_var, momentum,
-                                       eps, save_mean, save_invstd, res, y, nullptr, relu, stream);
-}
-
-int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                            const float *running_mean, const float *running_var, float eps, const float *res,
-                            float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
-  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
-  AS_CHECK_ARG(x && (y || y_bf16) && running_mean && running_var, "bn_fwd_infer: null pointer");
-  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
-  hipStream_t s = as_stream(stream);
-  int64_t total4 = rows * c / 4;
-  bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight,
-                                                         bias, res, y, reinterpret_cast<uint2 *>(y_bf16), relu);
-  AS_CHECK_LAUNCH("bn_infer_apply");
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                          const float *running_mean, const float *running_var, float eps, const float *res,
-                          float *y, int relu, adaptseg_stream_t stream) {
-  return adaptseg_bn_fwd_infer_x(rows, c, x, weight, bias, running_mean, running_var, eps, res, y, nullptr, relu,
-                                 stream);
-}
-
-static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
-                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
-                       uint16_t *dx_bf16, float *dres, int relu, int train, float *dweight, float *dbias, void *ws,
-                       size_t ws_bytes, adaptseg_stream_t stream) {
-  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
-  AS_CHECK_ARG(dy && (dx || dx_bf16) && save_invstd && (!train || (x && save_mean)), "bn_bwd: null pointer");
-  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
-  AS_CHECK_ARG(!relu || y || train, "bn_bwd: activation without y needs train mode (mask from x)");
-  AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
-  // mask mode: ReLU 1 (from the saved output y) / 2 (recomputed from x, y == NULL);
-  // LeakyReLU 3 (from y) / 4 (from x)
-  const int rmode = relu == 0 ? 0 : relu == 1 ? (y ? 1 : 2) : (y ? 3 : 4);
-  hipStream_t s = as_stream(stream);
+template <typename TX>
+int bn_bwd_launch(int64_t rows, int c, const float *dy, const TX *y, const TX *x, const float *weight,
+                         const float *bias, const float *save_mean, const float *save_invstd, float *dx,
+                         uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
+                         size_t ws_bytes, hipStream_t s) {
   float *coef = nullptr;
   int slot;
+  const double eb = sizeof(TX);   // bytes per activation element (x, y)
   if (train) {
     size_t need = bn_ws_bytes(rows, c);
     if (!ws || ws_bytes < need) {
@@ -576,10 +479,9 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
     float *partial = reinterpret_cast<float *>(ws);
     coef = partial + (size_t)r.splits * 2 * c;
     // dy, x (+ y for the mask from y) in
-    timing_begin(kTBnReduceBwd, s, 4.0 * rows * c * (2 + ((rmode == 1 || rmode == 3) ? 1 : 0)), &slot);
-    bn_reduce_kernel<1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
-                                                                  save_invstd, weight, bias, rmode, r.per,
-                                                                  partial);
+    timing_begin(kTBnReduceBwd, s, (4.0 + eb * (1 + ((rmode == 1 || rmode == 3) ? 1 : 0))) * rows * c, &slot);
+    bn_reduce_kernel<1, TX><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean, save_invstd,
+                                                                     weight, bias, rmode, r.per, partial);
     timing_end(slot, s);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
@@ -588,7 +490,8 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   }
   // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
-               4.0 * rows * c * (1 + (dx ? 1 : 0) + (train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0) + (dres ? 1 : 0)) +
+               (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * ((train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0))) *
+                       rows * c +
                    (dx_bf16 ? 2.0 * rows * c : 0.0),
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);
@@ -601,19 +504,189 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   return ADAPTSEG_OK;
 }
 
+}  // namespace adaptseg
+
+using namespace adaptseg;
+
+extern "C" {
+
+int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes) {
+  AS_CHECK_ARG(bytes && rows > 0 && c > 0, "bn_workspace_size: bad args");
+  *bytes = bn_ws_bytes(rows, c);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                            float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                            float *y, uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes,
+                            adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
+  AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
+  AS_CHECK_ARG((x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && save_mean && save_invstd,
+               "bn_fwd_train: exactly one of x / x_bf16, and y or y_bf16");
+  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_train: the residual must be stored like x (fp32 or bf16)");
+  size_t need = bn_ws_bytes(rows, c);
+  if (!ws || ws_bytes < need) {
+    set_error("bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
+    return ADAPTSEG_ERR_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  ReducePlan r = reduce_plan(rows, c);
+  float *partial = reinterpret_cast<float *>(ws);
+  const double eb = x ? 4.0 : 2.0;   // bytes per activation element read
+  int slot;  // x in
+  timing_begin(kTBnReduceStats, s, eb * rows * c, &slot);
+  const __bf16 *xb = reinterpret_cast<const __bf16 *>(x_bf16), *rb = reinterpret_cast<const __bf16 *>(res_bf16);
+  if (x)
+    bn_reduce_kernel<0, float><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
+                                                                       nullptr, nullptr, nullptr, 0, r.per, partial);
+  else
+    bn_reduce_kernel<0, __bf16><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, xb, nullptr, nullptr, nullptr,
+                                                                        nullptr, nullptr, nullptr, 0, r.per, partial);
+  timing_end(slot, s);
+  AS_CHECK_LAUNCH("bn_reduce<stats>");
+  if (x)
+    bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean, save_invstd,
+                                                                   running_mean, running_var, momentum, eps);
+  else
+    bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, xb, partial, save_mean,
+                                                                   save_invstd, running_mean, running_var, momentum, eps);
+  AS_CHECK_LAUNCH("bn_stats_final");
+  const ApplyPlan ap = apply_plan(rows, c);
+  timing_begin(kTBnApply, s, eb * rows * c * ((res || res_bf16) ? 2 : 1) + (y ? 4.0 * rows * c : 0.0) +
+                                 (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
+  if (x)
+    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
+                                                                   weight, bias, res, y,
+                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
+  else
+    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, xb, save_mean, save_invstd,
+                                                                   weight, bias, rb, y,
+                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
+  timing_end(slot, s);
+  AS_CHECK_LAUNCH("bn_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          float *running_mean, float *running_var, float momentum, float eps,
+                          float *save_mean, float *save_invstd, const float *res, float *y, int relu,
+                          void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_train_x(rows, c, x, nullptr, weight, bias, running_mean, running_var, momentum, eps,
+                                 save_mean, save_invstd, res, nullptr, y, nullptr, relu, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                  const uint16_t *x_bf16, const float *weight, const float *bias,
+                                  float *running_mean, float *running_var, float momentum, float eps,
+                                  float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                                  float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
+  AS_CHECK_ARG(stats && ntiles > 0 && (x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && save_mean &&
+                   save_invstd,
+               "bn_fwd_train_tiles: null pointer (exactly one of x / x_bf16)");
+  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_train_tiles: the residual must be stored like x (fp32 or bf16)");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
+  hipStream_t s = as_stream(stream);
+  bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
+                                                                   running_mean, running_var, momentum, eps);
+  AS_CHECK_LAUNCH("bn_tiles_final");
+  const ApplyPlan ap = apply_plan(rows, c);
+  const double eb = x ? 4.0 : 2.0;
+  int slot;  // x (+res) in, y out
+  timing_begin(kTBnApply, s, eb * rows * c * ((res || res_bf16) ? 2 : 1) + (y ? 4.0 * rows * c : 0.0) +
+                                 (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
+  if (x)
+    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
+                                                                   weight, bias, res, y,
+                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
+  else
+    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
+        rows, c, ap.tc, ap.per, reinterpret_cast<const __bf16 *>(x_bf16), save_mean, save_invstd, weight, bias,
+        reinterpret_cast<const __bf16 *>(res_bf16), y, reinterpret_cast<uint2 *>(y_bf16), relu);
+  timing_end(slot, s);
+  AS_CHECK_LAUNCH("bn_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                const float *weight, const float *bias, float *running_mean, float *running_var,
+                                float momentum, float eps, float *save_mean, float *save_invstd, const float *res,
+                                float *y, int relu, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_train_tiles_x(rows, c, stats, ntiles, x, nullptr, weight, bias, running_mean, running_var,
+                                       momentum, eps, save_mean, save_invstd, res, nullptr, y, nullptr, relu, stream);
+}
+
+int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, const float *running_mean, const float *running_var, float eps,
+                            const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
+                            adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
+  AS_CHECK_ARG((x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && running_mean && running_var,
+               "bn_fwd_infer: null pointer (exactly one of x / x_bf16)");
+  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_infer: the residual must be stored like x (fp32 or bf16)");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
+  hipStream_t s = as_stream(stream);
+  int64_t total4 = rows * c / 4;
+  if (x)
+    bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight, bias,
+                                                           res, y, reinterpret_cast<uint2 *>(y_bf16), relu);
+  else
+    bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, reinterpret_cast<const __bf16 *>(x_bf16),
+                                                           running_mean, running_var, eps, weight, bias,
+                                                           reinterpret_cast<const __bf16 *>(res_bf16), y,
+                                                           reinterpret_cast<uint2 *>(y_bf16), relu);
+  AS_CHECK_LAUNCH("bn_infer_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
+                          const float *running_mean, const float *running_var, float eps, const float *res,
+                          float *y, int relu, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_infer_x(rows, c, x, nullptr, weight, bias, running_mean, running_var, eps, res, nullptr, y,
+                                 nullptr, relu, stream);
+}
+
+static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, const uint16_t *y_bf16, const float *x,
+                       const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
+                       const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
+                       float *dweight, float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
+  const bool xb = x_bf16 != nullptr;
+  AS_CHECK_ARG(dy && (dx || dx_bf16) && save_invstd && (!train || ((x || x_bf16) && save_mean)), "bn_bwd: null pointer");
+  AS_CHECK_ARG(!(x && x_bf16) && !(y && y_bf16) && (xb ? !y : !y_bf16),
+               "bn_bwd: the saved x and y are both fp32 or both bf16 (one pointer each)");
+  AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
+  AS_CHECK_ARG(!relu || y || y_bf16 || train, "bn_bwd: activation without y needs train mode (mask from x)");
+  AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
+  // mask mode: ReLU 1 (from the saved output y) / 2 (recomputed from x, y == NULL);
+  // LeakyReLU 3 (from y) / 4 (from x)
+  const bool has_y = y || y_bf16;
+  const int rmode = relu == 0 ? 0 : relu == 1 ? (has_y ? 1 : 2) : (has_y ? 3 : 4);
+  hipStream_t s = as_stream(stream);
+  if (xb || (!x && y_bf16))
+    return bn_bwd_launch(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), reinterpret_cast<const __bf16 *>(x_bf16),
+                         weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
+                         ws_bytes, s);
+  return bn_bwd_launch(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
+                       dweight, dbias, ws, ws_bytes, s);
+}
+
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
                     int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, nullptr, dres, relu, train,
-                     nullptr, nullptr, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr, dres, relu,
+                     train, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
-int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
-                      const float *bias, const float *save_mean, const float *save_invstd, float *dx,
-                      uint16_t *dx_bf16, float *dres, int relu, int train, void *ws, size_t ws_bytes,
-                      adaptseg_stream_t stream) {
-  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, relu, train,
-                     nullptr, nullptr, ws, ws_bytes, stream);
+int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const uint16_t *y_bf16, const float *x,
+                      const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
+                      const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
+                      void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return bn_bwd_impl(rows, c, dy, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, relu,
+                     train, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,
@@ -621,8 +694,8 @@ int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y,
                            const float *save_invstd, float *dx, float *dres, int act, float *dweight,
                            float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(dweight || dbias, "bn_bwd_affine: no affine gradient requested");
-  return bn_bwd_impl(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, nullptr, dres, act, 1, dweight,
-                     dbias, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr, dres, act,
+                     1, dweight, dbias, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

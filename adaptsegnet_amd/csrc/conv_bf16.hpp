@@ -70,8 +70,12 @@ __device__ __forceinline__ bf16x8 kc_frag(const char *img, int r0, int ks, int l
 
 // BN_ = 128 (4 waves, 2x2) or 256 (8 waves, 2x4; K-contiguous products only): the wider tile
 // halves the refetch of the gathered fp32 A operand, which bounds this kernel.
-template <int MODE, bool S2, int BN_ = 128>
-__global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+// ABF (forward only): the activation operand is a bf16 NHWC copy `ab` (bf16 activation storage,
+// the fp32 x may not exist): each slot loads its 8 bf16 as one 16-B load, no conversion.
+template <int MODE, bool S2, int BN_ = 128, bool ABF = false>
+__global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const ConvParams p, const __bf16 *__restrict__ wb,
+                                                                            const __bf16 *__restrict__ ab = nullptr) {
+  static_assert(!ABF || MODE == MODE_FWD, "bf16 activation copies: forward products");
   constexpr bool MC = MODE == MODE_WGRAD;      // both operands M/N-contiguous
   constexpr int BM = 128, BN = BN_, BK = kB16BK, NT = bf16_threads(MODE);
   constexpr int WAVES_M = 2, WAVES_N = NT / 128;  // 2x2 (WGRAD) or 2x4 waves
@@ -151,7 +155,8 @@ __global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const
         const int oh = (int)t - (int)b * p.oh;
         a_y[i] = oh * p.stride;
         a_x[i] = ow * p.stride;
-        a_pix[i] = (int)b * p.sxn + a_y[i] * p.sxh + a_x[i] * p.sxw + 8 * ch;
+        a_pix[i] = ABF ? (((int)b * p.h + a_y[i]) * p.w + a_x[i]) * p.c + 8 * ch   // contiguous NHWC copy
+                       : (int)b * p.sxn + a_y[i] * p.sxh + a_x[i] * p.sxw + 8 * ch;
       } else {
         uint32_t t = fdiv((uint32_t)mm, p.fd_w);
         const int iw = mm - (int)t * p.w;
@@ -195,14 +200,21 @@ __global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const
       seg_geom(p, sr, tap, seg, t, dy, dx);
       dy = uni(dy);
       dx = uni(dx);
-      const int soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
+      const int soff = ABF ? uni((dy * p.w + dx) * p.c + kbase - tap * p.c)
+                           : uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const bool v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.h) & ((unsigned)(a_x[i] + dx) < (unsigned)p.w);
         ma[S][i] = v;
-        const float *src = p.x + (v ? a_pix[i] + soff : 0);
-        ra[S][2 * i] = ld4(src);
-        ra[S][2 * i + 1] = ld4(src + 4);
+        if constexpr (ABF) {   // 8 bf16 in the two float4 registers' bits (no conversion at the store)
+          const uint4 q = *reinterpret_cast<const uint4 *>(ab + (v ? a_pix[i] + soff : 0));
+          ra[S][2 * i] = make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z),
+                                     __uint_as_float(q.w));
+        } else {
+          const float *src = p.x + (v ? a_pix[i] + soff : 0);
+          ra[S][2 * i] = ld4(src);
+          ra[S][2 * i + 1] = ld4(src + 4);
+        }
       }
 #pragma unroll
       for (int i = 0; i < NQB; ++i) {
@@ -277,8 +289,15 @@ __global__ void __launch_bounds__(bf16_threads(MODE), 2) igemm_bf16_kernel(const
       const int q = tid + NT * i;
       if constexpr (!MC) {
         const int row = q >> 3, ch = q & 7;
-        const uint2 lo = cvt4_bf16(ra[S][2 * i]), hi = cvt4_bf16(ra[S][2 * i + 1]);
-        const uint4 av = ma[S][i] ? make_uint4(lo.x, lo.y, hi.x, hi.y) : make_uint4(0, 0, 0, 0);
+        uint4 av;
+        if constexpr (ABF) {
+          const float4 r = ra[S][2 * i];
+          av = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
+        } else {
+          const uint2 lo = cvt4_bf16(ra[S][2 * i]), hi = cvt4_bf16(ra[S][2 * i + 1]);
+          av = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+        av = ma[S][i] ? av : make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4 *>(As + kc_off(row, ch)) = av;
       } else {
         const int kr = q >> 5, col = 4 * (q & 31);

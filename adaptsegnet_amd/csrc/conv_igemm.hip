@@ -52,7 +52,7 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
       if (p.flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
       v = epi_act(v, p.flags);
       if (p.flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], p.flags);
-      p.out[idx] = v;
+      if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
       if (p.outb) p.outb[idx] = (__bf16)v;
     }
   }
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
         v.z = epi_act_grad(v.z, a.z, p.flags); v.w = epi_act_grad(v.w, a.w, p.flags);
       }
     }
-    *reinterpret_cast<float4 *>(o) = v;
+    if (mode == MODE_WGRAD || p.out) *reinterpret_cast<float4 *>(o) = v;   // p.out NULL: bf16 storage
     if (mode != MODE_WGRAD && p.outb) {
       __bf16 *ob = p.outb + (o - p.out);
       ob[0] = (__bf16)v.x; ob[1] = (__bf16)v.y; ob[2] = (__bf16)v.z; ob[3] = (__bf16)v.w;
@@ -321,6 +321,11 @@ double conv_flops(const adaptseg_conv_desc *d) {
   return 2.0 * d->n * d->oh * d->ow * (double)d->k * d->c * d->kh * d->kw * d->nseg;
 }
 
+// Bytes of the split-K slabs [splits][M][N] fp32, 256-B aligned (the tile counters follow).
+size_t splitk_slab_bytes(const Plan &pl) {
+  return ((size_t)pl.p.splits * pl.p.M * pl.p.N * sizeof(float) + 255) / 256 * 256;
+}
+
 // Grid decomposition: tiles, then split K until the grid has ~2 blocks per CU while keeping
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
@@ -376,7 +381,8 @@ void set_splits(Plan &pl) {
   splits = (int)ceil_div(nkt, per);
   p.splits = splits;
   p.ktiles_per_split = per;
-  pl.slab_bytes = splits > 1 ? (size_t)splits * p.M * p.N * sizeof(float) : 0;
+  // split-K slabs + one arrival counter per output tile (folded epilogue), 256-B aligned
+  pl.slab_bytes = splits > 1 ? splitk_slab_bytes(pl) + (sizeof(unsigned) * (size_t)pl.tiles + 255) / 256 * 256 : 0;
   if (pl.bf16) pl.slab_bytes += bf16_pre_bytes(pl);
   if (pl.x3) pl.slab_bytes += x3_pre_bytes(pl);
 }
@@ -388,6 +394,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   fill_common(p, d);
   pl.mode = op;
   pl.act_ext = pl.act_ext2 = nullptr;
+  pl.wpack_ext = nullptr;
   const bool nhwc_in = d->in_stride[1] == 1;
   if (op == ADAPTSEG_CONV_FWD) {
     p.M = d->n * d->oh * d->ow;
@@ -532,59 +539,84 @@ int kernel_id(const Plan &pl, int mode) {
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
 }
 
+// Split-K outputs: the operands of the final sum are 16-byte aligned float4 rows (the folded
+// epilogue and splitk_reduce4_kernel both need that; else the scalar splitk_reduce_kernel).
+#ifndef ADAPTSEG_SPLITK_FOLD
+#define ADAPTSEG_SPLITK_FOLD 1
+#endif
+
+static bool splitk_vec(const ConvParams &q, const float *slab, const float *final_out, int mode) {
+  bool vec = q.N % 4 == 0 && aligned16(slab);
+  if (mode == MODE_WGRAD) {
+    vec = vec && q.kseg % 4 == 0;
+    for (int g = 0; g < q.nseg; ++g) vec = vec && aligned16(q.dw[g]);
+  } else {
+    vec = vec && aligned16(final_out) && (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res)) &&
+          (!(q.flags & kEpiActGrad) || aligned16(q.aux));
+    if (mode == MODE_FWD)
+      for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
+  }
+  return vec;
+}
+
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
-  if (pl.p.splits > 1 && !pl.bf16 && !pl.x3) {
-    if (!ws || ws_bytes < pl.slab_bytes) {
+  pl.p.tile_ctr = nullptr;
+  pl.p.fold_out = final_out;
+  if (!ws || ws_bytes < pl.slab_bytes) {
+    if (pl.slab_bytes) {
       set_error("conv: workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
       return ADAPTSEG_ERR_WORKSPACE;
     }
-    pl.p.out = reinterpret_cast<float *>(ws);
+  }
+  // workspace: [weight pack / operand copies (F32X3, bf16)][split-K slabs][tile counters]
+  const size_t pre = pl.x3 ? x3_pre_bytes(pl) : pl.bf16 ? bf16_pre_bytes(pl) : 0;
+  float *slab = nullptr;
+  bool fold = false;
+  if (pl.p.splits > 1) {
+    slab = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + pre);
+    pl.p.out = slab;
+    // the weight gradients of every kernel with the shared igemm_epilogue (the FAST / bf16 /
+    // F32X3 families) fold the split-K sum into their last-arriving split; the generic kernel
+    // and the (few) split forward / data gradients keep the reduce launch
+    fold = ADAPTSEG_SPLITK_FOLD && mode == MODE_WGRAD && pl.fast && splitk_vec(pl.p, slab, final_out, mode);
+    if (fold) {
+      unsigned *ctr = reinterpret_cast<unsigned *>(reinterpret_cast<char *>(slab) + splitk_slab_bytes(pl));
+      const hipError_t me = hipMemsetAsync(ctr, 0, sizeof(unsigned) * (size_t)pl.tiles, s);
+      if (me != hipSuccess) {
+        set_error("conv: tile-counter memset: %s", hipGetErrorString(me));
+        return ADAPTSEG_ERR_HIP;
+      }
+      pl.p.tile_ctr = ctr;
+    }
   }
   hipError_t e;
   int slot;
-  if (pl.bf16 || pl.x3) {  // [bf16 weight pack(s)][slabs]
-    const size_t wb = pl.x3 ? x3_pre_bytes(pl) : bf16_pre_bytes(pl);
-    if (!ws || ws_bytes < pl.slab_bytes) {
-      set_error("conv (%s): workspace %zu < required %zu", pl.x3 ? "f32x3" : "bf16", ws_bytes, pl.slab_bytes);
-      return ADAPTSEG_ERR_WORKSPACE;
-    }
-    if (pl.p.splits > 1) pl.p.out = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + wb);
-    // weight pack (+ bf16 activation copies) first, outside the timed bracket: the live
-    // roofline times the GEMM kernel alone, as rocprof reports it
+  if (pl.bf16 || pl.x3) {
+    // weight pack (+ operand copies) first, outside the timed bracket: the live roofline
+    // times the GEMM kernel alone, as rocprof reports it
     e = pl.x3 ? prep_x3(pl, ws, s) : prep_bf16(pl, ws, s);
     if (e == hipSuccess) {
       timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
       e = pl.x3 ? launch_x3(pl, ws, s) : launch_bf16(pl, ws, s);
       timing_end(slot, s);
     }
-    ws = reinterpret_cast<char *>(ws) + wb;  // the reduce below reads the slabs
   } else {
-  timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
-  if (mode == MODE_FWD) e = launch_fwd(pl, s);
-  else if (mode == MODE_DGRAD) e = launch_dgrad(pl, s);
-  else e = launch_wgrad(pl, s);
-  timing_end(slot, s);
+    timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
+    if (mode == MODE_FWD) e = launch_fwd(pl, s);
+    else if (mode == MODE_DGRAD) e = launch_dgrad(pl, s);
+    else e = launch_wgrad(pl, s);
+    timing_end(slot, s);
   }
   if (e != hipSuccess) {
     set_error("igemm launch: %s", hipGetErrorString(e));
     return ADAPTSEG_ERR_HIP;
   }
-  if (pl.p.splits > 1) {
-    const float *slab = reinterpret_cast<const float *>(ws);
+  if (pl.p.splits > 1 && !fold) {
     ConvParams q = pl.p;
     q.out = final_out;
-    size_t total = (size_t)q.M * q.N;
-    bool vec = q.N % 4 == 0 && aligned16(slab);
-    if (mode == MODE_WGRAD) {
-      vec = vec && q.kseg % 4 == 0;
-      for (int g = 0; g < q.nseg; ++g) vec = vec && aligned16(q.dw[g]);
-    } else {
-      vec = vec && aligned16(q.out) && (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res)) &&
-            (!(q.flags & kEpiActGrad) || aligned16(q.aux));
-      if (mode == MODE_FWD)
-        for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
-    }
+    const size_t total = (size_t)q.M * q.N;
+    const bool vec = splitk_vec(q, slab, final_out, mode);
     int slot;  // the slabs + read-modify-write operands in, the output out
     const int extra = (q.flags & ADAPTSEG_EPI_ACCUMULATE ? 1 : 0) +
                       (mode != MODE_WGRAD && (q.flags & ADAPTSEG_EPI_RESIDUAL) ? 1 : 0) +
@@ -625,6 +657,33 @@ static int out_copy(const float *y, uint16_t *yb, int64_t n, hipStream_t s) {
 
 // Thin convs (Cout <= 4) go to the vector-ALU kernels of conv_thin.hip.
 bool use_thin(const adaptseg_conv_desc *d, int op) { return thin_eligible(d, op); }
+
+// The plan's kernel reads only the operand copies of the _x forms (the fp32 operand may be
+// NULL): the LDS-DMA kernels, and the register-staged bf16 forward (its ABF form); for the
+// tap-GEMM (ASPP) products, its inner GEMM's forward / weight gradient on an LDS-DMA kernel.
+static bool copy_only(const Plan &pl, const adaptseg_conv_desc *d, int op) {
+  if (use_thin(d, op)) return false;
+  if (tapgemm_eligible(d)) return tapgemm_copy_only(d, op);
+  return pl.g16 || (pl.bf16 && op == ADAPTSEG_CONV_FWD);
+}
+
+// Bytes of the weight pack the plan's kernel reads (0: none).
+static size_t plan_wpack_bytes(const Plan &pl) {
+  if (pl.mode == MODE_WGRAD) return 0;
+  if (pl.x3) return x3_wpack_bytes(pl);
+  if (pl.bf16) return bf16_wpack_bytes(pl);
+  return 0;
+}
+
+// A caller-built weight pack for the plan (adaptseg_conv2d_wpack): its kernel then skips the
+// per-call pack.  Ignored when the final plan reads none (a misaligned operand downgraded it).
+static int attach_wpack(Plan &pl, const void *w_pack) {
+  pl.wpack_ext = nullptr;
+  if (!w_pack || plan_wpack_bytes(pl) == 0) return ADAPTSEG_OK;
+  AS_CHECK_ARG((reinterpret_cast<uintptr_t>(w_pack) & 15) == 0, "conv: weight pack must be 16-byte aligned");
+  pl.wpack_ext = w_pack;
+  return ADAPTSEG_OK;
+}
 
 }  // namespace adaptseg
 
@@ -680,24 +739,61 @@ int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *
   int st = make_plan(d, op, pl);
   if (st) return st;
   // the conditions the _x entry points accept a NULL fp32 operand under (aligned operands)
-  *only = pl.g16 && !use_thin(d, op) && !tapgemm_eligible(d) ? 1 : 0;
+  *only = copy_only(pl, d, op) ? 1 : 0;
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_wpack_size(const adaptseg_conv_desc *d, int op, size_t *bytes) {
+  AS_CHECK_ARG(bytes, "conv2d_wpack_size: null");
+  *bytes = 0;
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  if (use_thin(d, op) || tapgemm_eligible(d)) return ADAPTSEG_OK;
+  *bytes = plan_wpack_bytes(pl);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_wpack(const adaptseg_conv_desc *d, int op, const float *const *w, void *pack, size_t bytes,
+                          adaptseg_stream_t stream) {
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  AS_CHECK_ARG(w && pack, "conv2d_wpack: null pointer");
+  AS_CHECK_ARG((reinterpret_cast<uintptr_t>(pack) & 15) == 0, "conv2d_wpack: pack must be 16-byte aligned");
+  const size_t need = (use_thin(d, op) || tapgemm_eligible(d)) ? 0 : plan_wpack_bytes(pl);
+  AS_CHECK_ARG(need > 0, "conv2d_wpack: this product reads no weight pack (size 0)");
+  AS_CHECK_ARG(bytes >= need, "conv2d_wpack: %zu bytes < %zu", bytes, need);
+  for (int s = 0; s < d->nseg; ++s) {
+    AS_CHECK_ARG(w[s], "conv2d_wpack: null weight %d", s);
+    pl.p.wt[s] = w[s];
+  }
+  const hipError_t e = pl.x3 ? prep_x3_wpack(pl, pack, as_stream(stream)) : prep_bf16_wpack(pl, pack, as_stream(stream));
+  if (e != hipSuccess) {
+    set_error("conv2d_wpack: %s", hipGetErrorString(e));
+    return ADAPTSEG_ERR_HIP;
+  }
   return ADAPTSEG_OK;
 }
 
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                         const float *const *bias, const float *res, float *y, int flags, void *ws,
                         size_t ws_bytes, adaptseg_stream_t stream) {
-  return adaptseg_conv2d_fwd_x(d, x, nullptr, w, bias, res, y, nullptr, flags, ws, ws_bytes, stream);
+  return adaptseg_conv2d_fwd_x(d, x, nullptr, w, nullptr, bias, res, y, nullptr, flags, ws, ws_bytes, stream);
 }
 
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
-                          const float *const *w, const float *const *bias, const float *res, float *y,
-                          uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                          const float *const *w, const void *w_pack, const float *const *bias, const float *res,
+                          float *y, uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes,
+                          adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
-  AS_CHECK_ARG((x || x_bf16) && w && y, "conv fwd: null pointer");
-  AS_CHECK_ARG(x || (pl.g16 && !use_thin(d, ADAPTSEG_CONV_FWD) && !tapgemm_eligible(d)),
+  AS_CHECK_ARG((x || x_bf16) && w && (y || y_bf16), "conv fwd: null pointer");
+  AS_CHECK_ARG(y || !(use_thin(d, ADAPTSEG_CONV_FWD) || tapgemm_eligible(d)),
+               "conv fwd: this product needs the fp32 output (thin / tap-GEMM path)");
+  AS_CHECK_ARG(y || !(flags & ADAPTSEG_EPI_ACCUMULATE), "conv fwd: ACCUMULATE needs the fp32 output");
+  AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && x_bf16),
                "conv fwd: this product needs the fp32 input (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & kEpiActGrad), "conv fwd: *_GRAD flags not valid");
   AS_CHECK_ARG(!((flags & ADAPTSEG_EPI_LEAKY) && (flags & ADAPTSEG_EPI_RELU)), "conv fwd: LEAKY and RELU");
@@ -724,12 +820,14 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
   // a misaligned weight clears pl.fast and, in set_splits, the bf16-operand kernel: only that
   // kernel reads the copy, so a NULL x needs it to survive the alignment checks too
-  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext),
+  AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd: x is NULL but the plan (after the alignment checks) needs the fp32 input");
   p.out = y;
   p.outb = reinterpret_cast<__bf16 *>(y_bf16);
   p.res = res;
   p.flags = flags;
+  st = attach_wpack(pl, w_pack);
+  if (st) return st;
   return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
 }
 
@@ -759,23 +857,26 @@ int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
 int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w, float *y,
                                 float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
                                 adaptseg_stream_t stream) {
-  return adaptseg_conv2d_fwd_bnstats_x(d, x, nullptr, w, y, stats, stats_bytes, ntiles, ws, ws_bytes, stream);
+  return adaptseg_conv2d_fwd_bnstats_x(d, x, nullptr, w, nullptr, y, nullptr, stats, stats_bytes, ntiles, ws, ws_bytes,
+                                       stream);
 }
 
 int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
-                                  const float *const *w, float *y, float *stats, size_t stats_bytes, int *ntiles,
-                                  void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                                  const float *const *w, const void *w_pack, float *y, uint16_t *y_bf16,
+                                  float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                  adaptseg_stream_t stream) {
   AS_CHECK_ARG(ntiles && stats, "conv fwd_bnstats: null stats / ntiles");
   *ntiles = 0;
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
-  AS_CHECK_ARG((x || x_bf16) && w && y, "conv fwd_bnstats: null pointer");
-  AS_CHECK_ARG(x || (pl.g16 && !tapgemm_eligible(d)),
+  AS_CHECK_ARG((x || x_bf16) && w && (y || y_bf16), "conv fwd_bnstats: null pointer");
+  AS_CHECK_ARG(y || !tapgemm_eligible(d), "conv fwd_bnstats: this product needs the fp32 output");
+  AS_CHECK_ARG(x || copy_only(pl, d, ADAPTSEG_CONV_FWD),
                "conv fwd_bnstats: this product needs the fp32 input (no bf16-operand kernel for it)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
   if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
-    return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, y, nullptr, 0, ws, ws_bytes, stream);
+    return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, nullptr, y, y_bf16, 0, ws, ws_bytes, stream);
   ConvParams &p = pl.p;
   p.x = x;
   for (int s = 0; s < d->nseg; ++s) {
@@ -785,9 +886,10 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
-  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext),
+  AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd_bnstats: x is NULL but the plan (after the alignment checks) needs the fp32 input");
   p.out = y;
+  p.outb = reinterpret_cast<__bf16 *>(y_bf16);
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
     const int nt = (int)ceil_div(p.M, pl.g16 ? pl.g16_bm : kCfgBM[pl.cfg]);
@@ -797,23 +899,26 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
       *ntiles = nt;
     }
   }
+  st = attach_wpack(pl, w_pack);
+  if (st) return st;
   return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
                              const float *res, const float *aux, float *dx, int flags, void *ws,
                              size_t ws_bytes, adaptseg_stream_t stream) {
-  return adaptseg_conv2d_bwd_data_x(d, dy, nullptr, w, res, aux, dx, nullptr, flags, ws, ws_bytes, stream);
+  return adaptseg_conv2d_bwd_data_x(d, dy, nullptr, w, nullptr, res, aux, dx, nullptr, flags, ws, ws_bytes, stream);
 }
 
 int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
-                               const float *const *w, const float *res, const float *aux, float *dx,
-                               uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+                               const float *const *w, const void *w_pack, const float *res, const float *aux,
+                               float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
+                               adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
   AS_CHECK_ARG((dy || dy_bf16) && w && dx, "conv bwd_data: null pointer");
-  AS_CHECK_ARG(dy || (pl.g16 && !use_thin(d, ADAPTSEG_CONV_BWD_DATA) && !tapgemm_eligible(d)),
+  AS_CHECK_ARG(dy || copy_only(pl, d, ADAPTSEG_CONV_BWD_DATA),
                "conv bwd_data: this product needs the fp32 dY (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY | ADAPTSEG_EPI_RELU)), "conv bwd_data: LEAKY/RELU not valid");
   AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv bwd_data: residual flag without res");
@@ -846,6 +951,8 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   p.res = res;
   p.aux = aux;
   p.flags = flags;
+  st = attach_wpack(pl, w_pack);
+  if (st) return st;
   return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
 }
 
@@ -862,8 +969,8 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
   int st = make_plan(d, ADAPTSEG_CONV_BWD_WEIGHT, pl);
   if (st) return st;
   AS_CHECK_ARG((dy || dy_bf16) && (x || x_bf16) && dw, "conv bwd_weight: null pointer");
-  AS_CHECK_ARG((dy && x) || (dy_bf16 && x_bf16 && pl.g16 && !db && !use_thin(d, ADAPTSEG_CONV_BWD_WEIGHT) &&
-                             !tapgemm_eligible(d)),
+  AS_CHECK_ARG((dy && x) || (dy_bf16 && x_bf16 && copy_only(pl, d, ADAPTSEG_CONV_BWD_WEIGHT) && !db) ||
+                   (tapgemm_eligible(d) && dy && x_bf16 && copy_only(pl, d, ADAPTSEG_CONV_BWD_WEIGHT)),
                "conv bwd_weight: this product needs the fp32 operands (no bf16-operand kernel / bias gradient)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
   hipStream_t s = as_stream(stream);

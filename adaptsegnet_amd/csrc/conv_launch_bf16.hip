@@ -125,9 +125,9 @@ size_t bf16_wpack_bytes(const Plan &pl) {
 }
 
 // Weight pack (untimed: the bench's roofline times the GEMM alone)
-hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
+hipError_t prep_bf16_wpack(const Plan &pl, void *pack, hipStream_t s) {
   const ConvParams &p = pl.p;
-  __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
+  __bf16 *wb = reinterpret_cast<__bf16 *>(pack);
   bool wal = true;   // weights 16-B aligned (the vector forms' float4 loads)
   for (int g = 0; g < p.nseg; ++g) wal = wal && (reinterpret_cast<uintptr_t>(p.wt[g]) & 15) == 0;
   if (pl.mode == MODE_FWD) {
@@ -143,6 +143,15 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
     dim3 g((unsigned)ceil_div(p.c, 64), (unsigned)ceil_div(p.k, 64), (unsigned)p.ntaps);
     if (wal && p.c % 4 == 0 && p.k % 8 == 0) conv_wpack_dgrad_v_kernel<<<g, 256, 0, s>>>(p, wb);
     else conv_wpack_dgrad_kernel<<<g, 256, 0, s>>>(p, wb);
+  }
+  return hipGetLastError();
+}
+
+hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
+  const ConvParams &p = pl.p;
+  if (!pl.wpack_ext) {
+    const hipError_t e = prep_bf16_wpack(pl, wpack, s);
+    if (e != hipSuccess) return e;
   }
   // the activation operands' bf16 copies the caller did not supply, after the (256-B aligned) weight pack
   if (pl.g16) {
@@ -169,7 +178,7 @@ hipError_t prep_bf16(Plan &pl, void *wpack, hipStream_t s) {
 
 hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
-  const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
+  const __bf16 *wb = reinterpret_cast<const __bf16 *>(pl.wpack_ext ? pl.wpack_ext : wpack);
   if (pl.g16) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(bf16_wpack_bytes(pl));
     const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext)
@@ -205,7 +214,11 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   }
   const bool w256 = pl.bf16_bn == 256 && pl.mode != MODE_WGRAD;
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(bf16_threads(pl.mode));
-  if (pl.mode == MODE_FWD) {
+  if (pl.mode == MODE_FWD && pl.act_ext) {   // the caller's bf16 activation copy (bf16 activation storage)
+    const __bf16 *act = reinterpret_cast<const __bf16 *>(pl.act_ext);
+    if (w256) igemm_bf16_kernel<MODE_FWD, false, 256, true><<<grid, block, 0, s>>>(p, wb, act);
+    else igemm_bf16_kernel<MODE_FWD, false, 128, true><<<grid, block, 0, s>>>(p, wb, act);
+  } else if (pl.mode == MODE_FWD) {
     if (w256) igemm_bf16_kernel<MODE_FWD, false, 256><<<grid, block, 0, s>>>(p, wb);
     else igemm_bf16_kernel<MODE_FWD, false, 128><<<grid, block, 0, s>>>(p, wb);
   } else if (pl.mode == MODE_DGRAD && pl.s2) {

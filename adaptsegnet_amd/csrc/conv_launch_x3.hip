@@ -50,14 +50,23 @@ static void split_copy(const float *x, int n, int h, int w, int c, int sxn, int 
       x, n, h, w, c / 8, sxn, sxh, sxw, reinterpret_cast<uint4 *>(out), n8);
 }
 
-hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
+hipError_t prep_x3_wpack(const Plan &pl, void *pack, hipStream_t s) {
   const ConvParams &p = pl.p;
   int rows_pad, ktot;
   x3_pack_dims(pl, rows_pad, ktot);
   // one thread per (row, 8-k chunk), 16-B stores (conv_wpack_x3v_kernel)
   const dim3 pg((unsigned)(rows_pad / x3_bn(pl.mode)), (unsigned)(ktot / kX3BK));
-  if (pl.mode == MODE_FWD) conv_wpack_x3v_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
-  else if (pl.mode == MODE_DGRAD) conv_wpack_x3v_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)wpack, ktot);
+  if (pl.mode == MODE_FWD) conv_wpack_x3v_kernel<MODE_FWD><<<pg, 256, 0, s>>>(p, (char *)pack, ktot);
+  else if (pl.mode == MODE_DGRAD) conv_wpack_x3v_kernel<MODE_DGRAD><<<pg, 256, 0, s>>>(p, (char *)pack, ktot);
+  return hipGetLastError();
+}
+
+hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
+  const ConvParams &p = pl.p;
+  if (!pl.wpack_ext) {
+    const hipError_t e = prep_x3_wpack(pl, wpack, s);
+    if (e != hipSuccess) return e;
+  }
   if (pl.x3g) {   // the operands' term images the caller did not supply
     char *base = reinterpret_cast<char *>(wpack) + al256(x3_wpack_bytes(pl));
     if (!pl.act_ext) {
@@ -73,7 +82,7 @@ hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s) {
 
 hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
-  __bf16 *wb = reinterpret_cast<__bf16 *>(wpack);
+  const __bf16 *wb = reinterpret_cast<const __bf16 *>(pl.wpack_ext ? pl.wpack_ext : wpack);
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(x3_threads(pl.mode));
   if (pl.x3g) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(x3_wpack_bytes(pl));

@@ -188,6 +188,14 @@ int tapgemm_kernel_id(const adaptseg_conv_desc *d, int op, int *kid, int *splits
   return ADAPTSEG_OK;
 }
 
+// The inner GEMM reads only x's bf16 copy, so the _x forms accept x == NULL: forward and weight
+// gradient on an LDS-DMA inner kernel.  The data gradient's tap scatter reads dY in fp32.
+bool tapgemm_copy_only(const adaptseg_conv_desc *d, int op) {
+  Plan pl;
+  if (op == ADAPTSEG_CONV_BWD_DATA || inner_plan(d, op, pl)) return false;
+  return pl.g16;
+}
+
 static int need_ws(const adaptseg_conv_desc *d, int op, size_t ws_bytes, void *ws) {
   const size_t need = tapgemm_workspace(d, op);
   if (!ws || ws_bytes < need) {
@@ -218,6 +226,7 @@ int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_b
   if (st) return st;
   pl.p.x = x;
   pl.act_ext = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;   // read by the bf16 kernels only
+  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext), "conv fwd (tap-GEMM): x is NULL and the inner GEMM needs it");
   pl.p.wt[0] = wp;
   pl.p.out = z;
   pl.p.flags = 0;
@@ -279,6 +288,7 @@ int tapgemm_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float
   pl.p.dy = gbuf;
   pl.p.x = x;
   pl.act_ext2 = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;   // x's copy; dY's is made here
+  AS_CHECK_ARG(x || (pl.g16 && pl.act_ext2), "conv bwd_weight (tap-GEMM): x is NULL and the inner GEMM needs it");
   pl.p.dw[0] = dwp;
   pl.p.flags = 0;
   st = run_plan(pl, MODE_WGRAD, gws, gws_bytes, s);

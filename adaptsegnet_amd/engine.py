@@ -76,7 +76,13 @@ class WgradStream:
 def bf16_operands() -> bool:
     """Under the bf16 conv math (config c5) the BN passes that produce conv operands also write
     a bf16 copy of them, which the bf16 LDS-DMA conv kernel reads instead of converting the
-    fp32 tensor itself (adaptseg_conv2d_*_x): one pass over every such activation less."""
+    fp32 tensor itself (adaptseg_conv2d_*_x): one pass over every such activation less.
+
+    It also stores the generator's activations in bf16, as torch.autocast(bfloat16) does: every
+    Bottleneck conv output (c1, c2, c3, the downsample's), the BN outputs and the residual
+    stream (the block outputs) are bf16 tensors; BatchNorm normalises them in fp32 with fp32
+    statistics (from the conv's fp32 accumulators); the gradients stay fp32.  An fp32 copy of
+    a BN output / block output is written only where a consumer kernel still reads fp32."""
     return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
 
 
@@ -117,7 +123,7 @@ def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False, fp32=True):
         y, mean, invstd = r[:3]
         return y, (mean, invstd, True), (r[3] if bf16 else None)
     r = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
-                       relu=relu, bf16_out=bf16)
+                       relu=relu, bf16_out=bf16, fp32_out=fp32)
     y, yb = r if bf16 else (r, None)
     return y, (bn.running_mean, None, False), yb
 
@@ -152,39 +158,63 @@ class BlockRec:
                  "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b")
 
 
-def _conv_bn(g, x, n, h, w, weight, strides=None, xb=None):
+def _conv_bn(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
     """Conv feeding a train-mode BN: also returns the BN's row-tile statistics (or None)."""
-    return K.conv_fwd_bnstats(g, x, n, h, w, [weight], strides=strides, xb=xb)
+    return K.conv_fwd_bnstats(g, x, n, h, w, [weight], strides=strides, xb=xb, bf16_only=bf16_only)
 
 
-def _conv_plain(g, x, n, h, w, weight, strides=None, xb=None):
-    return K.conv_fwd(g, x, n, h, w, [weight], strides=strides, xb=xb), None
+def _conv_plain(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
+    return K.conv_fwd(g, x, n, h, w, [weight], strides=strides, xb=xb, bf16_only=bf16_only), None
 
 
-def block_forward(blk, x, n, h, w, training, save, xb=None):
-    """xb: bf16 copy of x (bf16 conv math), or None.  Returns (out, rec, bf16 copy of out)."""
+def block_input_fp32(blk, n, h, w) -> bool:
+    """Under bf16 activation storage: does some consumer of this block's INPUT (its conv1 and
+    downsample conv: forward and weight gradient) still read fp32?  Then its producer (the
+    previous block) writes the fp32 output beside the bf16 one."""
+    if not bf16_only(blk.conv1.geom(), n, h, w, (0, 2)):
+        return True
+    return blk.downsample is not None and not bf16_only(blk.downsample[0].geom(), n, h, w, (0, 2))
+
+
+def out_fp32_needed(nxt, cls, n, h, w) -> bool:
+    """Must a block output of (h, w) also be stored in fp32?  Always, unless bf16 activation
+    storage is on; then only when the next Bottleneck ``nxt`` (block_input_fp32) or a classifier
+    ``cls`` reading it (its tap-GEMM forward / weight gradient) still reads fp32."""
+    if not bf16_operands():
+        return True
+    if nxt is not None and block_input_fp32(nxt, n, h, w):
+        return True
+    return cls is not None and not bf16_only(aspp_geom(cls), n, h, w, (0, 2))
+
+
+def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
+    """xb: bf16 copy of x (bf16 conv math), or None; x may be None when xb is given (bf16
+    activation storage).  out_fp32: also write the fp32 block output (bf16 storage: a consumer
+    reads fp32; block_input_fp32).  Returns (out or None, rec, bf16 copy of out)."""
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     oh, ow = g1.out_hw(h, w)
     conv = _conv_bn if training else _conv_plain
-    sh = bf16_operands()
-    # train mode (the BN backward recomputes its ReLU mask from x): y1 / y2 are read only by the
-    # next conv's forward and weight gradient — with both on bf16-operand kernels, only their
-    # bf16 copies are written
-    thin1 = sh and training and bf16_only(g2, n, oh, ow, (0, 2))
-    thin2 = sh and training and bf16_only(g3, n, oh, ow, (0, 2))
-    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb)
+    sh = bf16_operands()   # bf16 conv math: bf16 activation storage + operand copies
+    # y1 / y2 are read only by the next conv's forward and weight gradient (the BN backward
+    # recomputes its ReLU mask from x in train mode, reads the bf16 y in eval mode) — with both
+    # on bf16-operand kernels, only their bf16 copies are written
+    thin1 = sh and bf16_only(g2, n, oh, ow, (0, 2))
+    thin2 = sh and bf16_only(g3, n, oh, ow, (0, 2))
+    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=sh)
     y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh, fp32=not thin1)
-    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b)
+    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=sh)
     y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
-    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b)
+    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=sh)
     cd = sd = None
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
-        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight, xb=xb)
-        r, sd = bn_forward(dbn, cd, None, False, training, td)
+        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight, xb=xb, bf16_only=sh)
+        r, sd, rb = bn_forward_b(dbn, cd, None, False, training, td, bf16=sh, fp32=not sh)
+        if sh:
+            r = rb   # the residual stream is bf16
     else:
-        r = x
-    out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh)
+        r = xb if sh else x
+    out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh, fp32=not sh or out_fp32)
     rec = None
     if save:
         rec = BlockRec()
@@ -192,6 +222,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None):
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         rec.xb, rec.y1b, rec.y2b = xb, y1b, y2b   # the weight gradients' bf16 x operands
+        if sh:
+            rec.out = outb   # bf16 storage: the BN3 backward's mask source is the bf16 output
     return out, rec, outb
 
 
@@ -244,19 +276,19 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
     sh = bf16_operands()   # bf16 copies of each data-gradient operand (bf16 conv math)
-    train = rec.s3[2]
     # a BN-backward output read only by bf16-operand data / weight gradients: copy only
-    f3 = not (sh and train and bf16_only(g3, n, oh, ow, (1, 2)))
-    f2 = not (sh and train and bf16_only(g2, n, oh, ow, (1, 2)))
-    f1 = not (sh and train and rec.xb is not None and bf16_only(g1, n, h, w, (1, 2)))
+    f3 = not (sh and bf16_only(g3, n, oh, ow, (1, 2)))
+    f2 = not (sh and bf16_only(g2, n, oh, ow, (1, 2)))
+    f1 = not (sh and rec.xb is not None and bf16_only(g1, n, h, w, (1, 2)))
     r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
     dc3, dc3b = r if sh else (r, None)
     dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b)
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
-    r = bn_backward(blk.bn2, dy2, rec.y2, rec.c2, rec.s2, relu=True, dx=dy2, mask_from_x=True, bf16=sh,
-                    fp32=f2)
+    # (the saved y is the mask source in eval mode: bf16 like x under bf16 storage)
+    r = bn_backward(blk.bn2, dy2, rec.y2b if sh else rec.y2, rec.c2, rec.s2, relu=True, dx=dy2,
+                    mask_from_x=True, bf16=sh, fp32=f2)
     dy2b = r[1] if sh else None
     if not f2:
         dy2 = None   # not written: its consumers read dy2b
@@ -264,8 +296,8 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
-    r = bn_backward(blk.bn1, dy1, rec.y1, rec.c1, rec.s1, relu=True, dx=dy1, mask_from_x=True, bf16=sh,
-                    fp32=f1)
+    r = bn_backward(blk.bn1, dy1, rec.y1b if sh else rec.y1, rec.c1, rec.s1, relu=True, dx=dy1,
+                    mask_from_x=True, bf16=sh, fp32=f1)
     dy1b = r[1] if sh else None
     if not f1:
         dy1 = None
@@ -274,7 +306,7 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
-        fd = not (sh and train and rec.xb is not None and bf16_only(gd, n, h, w, (1, 2)))
+        fd = not (sh and rec.xb is not None and bf16_only(gd, n, h, w, (1, 2)))
         r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout, bf16=sh, fp32=fd)
         goutb = r[1] if sh else None
         gd_in = gout if fd else None   # gout keeps the residual gradient when not rewritten
@@ -347,19 +379,25 @@ class _DeeplabMultiFn(torch.autograd.Function):
         ph, pw = p.shape[1], p.shape[2]
         recs = []
         cur, curb, ch, cw = p, None, ph, pw
-        for layer in (model.layer1, model.layer2, model.layer3):
-            for blk in layer:
-                nh, nw = blk.conv1.geom().out_hw(ch, cw)
-                cur, rec, curb = block_forward(blk, cur, n, ch, cw, training, save, xb=curb)
-                recs.append(rec)
-                ch, cw = nh, nw
+        blocks = [b for layer in (model.layer1, model.layer2, model.layer3) for b in layer]
+        for i, blk in enumerate(blocks):
+            nh, nw = blk.conv1.geom().out_hw(ch, cw)
+            last = i + 1 == len(blocks)
+            nxt = model.layer4[0] if last else blocks[i + 1]
+            f32 = out_fp32_needed(nxt, model.layer5 if last else None, n, nh, nw)
+            cur, rec, curb = block_forward(blk, cur, n, ch, cw, training, save, xb=curb, out_fp32=f32)
+            recs.append(rec)
+            ch, cw = nh, nw
         p3, h3, w3 = cur, ch, cw
         p3b = curb
         x1 = aspp_forward(model.layer5, p3, n, h3, w3, xb=p3b)
         q, qb = p3, p3b
         recs4 = []
-        for blk in model.layer4:
-            q, rec, qb = block_forward(blk, q, n, h3, w3, training, save, xb=qb)
+        n4 = len(model.layer4)
+        for i, blk in enumerate(model.layer4):
+            last = i + 1 == n4
+            f32 = out_fp32_needed(None if last else model.layer4[i + 1], model.layer6 if last else None, n, h3, w3)
+            q, rec, qb = block_forward(blk, q, n, h3, w3, training, save, xb=qb, out_fp32=f32)
             recs4.append(rec)
         del curb
         x2 = aspp_forward(model.layer6, q, n, h3, w3, xb=qb)

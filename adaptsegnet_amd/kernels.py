@@ -9,6 +9,7 @@ operator of ``adaptsegnet_amd.ops`` (whose CUDA kernel calls the C ABI of includ
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from dataclasses import dataclass
 
@@ -25,7 +26,7 @@ __all__ = [
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
-    "axpy", "add_i64", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
+    "axpy", "add_i64", "weight_pack_scope", "pack_builds", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
 ]
 
 
@@ -89,6 +90,74 @@ def _desc(g: ConvGeom, n, h, w, strides):
     return _ops.conv_desc(n, g.cin, h, w, strides, g.cout, g.kh, g.kw, g.stride, g.pads, g.dils)
 
 
+# ---------------------------------------------------------------------------------------
+# Weight packs, built once per training step
+# ---------------------------------------------------------------------------------------
+class _PackCache:
+    """Caller-owned weight packs (adaptseg_conv2d_wpack) of the F32X3 / bf16 forward and
+    data-gradient kernels.  Active only inside weight_pack_scope(); every pack built inside a
+    scope is stale once the outermost scope exits (the next use rebuilds it in place)."""
+
+    def __init__(self):
+        self.depth = 0       # weight_pack_scope nesting
+        self.epoch = 0       # bumped when the outermost scope exits
+        self.entries = {}    # key -> [pack buffer (uint8), epoch it was built in]
+        self.sizes = {}      # (geometry, op, math) -> pack bytes (0: the kernel reads none)
+        self.builds = 0      # packs built (tests)
+
+
+_PACKS = _PackCache()
+
+
+@contextlib.contextmanager
+def weight_pack_scope():
+    """Inside the scope each conv's weight pack is built ONCE and reused by every forward /
+    data-gradient call on the same weights (a c2 step calls each G conv's forward twice and
+    each D conv's three times); leaving the outermost scope marks every pack stale.  The caller
+    promises not to write the weights inside it: AdaptSegTrainer.step wraps its step body, whose
+    optimiser launches (train_gta2cityscapes_multi.py:532-540) follow the step's last conv.  A
+    weight write between steps (load_state_dict, .data, a user's optimiser) is therefore always
+    seen by the next step's packs.  Outside any scope every call packs for itself."""
+    _PACKS.depth += 1
+    try:
+        yield
+    finally:
+        _PACKS.depth -= 1
+        if _PACKS.depth == 0:
+            _PACKS.epoch += 1
+
+
+def pack_builds() -> int:
+    """Number of weight packs built through the cache so far (tests)."""
+    return _PACKS.builds
+
+
+def _wpack(g, n, h, w, strides, weights, op):
+    """The cached weight pack for this product inside a weight_pack_scope, else None."""
+    if _PACKS.depth == 0:
+        return None
+    math = _ops._CONV_MATH[0]
+    skey = (g, op, math)
+    size = _PACKS.sizes.get(skey)
+    if size is None:
+        d = _desc(g, n, h, w, tuple(strides))[0]
+        b = ctypes.c_size_t(0)
+        check(_lib.lib().adaptseg_conv2d_wpack_size(ctypes.byref(d), op, ctypes.byref(b)), "conv2d_wpack_size")
+        size = _PACKS.sizes[skey] = b.value
+    if size == 0:
+        return None
+    key = (tuple(t.data_ptr() for t in weights), g, op, math)
+    e = _PACKS.entries.get(key)
+    if e is None or e[0].numel() < size:
+        e = _PACKS.entries[key] = [torch.empty(size, dtype=torch.uint8, device=weights[0].device), -1]
+    if e[1] != _PACKS.epoch:
+        _OP.conv2d_wpack(list(weights), e[0], (n, g.cin, h, w), tuple(strides), _wshape(g), g.stride, g.pads,
+                         g.dils, op)
+        e[1] = _PACKS.epoch
+        _PACKS.builds += 1
+    return e[0]
+
+
 def nhwc_strides(n, h, w, c):
     """(n, c, h, w) element strides of a contiguous NHWC buffer."""
     return (h * w * c, 1, w * c, c)
@@ -99,18 +168,29 @@ def _wshape(g: ConvGeom):
 
 
 def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, biases=None,
-             strides=None, out=None, res=None, flags: int = 0, xb=None, bf16_out: bool = False):
+             strides=None, out=None, res=None, flags: int = 0, xb=None, bf16_out: bool = False,
+             bf16_only: bool = False):
     """y[n,oh,ow,cout] = sum_seg conv(x, w_seg) + sum_seg b_seg (+res) (EPI_LEAKY / EPI_RELU).
     xb: optional bf16 copy of x (contiguous NHWC) for the bf16 conv math (bn_* ``bf16_out``).
-    bf16_out: also return a bf16 copy of y written by the epilogue -> (y, yb)."""
+    bf16_out: also return a bf16 copy of y written by the epilogue -> (y, yb).
+    bf16_only: y stored as bf16 only (bf16 activation storage): returns the bf16 tensor."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
     oh, ow = g.out_hw(h, w)
+    dev = (x if x is not None else xb).device
+    if bf16_only:
+        outb = torch.empty((n, oh, ow, g.cout), device=dev, dtype=torch.bfloat16)
+        wp = _wpack(g, n, h, w, strides, weights, CONV_FWD)
+        _OP.conv2d_fwd(x, xb, list(weights), wp, list(biases) if biases is not None else [], res, None, outb,
+                       (n, g.cin, h, w), strides, _wshape(g), g.stride, g.pads, g.dils,
+                       flags | (EPI_RESIDUAL if res is not None else 0))
+        return outb
     if out is None:
-        out = torch.empty((n, oh, ow, g.cout), device=(x if x is not None else xb).device, dtype=torch.float32)
+        out = torch.empty((n, oh, ow, g.cout), device=dev, dtype=torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
     outb = _bf16_like(out, bf16_out)
-    _OP.conv2d_fwd(x, xb, list(weights), list(biases) if biases is not None else [], res, out, outb,
+    wp = _wpack(g, n, h, w, strides, weights, CONV_FWD)
+    _OP.conv2d_fwd(x, xb, list(weights), wp, list(biases) if biases is not None else [], res, out, outb,
                    (n, g.cin, h, w), strides, _wshape(g), g.stride, g.pads, g.dils, flags)
     return (out, outb) if bf16_out else out
 
@@ -122,22 +202,28 @@ def conv_bnstats_tiles(g: ConvGeom, n: int, h: int, w: int, strides) -> int:
     return nt.value
 
 
-def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, strides=None, xb=None):
+def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, strides=None, xb=None,
+                     bf16_only: bool = False):
     """y = conv(x, w) plus the per-row-tile BatchNorm statistics of y when the kernel can
-    produce them: returns (y, (stats, ntiles)) or (y, None)."""
+    produce them: returns (y, (stats, ntiles)) or (y, None).  bf16_only: y is stored as bf16
+    only (bf16 activation storage, config c5; the statistics still come from the fp32
+    accumulators)."""
     strides = tuple(strides or nhwc_strides(n, h, w, g.cin))
     nt = conv_bnstats_tiles(g, n, h, w, strides)
     # the tile count is planned for 16-byte aligned operands; an unaligned view (a storage
     # offset) takes a kernel without fused statistics, so plan the plain forward for it
     if nt == 0 or not _aligned16(x, *weights):
-        return conv_fwd(g, x, n, h, w, weights, strides=strides, xb=xb), None
+        return conv_fwd(g, x, n, h, w, weights, strides=strides, xb=xb, bf16_only=bf16_only), None
     oh, ow = g.out_hw(h, w)
     dev = (x if x is not None else xb).device
-    out = torch.empty((n, oh, ow, g.cout), device=dev, dtype=torch.float32)
+    shape = (n, oh, ow, g.cout)
+    out = None if bf16_only else torch.empty(shape, device=dev, dtype=torch.float32)
+    outb = torch.empty(shape, device=dev, dtype=torch.bfloat16) if bf16_only else None
     stats = torch.empty(nt * (1 + 2 * g.cout), device=dev, dtype=torch.float32)
-    _OP.conv2d_fwd_bnstats(x, xb, list(weights), out, stats, (n, g.cin, h, w), strides, _wshape(g), g.stride,
-                           g.pads, g.dils, nt)
-    return out, (stats, nt)
+    wp = _wpack(g, n, h, w, strides, weights, CONV_FWD)
+    _OP.conv2d_fwd_bnstats(x, xb, list(weights), wp, out, outb, stats, (n, g.cin, h, w), strides, _wshape(g),
+                           g.stride, g.pads, g.dils, nt)
+    return (outb if bf16_only else out), (stats, nt)
 
 
 def _aligned16(*ts) -> bool:
@@ -155,7 +241,8 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
     if aux is not None and not flags & EPI_RELU_GRAD:
         flags |= EPI_LEAKY_GRAD
     outb = _bf16_like(out, bf16_out)
-    _OP.conv2d_bwd_data(dy, dyb, list(weights), res, aux, out, outb, (n, g.cin, h, w), _wshape(g), g.stride,
+    wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
+    _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, aux, out, outb, (n, g.cin, h, w), _wshape(g), g.stride,
                         g.pads, g.dils, flags)
     return (out, outb) if bf16_out else out
 
@@ -177,12 +264,17 @@ def _bf16_like(t, want):
     return torch.empty(t.shape, device=t.device, dtype=torch.bfloat16) if want else None
 
 
+def _f32_like(t):
+    return torch.empty(t.shape, device=t.device, dtype=torch.float32)
+
+
 def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=None,
                  relu=True, out=None, bf16_out=False, fp32_out=True):
     """bf16_out: also return a bf16 (RNE) copy of y, the operand of a bf16-math conv: (y, mean,
-    invstd, yb).  fp32_out=False (with bf16_out): only the copy is written, y is None."""
+    invstd, yb).  fp32_out=False (with bf16_out): only the copy is written, y is None.
+    x / res may be bf16 tensors (bf16 activation storage), both or neither."""
     c = x.shape[-1]
-    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    y = (_f32_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
     yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
@@ -196,7 +288,7 @@ def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, moment
     """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles."""
     stats, ntiles = tiles
     c = x.shape[-1]
-    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    y = (_f32_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
     yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
@@ -207,7 +299,7 @@ def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, moment
 
 def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None,
                  bf16_out=False, fp32_out=True):
-    y = (torch.empty_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
+    y = (_f32_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
     yb = _bf16_like(x, bf16_out)
     _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, float(eps), int(relu))
     return (y, yb) if bf16_out else y

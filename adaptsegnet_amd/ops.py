@@ -20,6 +20,7 @@ meant for torch.compile's functionalization.
 
 Reference call sites the ops stand in for (file:line in /root/reference):
   conv2d_*            nn.Conv2d in model/deeplab_multi.py:64-75,112,128 / discriminator.py:10-14
+                      (conv2d_wpack: the per-step weight pack, optimiser train:532-540 between steps)
   bn_*                nn.BatchNorm2d (+ReLU, residual)  model/deeplab_multi.py:65-101,130-135
   maxpool2d_*         nn.MaxPool2d(3, 2, 1)             model/deeplab_multi.py:135
   upsample_bilinear_* nn.Upsample(bilinear, align_corners=True)  model/deeplab_multi.py:188-189
@@ -147,40 +148,51 @@ def _op(schema):
 
 
 # ---- convolution ------------------------------------------------------------------------
-@_op("conv2d_fwd(Tensor? x, Tensor? xb, Tensor[] weight, Tensor?[] bias, Tensor? res, Tensor(a!) out, "
-     "Tensor(b!)? outb, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, "
-     "int flags) -> ()")
-def _conv2d_fwd(x, xb, weight, bias, res, out, outb, in_shape, in_stride, w_shape, stride, pad, dil, flags):
+@_op("conv2d_wpack(Tensor[] weight, Tensor(a!) pack, int[] in_shape, int[] in_stride, int[] w_shape, int stride, "
+     "int[] pad, int[] dil, int op) -> ()")
+def _conv2d_wpack(weight, pack, in_shape, in_stride, w_shape, stride, pad, dil, op):
+    d, _, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    check(_lib.lib().adaptseg_conv2d_wpack(ctypes.byref(d), int(op), _ptrs(weight), _p(pack), pack.numel(),
+                                           _stream()), "conv2d_wpack")
+
+
+@_op("conv2d_fwd(Tensor? x, Tensor? xb, Tensor[] weight, Tensor? wpack, Tensor?[] bias, Tensor? res, "
+     "Tensor(a!)? out, Tensor(b!)? outb, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, "
+     "int[] dil, int flags) -> ()")
+def _conv2d_fwd(x, xb, weight, wpack, bias, res, out, outb, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_FWD], out.device)
+    wp, wsz = _ws_args(ws[CONV_FWD], (out if out is not None else outb).device)
     check(_lib.lib().adaptseg_conv2d_fwd_x(
-        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _ptrs(bias) if len(bias) else None, _p(res), _p(out),
-        _p(outb), flags, wp, wsz, _stream()), "conv2d_fwd")
+        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(wpack), _ptrs(bias) if len(bias) else None, _p(res),
+        _p(out), _p(outb), flags, wp, wsz, _stream()), "conv2d_fwd")
 
 
-@_op("conv2d_fwd_bnstats(Tensor? x, Tensor? xb, Tensor[] weight, Tensor(a!) out, Tensor(b!) stats, "
-     "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int ntiles) -> ()")
-def _conv2d_fwd_bnstats(x, xb, weight, out, stats, in_shape, in_stride, w_shape, stride, pad, dil, ntiles):
+@_op("conv2d_fwd_bnstats(Tensor? x, Tensor? xb, Tensor[] weight, Tensor? wpack, Tensor(a!)? out, Tensor(c!)? outb, "
+     "Tensor(b!) stats, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, "
+     "int ntiles) -> ()")
+def _conv2d_fwd_bnstats(x, xb, weight, wpack, out, outb, stats, in_shape, in_stride, w_shape, stride, pad, dil,
+                        ntiles):
     d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_FWD], out.device)
+    wp, wsz = _ws_args(ws[CONV_FWD], stats.device)
     nt = ctypes.c_int(0)
     check(_lib.lib().adaptseg_conv2d_fwd_bnstats_x(
-        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(out), _p(stats), ctypes.c_size_t(stats.numel() * 4),
-        ctypes.byref(nt), wp, wsz, _stream()), "conv2d_fwd_bnstats")
+        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(wpack), _p(out), _p(outb), _p(stats),
+        ctypes.c_size_t(stats.numel() * 4), ctypes.byref(nt), wp, wsz, _stream()), "conv2d_fwd_bnstats")
     if nt.value != ntiles:
         raise RuntimeError(f"conv2d_fwd_bnstats: planned {ntiles} statistics tiles, the launch produced "
                            f"{nt.value} (unaligned operand?)")
 
 
-@_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? res, Tensor? aux, Tensor(a!) dx, "
-     "Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
-def _conv2d_bwd_data(dy, dyb, weight, res, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
+@_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? aux, "
+     "Tensor(a!) dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, "
+     "int flags) -> ()")
+def _conv2d_bwd_data(dy, dyb, weight, wpack, res, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
     n, c, h, w = in_shape
     d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_DATA], dx.device)
     check(_lib.lib().adaptseg_conv2d_bwd_data_x(
-        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(res), _p(aux), _p(dx), _p(dxb), flags, wp, wsz,
-        _stream()),
+        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(wpack), _p(res), _p(aux), _p(dx), _p(dxb), flags, wp,
+        wsz, _stream()),
         "conv2d_bwd_data")
 
 
@@ -212,15 +224,23 @@ def _rc(t):
     return t.numel() // c, c
 
 
+def _fb(t):
+    """(fp32 pointer, bf16 pointer) of an activation operand stored as either."""
+    if t is None:
+        return None, None
+    return (None, _p(t)) if t.dtype == torch.bfloat16 else (_p(t), None)
+
+
 @_op("bn_fwd_train(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
      "Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, "
      "int act) -> ()")
 def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, momentum, eps, act):
+    """x / res: fp32 or bf16 (bf16 activation storage, config c5)."""
     rows, c = _rc(x)
     wp, wsz = _ws_args(bn_ws_bytes(rows, c), x.device)
     check(_lib.lib().adaptseg_bn_fwd_train_x(
-        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(momentum), float(eps),
-        _p(mean), _p(invstd), _p(res), _p(y), _p(yb), int(act), wp, wsz, _stream()), "bn_fwd_train")
+        rows, c, *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(momentum), float(eps),
+        _p(mean), _p(invstd), *_fb(res), _p(y), _p(yb), int(act), wp, wsz, _stream()), "bn_fwd_train")
 
 
 @_op("bn_fwd_train_tiles(Tensor x, Tensor stats, int ntiles, Tensor? weight, Tensor? bias, "
@@ -230,8 +250,8 @@ def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_va
                         momentum, eps, act):
     rows, c = _rc(x)
     check(_lib.lib().adaptseg_bn_fwd_train_tiles_x(
-        rows, c, _p(stats), int(ntiles), _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
-        float(momentum), float(eps), _p(mean), _p(invstd), _p(res), _p(y), _p(yb), int(act), _stream()),
+        rows, c, _p(stats), int(ntiles), *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
+        float(momentum), float(eps), _p(mean), _p(invstd), *_fb(res), _p(y), _p(yb), int(act), _stream()),
         "bn_fwd_train_tiles")
 
 
@@ -240,17 +260,18 @@ def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_va
 def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, act):
     rows, c = _rc(x)
     check(_lib.lib().adaptseg_bn_fwd_infer_x(
-        rows, c, _p(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps), _p(res), _p(y),
+        rows, c, *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps), *_fb(res), _p(y),
         _p(yb), int(act), _stream()), "bn_fwd_infer")
 
 
 @_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
      "Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
 def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
+    """y / x (the saved activations): fp32 or bf16; dy, dx, dres fp32."""
     rows, c = _rc(dy)
     wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)
     check(_lib.lib().adaptseg_bn_bwd_x(
-        rows, c, _p(dy), _p(y), _p(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dxb), _p(dres),
+        rows, c, _p(dy), *_fb(y), *_fb(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dxb), _p(dres),
         int(act), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
 
 

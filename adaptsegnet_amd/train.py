@@ -41,6 +41,7 @@ import torch
 import torch.distributed as dist
 
 from . import functional as F
+from . import kernels as K
 from .optim import SGD, Adam, lr_poly
 
 
@@ -247,8 +248,11 @@ class AdaptSegTrainer:
         if prio == "auto":   # VGG has no BN passes for the side stream to fill: -1.7 % with it
             prio = None if getattr(self.model, "single_output", False) else -1
         dev = next(self.model.parameters()).device
+        # each conv's weight pack is built once per step (the optimisers, the only writers of the
+        # weights, run after the step's last conv): kernels.weight_pack_scope
         if prio is None or dev.type != "cuda":
-            return self._step_body(i_iter, batches)
+            with K.weight_pack_scope():
+                return self._step_body(i_iter, batches)
         batches = list(batches)
         key = (dev.index, prio)
         hp = AdaptSegTrainer._hp_streams.get(key)
@@ -256,7 +260,7 @@ class AdaptSegTrainer:
             hp = AdaptSegTrainer._hp_streams[key] = torch.cuda.Stream(dev, priority=prio)
         cur = torch.cuda.current_stream(dev)
         hp.wait_stream(cur)
-        with torch.cuda.stream(hp):
+        with torch.cuda.stream(hp), K.weight_pack_scope():
             L = self._step_body(i_iter, batches)
         cur.wait_stream(hp)
         return L

@@ -13,7 +13,7 @@ if [ "$SEL" != "none" ]; then
   tail -1 gpurun_out/abl_t.log
 fi
 for rep in 1 2 3; do
-  timeout -k 10 300 ADAPTSEG_LIBRARY=$A python -u bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/abl.json 2>/dev/null || exit 4
+  ADAPTSEG_LIBRARY=$A timeout -k 10 300 python -u bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/abl.json 2>/dev/null || exit 4
   python -c "import json; d=json.loads(open('gpurun_out/abl.json').read().strip().splitlines()[-1]); print('A', round(d['value'],3), round(d['ms_per_step'],2))"
   timeout -k 10 300 python -u bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/abl.json 2>/dev/null || exit 4
   python -c "import json; d=json.loads(open('gpurun_out/abl.json').read().strip().splitlines()[-1]); print('B', round(d['value'],3), round(d['ms_per_step'],2))"

@@ -5,5 +5,5 @@ cd "${GRAFT_REPO_ROOT}" || exit 2
 LIBS=$1; shift
 for L in $LIBS; do
   echo "== $L"
-  timeout -k 10 200 ADAPTSEG_LIBRARY=adaptsegnet_amd/lib/$L python -u tools/conv_bench.py "$@" | grep -E "^op|TOTAL" || exit 4
+  ADAPTSEG_LIBRARY=adaptsegnet_amd/lib/$L timeout -k 10 200 python -u tools/conv_bench.py "$@" | grep -E "^op|TOTAL" || exit 4
 done

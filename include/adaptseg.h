@@ -130,22 +130,43 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
    the GEMM epilogue or split-K reduce beside y / dx (a separate pass on the thin and tap-GEMM
    paths), so that a consumer conv's _x operand needs no conversion pass: the discriminator
    convs (model/discriminator.py:14-27) chain conv -> LeakyReLU -> conv with no BatchNorm
-   between.  Contiguous NHWC like y; 2-byte alignment suffices. */
+   between.  Contiguous NHWC like y; 2-byte alignment suffices.  bf16 activation storage (config
+   c5): the forward forms take y == NULL with y_bf16 given — the conv output is stored in bf16
+   only (fused BN statistics still come from the fp32 accumulators) — on the implicit-GEMM
+   kernels (not the thin / tap-GEMM paths, which return ADAPTSEG_ERR_ARG for it). */
 /* *only = 1 when product `op` of `d` (16-byte aligned operands) runs on a kernel that reads
-   ONLY the operand copies of the _x forms (the LDS-DMA kernels), so the fp32 operand may be
-   NULL and its producer need not write it; 0 otherwise (thin, tap-GEMM, per-element and
-   register-staged kernels read the fp32 operand).  Host-side planning, no GPU.  The same plan
+   ONLY the operand copies of the _x forms (the LDS-DMA kernels; the register-staged bf16
+   forward; a tap-GEMM forward / weight gradient whose inner GEMM is on an LDS-DMA kernel), so
+   the fp32 operand may be NULL and its producer need not write it; 0 otherwise (thin,
+   per-element and register-staged fp32 kernels, the tap-GEMM data gradient read fp32).  Host-side planning, no GPU.  The same plan
    the _x entry points check against. */
 int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *only);
+/* Caller-owned weight packs.  The F32X3 and bf16 kernels read the weights of the forward and
+   data-gradient products as a pack (the exact three-term bf16 split, or bf16 rows, laid out in
+   the kernels' tile order) which the entry points otherwise build per call
+   (optimizer.step in train_gta2cityscapes_multi.py:532-540 is the only writer of the weights:
+   a training step calls each conv's forward 2-3 times and its data gradient 1-3 times on
+   unchanged weights).  adaptseg_conv2d_wpack_size: *bytes = 0 when product `op` of `d` (16-byte
+   aligned operands) reads no pack (fp32-input, thin and tap-GEMM kernels, the weight gradient);
+   adaptseg_conv2d_wpack builds it (same kernel as the per-call pack, same bytes).  The `w_pack`
+   argument of the _x forms takes one (NULL = build per call); it is valid for the weights it
+   was built from until they are written — keeping that promise is the caller's side (the
+   trainer rebuilds every pack once per step, adaptsegnet_amd.kernels.weight_pack_scope).  A
+   plan that ends on a kernel without a pack (misaligned operands) ignores it. */
+int adaptseg_conv2d_wpack_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
+int adaptseg_conv2d_wpack(const adaptseg_conv_desc *d, int op, const float *const *w, void *pack, size_t bytes,
+                          adaptseg_stream_t stream);
 int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
-                          const float *const *w, const float *const *bias, const float *res, float *y,
-                          uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+                          const float *const *w, const void *w_pack, const float *const *bias, const float *res,
+                          float *y, uint16_t *y_bf16, int flags, void *ws, size_t ws_bytes,
+                          adaptseg_stream_t stream);
 int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
-                                  const float *const *w, float *y, float *stats, size_t stats_bytes,
-                                  int *ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+                                  const float *const *w, const void *w_pack, float *y, uint16_t *y_bf16,
+                                  float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                  adaptseg_stream_t stream);
 int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
-                               const float *const *w, const float *res, const float *aux, float *dx,
-                               uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
+                               const float *const *w, const void *w_pack, const float *res, const float *aux,
+                               float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
                                adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
@@ -193,21 +214,24 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                 float *save_invstd, const float *res, float *y, int relu,
                                 adaptseg_stream_t stream);
 
-/* The forward BN passes with an optional bf16 (RNE) copy of y written beside it (y_bf16,
-   contiguous [rows][c], NULL = none): the operand of the next conv under bf16 conv math.
-   y may be NULL when y_bf16 is given (only the copy is written). */
-int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                            float *running_mean, float *running_var, float momentum, float eps,
-                            float *save_mean, float *save_invstd, const float *res, float *y,
-                            uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+/* The forward BN passes with bf16 activation storage (conv math BF16 = config c5, autocast
+   semantics: the convs store bf16, BatchNorm reads bf16 and normalises in fp32).  Activation
+   operands are fp32 (x, res) or bf16 (x_bf16, res_bf16) — exactly one of x / x_bf16, and the
+   residual stored like x.  Outputs: y (fp32) and / or y_bf16 (a bf16 RNE copy, contiguous
+   [rows][c]), at least one. */
+int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                            float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                            float *y, uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes,
+                            adaptseg_stream_t stream);
 int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
-                                  const float *weight, const float *bias, float *running_mean,
-                                  float *running_var, float momentum, float eps, float *save_mean,
-                                  float *save_invstd, const float *res, float *y, uint16_t *y_bf16,
-                                  int relu, adaptseg_stream_t stream);
-int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const float *weight, const float *bias,
-                            const float *running_mean, const float *running_var, float eps,
-                            const float *res, float *y, uint16_t *y_bf16, int relu,
+                                  const uint16_t *x_bf16, const float *weight, const float *bias,
+                                  float *running_mean, float *running_var, float momentum, float eps,
+                                  float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                                  float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream);
+int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, const float *running_mean, const float *running_var, float eps,
+                            const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
                             adaptseg_stream_t stream);
 
 /* Eval-mode BN (running statistics): y = (x-rm)/sqrt(rv+eps)*w + b (+res), ReLU if relu. */
@@ -226,13 +250,14 @@ int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const 
                     const float *save_invstd, float *dx, float *dres, int relu, int train,
                     void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
-/* adaptseg_bn_bwd with an optional bf16 (RNE) copy of dx (dx_bf16, NULL = none): the
-   data-gradient operand of the conv that produced x, under bf16 conv math.  dx may be NULL
-   when dx_bf16 is given. */
-int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const float *x,
-                      const float *weight, const float *bias, const float *save_mean,
-                      const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu,
-                      int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+/* adaptseg_bn_bwd with bf16 activation storage and an optional bf16 (RNE) copy of dx
+   (dx_bf16, NULL = none: the data-gradient operand of the conv that produced x, under bf16
+   conv math; dx may be NULL when dx_bf16 is given).  The saved activations x and y are both
+   fp32 or both bf16 (y_bf16 / x_bf16); the gradients dy, dres stay fp32. */
+int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const uint16_t *y_bf16, const float *x,
+                      const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
+                      const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
+                      void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's
    NaiveConvolution norms, model/custom_layers.py:25-33): additionally dbias[c] += sum(g),

@@ -199,19 +199,55 @@ def _bn(x, P, key, train):
                         P[key + ".bias"], train, BN_MOMENTUM, BN_EPS)
 
 
+class _StoreBF16(torch.autograd.Function):
+    """Round to bf16 (RNE) in the forward, identity in the backward: an activation STORED in
+    bf16 whose gradient stays in full precision (the engine's bf16 activation storage)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.bfloat16).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+_ACT_BF16 = [False]
+
+
+class bf16_activation_storage:
+    """Context manager: inside it, every Bottleneck conv output, BN output and block output is
+    rounded to bf16 as it is stored (torch.autocast(bfloat16)'s storage; the engine's config c5
+    program, engine.bf16_operands).  The stem, the classifiers and the discriminators are
+    unaffected, as in the engine."""
+
+    def __enter__(self):
+        self._prev = _ACT_BF16[0]
+        _ACT_BF16[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _ACT_BF16[0] = self._prev
+
+
+def _st(t):
+    return _StoreBF16.apply(t) if _ACT_BF16[0] else t
+
+
 def _bottleneck(y, P, pre, stride, dil, has_ds, train):
-    """deeplab_multi.py:83-103 — the stride sits on the first 1x1 conv (:64)."""
-    t = F.conv2d(y, P[pre + "conv1.weight"], None, stride)
-    t = F.relu(_bn(t, P, pre + "bn1", train))
-    t = F.conv2d(t, P[pre + "conv2.weight"], None, 1, dil, dil)
-    t = F.relu(_bn(t, P, pre + "bn2", train))
-    t = _bn(F.conv2d(t, P[pre + "conv3.weight"]), P, pre + "bn3", train)
+    """deeplab_multi.py:83-103 — the stride sits on the first 1x1 conv (:64).  _st: bf16
+    storage of each stored activation (identity unless bf16_activation_storage is on)."""
+    t = _st(F.conv2d(y, P[pre + "conv1.weight"], None, stride))
+    t = _st(F.relu(_bn(t, P, pre + "bn1", train)))
+    t = _st(F.conv2d(t, P[pre + "conv2.weight"], None, 1, dil, dil))
+    t = _st(F.relu(_bn(t, P, pre + "bn2", train)))
+    t = _bn(_st(F.conv2d(t, P[pre + "conv3.weight"])), P, pre + "bn3", train)
     if has_ds:
-        sc = _bn(F.conv2d(y, P[pre + "downsample.0.weight"], None, stride), P,
-                 pre + "downsample.1", train)
+        sc = _st(_bn(_st(F.conv2d(y, P[pre + "downsample.0.weight"], None, stride)), P,
+                     pre + "downsample.1", train))
     else:
         sc = y
-    return F.relu(t + sc)
+    return _st(F.relu(t + sc))
 
 
 def _aspp(y, P, pre, rates=ASPP_RATES):

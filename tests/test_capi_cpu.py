@@ -124,11 +124,11 @@ def test_bf16_operand_abi_checks_on_host():
     d = K._desc(K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,)), 4, 64, 128, K.nhwc_strides(4, 64, 128, 256))[0]
     w = _lib.ptr_array([16])
     # F32X3 math: no bf16-operand kernel, so the fp32 input is required
-    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, ctypes.c_void_p(256), w, None, None,
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, ctypes.c_void_p(256), w, None, None, None,
                                  ctypes.c_void_p(512), None, 0, None, 0, None)
     assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
-    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, ctypes.c_void_p(512), None, 0, None, 0,
-                                 None)
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, None, ctypes.c_void_p(512), None, 0, None,
+                                 0, None)
     assert st == 1
     K.set_conv_math(K.MATH_BF16)
     try:

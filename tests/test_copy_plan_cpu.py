@@ -74,8 +74,9 @@ def test_skip_decisions_match_across_geometries_but_the_kernel_variants_do_not()
 
 def test_copy_operand_only_matches_the_lds_dma_selectors():
     """adaptseg_conv2d_copy_operand_only (what engine.bf16_only asks) is exactly the set of
-    products the planner puts on the LDS-DMA kernels (selectors 100*op + 94 / 97-99, 192 / 193),
-    for every conv geometry of the c5 step; and it is never true under the fp32 conv maths."""
+    products the planner puts on the LDS-DMA kernels (selectors 100*op + 94 / 97-99, 192 / 193)
+    or the register-staged bf16 forward (90-93), for every conv geometry of the c5 step; and it
+    is never true under the fp32 conv maths."""
     import bench
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
@@ -100,8 +101,12 @@ def test_copy_operand_only_matches_the_lds_dma_selectors():
         for g, n, h, w, op, st in geoms:
             kid, _ = K.conv_kernel_id(g, n, h, w, op, st)
             lds_dma = kid % 100 in (94, 97, 98, 99) or (op == 1 and kid % 100 in (92, 93))
-            if g.cout <= 32:   # tap-GEMM (ASPP heads) / thin paths: the selector is the inner GEMM's,
-                lds_dma = False   # but the entry point itself reads the fp32 operand
+            # the register-staged bf16 forward (90-93) reads the contiguous bf16 copy too
+            lds_dma = lds_dma or (op == 0 and kid % 100 in (90, 91, 92, 93))
+            if g.cout <= 32:   # tap-GEMM (ASPP heads): the selector is the inner GEMM's, whose
+                # forward / weight gradient read x's copy; its data gradient's tap scatter and
+                # the thin (Cout 1) discriminator head read fp32
+                lds_dma = lds_dma and op != 1 and len(g.pads) > 1
             assert K.conv_copy_operand_only(g, n, h, w, op, st) == lds_dma, (g, n, h, w, op, kid)
             seen.add(lds_dma)
         assert seen == {True, False}
@@ -127,20 +132,46 @@ def test_null_fp32_operand_with_misaligned_weight_is_rejected_on_host(op):
         assert K.conv_copy_operand_only(g, 4, 64, 128, op)
         aligned, misaligned = ctypes.c_void_p(4096), _lib.ptr_array([4096 + 4])
         if op == 0:
-            st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, aligned, misaligned, None, None,
+            st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, aligned, misaligned, None, None, None,
                                          ctypes.c_void_p(8192), None, 0, None, 0, None)
             assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
             nt = ctypes.c_int(0)
-            st = L.adaptseg_conv2d_fwd_bnstats_x(ctypes.byref(d), None, aligned, misaligned, ctypes.c_void_p(8192),
+            st = L.adaptseg_conv2d_fwd_bnstats_x(ctypes.byref(d), None, aligned, misaligned, None, ctypes.c_void_p(8192), None,
                                                  ctypes.c_void_p(16384), 1 << 20, ctypes.byref(nt), None, 0, None)
             assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
         elif op == 1:
-            st = L.adaptseg_conv2d_bwd_data_x(ctypes.byref(d), None, aligned, misaligned, None, None,
+            st = L.adaptseg_conv2d_bwd_data_x(ctypes.byref(d), None, aligned, misaligned, None, None, None,
                                               ctypes.c_void_p(8192), None, 0, None, 0, None)
             assert st == 1 and b"fp32 dY" in L.adaptseg_last_error()
         else:   # weight gradient: fp32 x present but misaligned, dY only as a copy
             st = L.adaptseg_conv2d_bwd_weight_x(ctypes.byref(d), None, aligned, ctypes.c_void_p(4096 + 4), aligned,
                                                 _lib.ptr_array([8192]), None, 0, None, 0, None)
             assert st == 1 and b"fp32 operands" in L.adaptseg_last_error()
+    finally:
+        K.set_conv_math(prev)
+
+
+def test_weight_pack_sizes_follow_the_plan():
+    """adaptseg_conv2d_wpack_size: the F32X3 forward / data-gradient products read a three-term
+    pack (6 B per weight, rows padded to 128-wide tiles), the bf16 ones a bf16 pack (2 B), the
+    weight gradients, thin (Cout <= 4) and tap-GEMM (ASPP) products none."""
+    from adaptsegnet_amd import kernels as K
+
+    def size(g, op, n=2, h=32, w=48):
+        d = K._desc(g, n, h, w, K.nhwc_strides(n, h, w, g.cin))[0]
+        b = ctypes.c_size_t(0)
+        assert _lib.lib().adaptseg_conv2d_wpack_size(ctypes.byref(d), op, ctypes.byref(b)) == 0
+        return b.value
+
+    g = K.ConvGeom(256, 512, 3, 3, 1, (2,), (2,))
+    assert size(g, 0) == 3 * 512 * 9 * 256 * 2 and size(g, 1) == 3 * 256 * 9 * 512 * 2 and size(g, 2) == 0
+    assert size(K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,)), 0) == 0                          # thin
+    assert size(K.ConvGeom(2048, 19, 3, 3, 1, (6, 12, 18, 24), (6, 12, 18, 24)), 0) == 0  # tap-GEMM
+    prev = K.get_conv_math()
+    try:
+        K.set_conv_math(K.MATH_BF16)
+        assert size(g, 0) == 512 * 9 * 256 * 2 and size(g, 1) == 256 * 9 * 512 * 2
+        K.set_conv_math(K.MATH_F32)
+        assert size(g, 0) == 0
     finally:
         K.set_conv_math(prev)

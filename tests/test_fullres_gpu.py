@@ -89,9 +89,11 @@ def bf16_math():
 @pytest.mark.parametrize("bn_train", [True, False], ids=["trainBN", "evalBN"])
 def test_fullres_c5_bf16_step_vs_oracle(bf16_math, bn_train):
     """BASELINE config c5's program (multi-level LS-GAN, bf16 conv math, train:578-679) at its own
-    geometry — source 1280x720, target 1024x512, batch 1 — against the fp32 oracle: the bf16
-    LDS-DMA kernels on the producer-written operand copies, with the fp32 activations that only
-    those kernels read never written (engine.bf16_only), run unsplit at this size.  Losses within
+    geometry — source 1280x720, target 1024x512, batch 1 — against the fp32 oracle with bf16
+    activation storage (every Bottleneck conv / BN / block output rounded to bf16 as stored,
+    R.bf16_activation_storage; the engine's torch.autocast-style storage): the bf16 LDS-DMA
+    kernels on bf16 activations, with the fp32 tensors that only those kernels read never
+    written (engine.bf16_only), run unsplit at this size.  Losses within
     2e-2 relative (bf16 operand rounding, ~2^-9 per operand through ~100 layers); eval BN: every
     update cosine >= 0.99.  Train BN: the trunk update is not comparable with the fp32 oracle's
     at all — the reference's OWN arithmetic with bf16 conv operands moves it to cosine -0.002
@@ -99,7 +101,8 @@ def test_fullres_c5_bf16_step_vs_oracle(bf16_math, bn_train):
     random-init train-BN trunk gradient is chaotic under bf16 rounding, the losses and heads are
     not), so the train-BN check is the losses, the heads' update (>= 0.97; the emulation: 0.9998)
     and the discriminators' (>= 0.85: Adam's first step is nearly sign(g); the emulation 0.92)."""
-    _step_vs_oracle("c3", bn_train, "LS", 2e-2, trunk=not bn_train, d_bound=0.85 if bn_train else None)
+    _step_vs_oracle("c3", bn_train, "LS", 2e-2, trunk=not bn_train, d_bound=0.85 if bn_train else None,
+                    act_bf16=True)
 
 
 def test_fullres_c5_bf16_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monkeypatch):
@@ -155,7 +158,9 @@ def test_c1_forward_crossentropy2d_vs_oracle():
         assert abs(loss - l_ref) <= 1e-3 * abs(l_ref)
 
 
-def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None):
+def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16=False):
+    """act_bf16: the oracle stores the Bottleneck activations in bf16 as the engine's bf16
+    program does (R.bf16_activation_storage)."""
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     level, src, tgt = GEOMS[geom]
     xs, lab, xt = _batch(src, tgt)
@@ -165,7 +170,11 @@ def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None):
     D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=torch.float32, trainable=lambda k: True)
     D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
     opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
-    ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
+    if act_bf16:
+        with R.bf16_activation_storage():
+            ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
+    else:
+        ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
     # HIP engine
     tr, m, d1, d2 = _hip_trainer(level, src, tgt, bn_train, gan=gan)
     got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()

@@ -308,3 +308,54 @@ def test_iter_size_two_accumulates_sub_batches(data, level, gan):
         f, _ = frob(_updates(None, keys, g0, sd), dref)
         f32, _ = frob(_updates(G32, keys, g0), dref)
         assert f <= 2 * f32 + 1e-4, (gname, f, f32)
+
+
+@pytest.mark.parametrize("math", ["f32x3", "bf16"])
+def test_weight_packs_are_built_once_per_step_and_bitwise_neutral(data, math, monkeypatch):
+    """kernels.weight_pack_scope (AdaptSegTrainer.step): each conv's F32X3 / bf16 weight pack is
+    built ONCE per step and reused by every forward / data-gradient call on those weights
+    (adaptseg_conv2d_wpack + the _x forms' w_pack).  Two multi-level steps with the cache and
+    with per-call packs give bitwise the same losses and parameters; every pack is rebuilt in
+    the next step (the optimiser wrote the weights), exactly once."""
+    from adaptsegnet_amd import kernels as K
+    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32X3)
+    try:
+        cfg = dict(level="multi-level", gan="LS", input_size=(57, 41), input_size_target=(49, 33))
+        builds0 = K.pack_builds()
+        m_a, d1_a, d2_a, got_a = _run_hip("multi-level", "LS", cfg, data, 1, bn_train=True)
+        per_step = K.pack_builds() - builds0
+        assert per_step > 0
+        from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+        tr = AdaptSegTrainer(m_a, d1_a, d2_a, StepConfig(**cfg))
+        xs, lab, xt = data
+        b = [(xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))]
+        got_a.append(tr.step(1, b).values())
+        assert K.pack_builds() - builds0 == 2 * per_step   # once per step, not per call
+        monkeypatch.setattr(K, "_wpack", lambda *a, **kw: None)   # per-call packs
+        m_b, d1_b, d2_b, got_b = _run_hip("multi-level", "LS", cfg, data, 1, bn_train=True)
+        tr = AdaptSegTrainer(m_b, d1_b, d2_b, StepConfig(**cfg))
+        got_b.append(tr.step(1, b).values())
+        assert got_a == got_b, (got_a, got_b)
+        for ma, mb in ((m_a, m_b), (d1_a, d1_b), (d2_a, d2_b)):
+            for (ka, va), (kb, vb) in zip(ma.state_dict().items(), mb.state_dict().items()):
+                assert ka == kb and torch.equal(va, vb), ka
+    finally:
+        K.set_conv_math(K.MATH_F32X3)
+
+
+def test_weight_write_between_scopes_invalidates_the_packs(data):
+    """A weight write the trainer does not see (through .data, which bypasses autograd's
+    version counter) between two pack scopes is picked up: the second scope rebuilds every
+    pack, so its forward equals a forward with per-call packs on the new weights, bitwise."""
+    from adaptsegnet_amd import kernels as K
+    xs = data[0].float().to(DEV)
+    m = build_g().eval()
+    with torch.no_grad(), K.weight_pack_scope():
+        m(xs, (57, 41))
+        for p in m.parameters():
+            p.data.mul_(0.5)
+    with torch.no_grad(), K.weight_pack_scope():
+        got = m(xs, (57, 41))[1].clone()
+    with torch.no_grad():
+        ref = m(xs, (57, 41))[1]
+    assert torch.equal(got, ref)

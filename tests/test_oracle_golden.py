@@ -153,3 +153,24 @@ def test_reference_trajectory_fixture_and_oracle_iteration0():
     got = R.oracle_step(G, None, D2, opts, cfg, 0, [(xs, lab, xt)])
     for j, k in enumerate(["loss_seg2", "loss_adv_target2", "loss_D2"]):
         assert abs(got[k] - tr[0, j]) <= 1e-5 * abs(tr[0, j]), (k, got[k], tr[0, j])
+
+
+def test_bf16_activation_storage_rounds_block_outputs_and_passes_gradients_straight():
+    """R.bf16_activation_storage (the oracle side of config c5's bf16 activation storage): inside
+    it every Bottleneck output is exactly bf16-representable, the rounding is a straight-through
+    identity in the backward, and outside it the oracle is unchanged."""
+    P = R.to_torch(R.det_state(R.g_specs(), 7), dtype=torch.float64)
+    y = torch.randn(1, 256, 9, 11, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+    y = y.to(torch.bfloat16).double().requires_grad_()   # block inputs are stored bf16 as well
+    plain = R._bottleneck(y, P, "layer1.1.", 1, 1, False, False)
+    with R.bf16_activation_storage():
+        out = R._bottleneck(y, P, "layer1.1.", 1, 1, False, False)
+        assert R._ACT_BF16[0]
+    assert not R._ACT_BF16[0]
+    assert torch.equal(out, out.to(torch.bfloat16).double())
+    assert not torch.equal(plain, plain.to(torch.bfloat16).double())
+    rel = float((out - plain).abs().max() / plain.abs().max())
+    assert 0 < rel < 2e-2, rel
+    g = torch.randn_like(out)
+    (gi,) = torch.autograd.grad(R._StoreBF16.apply(out), out, g)
+    assert torch.equal(gi, g)
