@@ -541,8 +541,13 @@ int kernel_id(const Plan &pl, int mode) {
 
 // Split-K outputs: the operands of the final sum are 16-byte aligned float4 rows (the folded
 // epilogue and splitk_reduce4_kernel both need that; else the scalar splitk_reduce_kernel).
+// ADAPTSEG_SPLITK_FOLD=1 builds the in-kernel fold (splitk_fold, conv_kernels.hpp): the last
+// split to arrive at a tile sums every slab of it.  Measured and rejected (same box, two
+// alternating runs each, profiles/r3/splitk_fold_ab.txt): c2 25.86 vs 26.66 images/s, c5 35.70
+// vs 38.56 — a 128x128 fp32 slab is 64 KB, so one reducer block reads splits x 64 KB (0.6-1 MB)
+// serially at the tail of the launch, where the separate reduce spreads it over the chip.
 #ifndef ADAPTSEG_SPLITK_FOLD
-#define ADAPTSEG_SPLITK_FOLD 1
+#define ADAPTSEG_SPLITK_FOLD 0
 #endif
 
 static bool splitk_vec(const ConvParams &q, const float *slab, const float *final_out, int mode) {

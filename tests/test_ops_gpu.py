@@ -701,11 +701,12 @@ def test_to_nhwc_pad():
 
 @pytest.mark.parametrize("case", [(4, 64, 64, 96, 64, 1), (2, 256, 48, 64, 256, 3)], ids=["1x1-192split", "3x3-l3"])
 def test_folded_splitk_weight_gradient_is_deterministic(case, conv_math):
-    """Split-K weight gradients fold their slab sum into the split that arrives last at each
-    output tile (conv_kernels.hpp splitk_fold: write-through slabs, release / acquire around a
-    per-tile counter).  The sum runs in split order whatever the arrival order, so repeated
-    launches — with the other stream's kernels shuffling the arrival order — are bitwise equal,
-    and match fp64 at the parity tolerance (with accumulate into an existing gradient)."""
+    """Split-K weight gradients sum their slabs in split order whatever order the splits
+    arrive in (the default separate splitk_reduce4 launch, and the ADAPTSEG_SPLITK_FOLD=1
+    experiment build's in-kernel fold: write-through slabs, release / acquire around a per-tile
+    counter), so repeated launches — with the other stream's kernels shuffling the arrival
+    order — are bitwise equal, and match fp64 at the parity tolerance (with accumulate into an
+    existing gradient)."""
     k = K()
     n, cin, h, w, cout, ks = case
     geom = k.ConvGeom(cin, cout, ks, ks, 1, ((ks // 2) * 2,), (2,))
