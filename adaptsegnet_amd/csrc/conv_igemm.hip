@@ -326,15 +326,22 @@ size_t splitk_slab_bytes(const Plan &pl) {
   return ((size_t)pl.p.splits * pl.p.M * pl.p.N * sizeof(float) + 255) / 256 * 256;
 }
 
+// Row tile of the plan's kernel (the fused BN statistics count one partial per row tile).
+int plan_bm(const Plan &pl) {
+  if (pl.g16) return pl.g16_bm;
+  if (pl.x3r) return pl.mode == MODE_WGRAD ? pl.x3r_bm : 256;
+  return (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
+}
+
 // Grid decomposition: tiles, then split K until the grid has ~2 blocks per CU while keeping
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.x3g = pl.g16 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.x3g = pl.x3r = pl.g16 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
-  const int bm = pl.g16 ? pl.g16_bm : (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
+  const int bm = plan_bm(pl);
   const int bn = pl.g16 ? pl.g16_bn : pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
-  pl.bk = pl.g16 ? pl.g16_bk : pl.bf16 ? 64 : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
+  pl.bk = pl.g16 ? pl.g16_bk : pl.bf16 ? 64 : pl.x3r ? kX3rBK : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
     p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
@@ -366,14 +373,14 @@ void set_splits(Plan &pl) {
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
   constexpr int kG16WgradTarget = 256;
-  const int target = (pl.mode == MODE_WGRAD && pl.x3)    ? kX3WgradTarget
-                     : (pl.mode == MODE_WGRAD && pl.g16) ? kG16WgradTarget
-                                                         : kSplitTarget;
-  // the LDS-DMA bf16 kernel runs one block per CU: split only grids under half the CUs
-  const int split_below = pl.mode == MODE_WGRAD ? target : pl.g16 ? 128 : 257;
+  const int target = (pl.mode == MODE_WGRAD && (pl.g16 || pl.x3r)) ? kG16WgradTarget
+                     : (pl.mode == MODE_WGRAD && pl.x3)            ? kX3WgradTarget
+                                                                   : kSplitTarget;
+  // the LDS-DMA bf16 / x3r kernels run one block per CU: split only grids under half the CUs
+  const int split_below = pl.mode == MODE_WGRAD ? target : pl.x3r ? 256 : pl.g16 ? 128 : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, (pl.g16 && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
+    splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -476,7 +483,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.bf16 = true;
   }
   // F32X3 conv math: the vector FAST cases whose 16-deep K tiles stay inside one tap
-  pl.x3 = pl.x3g = false;
+  pl.x3 = pl.x3g = pl.x3r = false;
+  pl.x3r_bm = 256;
   const bool x3_math = conv_math() == ADAPTSEG_MATH_F32X3 || conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT;
   if (x3_math && pl.fast && !pl.ae && !pl.be) {
     if (op == ADAPTSEG_CONV_FWD) pl.x3 = d->c % kX3BK == 0;
@@ -484,8 +492,14 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.x3 = true;
     // pre-split operand images by LDS-DMA (conv_x3g.hpp): 16-B chunks of both weight-gradient
     // operands (Cin, Cout multiples of 8); every F32X3 forward / data gradient qualifies
-    if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT)
+    if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) {
       pl.x3g = op != ADAPTSEG_CONV_BWD_WEIGHT || (d->c % 8 == 0 && d->k % 8 == 0);
+      // 256x128 tiles with 32-deep steps (conv_x3r.hpp): a 32-deep step inside one tap
+      if (op == ADAPTSEG_CONV_FWD) pl.x3r = d->c % kX3rBK == 0;
+      else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3r = d->k % kX3rBK == 0;
+      else pl.x3r = pl.x3g;
+      if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = d->k >= 256 ? 256 : 128;
+    }
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
@@ -528,6 +542,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 }
 
 int kernel_id(const Plan &pl, int mode) {
+  // 88 / 89: the FAST cfg-8 stride-2 ids, which never occur (cfg 8 has no stride-2 form)
+  if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
   if (pl.x3g) return 100 * mode + 86 + (pl.s2 ? 1 : 0);
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
@@ -855,7 +871,7 @@ int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
   if (st) return st;
   if (tapgemm_eligible(d)) return ADAPTSEG_OK;
   if (pl.fast && pl.p.splits == 1)
-    *ntiles = (int)ceil_div(pl.p.M, pl.g16 ? pl.g16_bm : pl.bf16 ? 128 : kCfgBM[pl.cfg]);
+    *ntiles = (int)ceil_div(pl.p.M, plan_bm(pl));
   return ADAPTSEG_OK;
 }
 
@@ -897,7 +913,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   p.outb = reinterpret_cast<__bf16 *>(y_bf16);
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
-    const int nt = (int)ceil_div(p.M, pl.g16 ? pl.g16_bm : kCfgBM[pl.cfg]);
+    const int nt = (int)ceil_div(p.M, plan_bm(pl));
     if ((size_t)(nt + 2 * (int64_t)p.N * nt) * sizeof(float) <= stats_bytes) {
       p.stats = stats;
       p.stats_ntiles = nt;

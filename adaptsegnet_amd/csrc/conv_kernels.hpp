@@ -32,6 +32,7 @@ enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int kMaxTaps = 64;
 constexpr int BK = 16;
 constexpr int kX3BK = 16;
+constexpr int kX3rBK = 32;   // K step of the 256x128 F32X3 kernels (conv_x3r.hpp)
 // F32X3 kernel block: 128x128 tiles; 4 waves of 64x64 for the weight gradient, 8 waves of 64x32
 // for the K-contiguous products (FWD / DGRAD)
 constexpr int x3_bn(int mode) { return 128; }
@@ -1318,6 +1319,8 @@ struct Plan {
   bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
   bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
   bool x3g;    // ... on pre-split operand images by LDS-DMA (conv_x3g.hpp), MATH_F32X3_PRESPLIT
+  bool x3r;    // ... the 256x128x32 one-block-per-CU form of x3g (conv_x3r.hpp); x3g is set too
+  int x3r_bm;  // its row tile (256; weight gradients with Cout < 256: 128)
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
   int g16_bm, g16_bn, g16_bk;
@@ -1375,6 +1378,7 @@ hipError_t prep_bf16_wpack(const Plan &pl, void *pack, hipStream_t s);   // the 
 hipError_t launch_bf16(const Plan &pl, void *ws, hipStream_t s);
 // F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)
 size_t x3_wpack_bytes(const Plan &pl);
+int plan_bm(const Plan &pl);
 size_t x3_pre_bytes(const Plan &pl);   // workspace ahead of the slabs: weight pack + x3g term images
 hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s);    // the weight pack (unless wpack_ext) + copies
 hipError_t prep_x3_wpack(const Plan &pl, void *pack, hipStream_t s);  // the weight pack alone

@@ -1,6 +1,6 @@
 // Kernel instantiations and host launcher of the F32X3 conv math (conv_x3.hpp, conv_x3g.hpp):
 // fp32 convs on the bf16 MFMA through exact three-term bf16 splits.
-#include "conv_x3g.hpp"
+#include "conv_x3r.hpp"
 
 namespace adaptseg {
 
@@ -88,6 +88,19 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(x3_wpack_bytes(pl));
     const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext) : reinterpret_cast<const __bf16 *>(base);
     const uint32_t img = (uint32_t)x3g_act_elems(pl);
+    if (pl.x3r) {
+      if (pl.mode == MODE_FWD) igemm_x3r_kernel<MODE_FWD, false><<<grid, 512, 0, s>>>(p, act, img, wb);
+      else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3r_kernel<MODE_DGRAD, true><<<grid, 512, 0, s>>>(p, act, img, wb);
+      else if (pl.mode == MODE_DGRAD) igemm_x3r_kernel<MODE_DGRAD, false><<<grid, 512, 0, s>>>(p, act, img, wb);
+      else {
+        const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
+                                         : reinterpret_cast<const __bf16 *>(base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)));
+        const uint32_t img2 = (uint32_t)x3g_act2_elems(pl);
+        if (pl.x3r_bm == 256) igemm_x3r_wgrad_kernel<256><<<grid, 512, 0, s>>>(p, act, img, act2, img2);
+        else igemm_x3r_wgrad_kernel<128><<<grid, 512, 0, s>>>(p, act, img, act2, img2);
+      }
+      return hipGetLastError();
+    }
     if (pl.mode == MODE_FWD) igemm_x3g_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, act, img, wb);
     else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3g_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, act, img, wb);
     else if (pl.mode == MODE_DGRAD) igemm_x3g_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, act, img, wb);

@@ -30,7 +30,9 @@ def test_default_conv_math_selects_f32x3():
     """The library's default conv math is F32X3: the vector products of the step run on the
     split-bf16 kernel (selector 100*op + 95, +1 for the stride-2 parity path); thin and
     per-element products keep their fp32 kernels.  F32X3_PRESPLIT moves the products whose
-    operands come in 16-B chunks to the LDS-DMA kernel on pre-split images (100*op + 86 / 87);
+    operands come in 16-B chunks to the LDS-DMA kernels on pre-split images: 256x128x32 tiles
+    (conv_x3r.hpp, 100*op + 88, + 89 for the stride-2 parity path / 128-row weight gradients)
+    where a 32-deep step stays inside one tap, else 128x128x16 (conv_x3g.hpp, 100*op + 86 / 87);
     the stem's channel-padded weight gradient (Cin 4) stays on the staged one."""
     from adaptsegnet_amd import kernels as K
     assert K.get_conv_math() == K.MATH_F32X3
@@ -45,8 +47,12 @@ def test_default_conv_math_selects_f32x3():
     stem4 = K.ConvGeom(4, 64, 7, 7, 2, (3,), (1,))
     K.set_conv_math(K.MATH_F32X3_PRESPLIT)
     try:
-        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [86, 186, 286]
-        assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 187
+        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [88, 188, 288]
+        assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 189
+        g128 = K.ConvGeom(64, 128, 3, 3, 1, (1,), (1,))
+        assert K.conv_kernel_id(g128, 4, 64, 128, 2)[0] == 289   # Cout < 256: 128-row tiles
+        g16 = K.ConvGeom(48, 64, 3, 3, 1, (1,), (1,))
+        assert [K.conv_kernel_id(g16, 4, 64, 128, op)[0] for op in (0, 1)] == [86, 188]
         assert K.conv_kernel_id(stem4, 4, 512, 1024, 2, (4 * 512 * 1024, 1, 4 * 1024, 4))[0] == 295
     finally:
         K.set_conv_math(K.MATH_F32X3)
