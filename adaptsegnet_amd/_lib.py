@@ -57,6 +57,7 @@ _SIGS = {
     "adaptseg_version": [],
     "adaptseg_conv2d_workspace_size": [_DESC, _I, ctypes.POINTER(_SZ)],
     "adaptseg_conv2d_kernel_id": [_DESC, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
+    "adaptseg_conv2d_kernel_id_x": [_DESC, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
     "adaptseg_conv2d_copy_operand_only": [_DESC, _I, ctypes.POINTER(_I)],
     "adaptseg_conv2d_fwd": [_DESC, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data": [_DESC, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
@@ -80,6 +81,7 @@ _SIGS = {
     "adaptseg_bn_fwd_train_tiles": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _I, _P],
     "adaptseg_conv2d_bnstats_size": [_DESC, ctypes.POINTER(ctypes.c_size_t)],
     "adaptseg_conv2d_bnstats_tiles": [_DESC, ctypes.POINTER(_I)],
+    "adaptseg_conv2d_bnstats_tiles_x": [_DESC, _I, ctypes.POINTER(_I)],
     "adaptseg_conv2d_fwd_bnstats": [_DESC, _P, _PP, _P, _P, _SZ, ctypes.POINTER(ctypes.c_int), _P, _SZ, _P],
     "adaptseg_bn_fwd_infer": [_L, _I, _P, _P, _P, _P, _P, _F, _P, _P, _I, _P],
     "adaptseg_bn_bwd": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],

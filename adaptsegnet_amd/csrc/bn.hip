@@ -11,6 +11,7 @@
 #include "common.hpp"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace adaptseg {
 
@@ -58,6 +59,22 @@ __device__ __forceinline__ float4 lda4(const __bf16 *p) {
 __device__ __forceinline__ float lda1(const float *p) { return *p; }
 __device__ __forceinline__ float lda1(const __bf16 *p) { return (float)*p; }
 
+// Under the F32X3 conv maths the operand copies are three exact bf16 term images [3][rows][C]
+// (common.hpp split3), `timg` elements apart: the residual and the saved output (the ReLU mask
+// source) of a BN may then be stored as terms only, read back exactly (join3).  X3 tags that
+// storage; its pointer is term 0.
+struct X3 {};
+template <typename T> struct Act { typedef const T *ptr; };
+template <> struct Act<X3> { typedef const __bf16 *ptr; };
+template <typename T>
+__device__ __forceinline__ float4 ldr4(typename Act<T>::ptr p, int64_t e, int64_t timg) {
+  if constexpr (std::is_same<T, X3>::value)
+    return join3(*reinterpret_cast<const uint2 *>(p + e), *reinterpret_cast<const uint2 *>(p + e + timg),
+                 *reinterpret_cast<const uint2 *>(p + e + 2 * timg));
+  else
+    return lda4(p + e);
+}
+
 constexpr int kReduceUnroll = 4;
 // ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
 // GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
@@ -72,12 +89,12 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
 
 // Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
 // Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
-template <int MODE, typename TX>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
+template <int MODE, typename TX, typename TY = TX>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
 __global__ void __launch_bounds__(256)
 bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
-                 const TX *__restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
+                 typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
-                 int64_t rows_per_split, float *__restrict__ partial) {
+                 int64_t rows_per_split, float *__restrict__ partial, int64_t timg = 0) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc;   // channel quad within block
   const int rl = threadIdx.x / tc;   // row lane
@@ -109,7 +126,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const fl
         v[u] = lda4(x + e);
         if (MODE == 1) {
           g[u] = *reinterpret_cast<const float4 *>(dy + e);
-          if (relu == 1 || relu == 3) o[u] = lda4(y + e);
+          if (relu == 1 || relu == 3) o[u] = ldr4<TY>(y, e, timg);
         }
       }
 #pragma unroll
@@ -264,11 +281,26 @@ __device__ __forceinline__ uint2 bf16x4_rne(float4 v) {
   return __builtin_bit_cast(uint2, __builtin_convertvector(f, b4v));
 }
 
-template <typename TX>
+// The operand copy of four outputs at uint2 index k: one bf16 RNE image (img4 == 0, BF16 maths)
+// or the three exact term images, img4 uint2 apart (F32X3 maths)
+__device__ __forceinline__ void store_copy(uint2 *yb, int64_t k, float4 o, int64_t img4) {
+  if (img4) {
+    uint2 h, m, l;
+    split3(o, h, m, l);
+    yb[k] = h;
+    yb[k + img4] = m;
+    yb[k + 2 * img4] = l;
+  } else {
+    yb[k] = bf16x4_rne(o);
+  }
+}
+
+template <typename TX, typename TR = TX>
 __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restrict__ x,
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
-                                      const TX *__restrict__ res, float *__restrict__ y, uint2 *yb, int relu) {
+                                      typename Act<TR>::ptr __restrict__ res, float *__restrict__ y, uint2 *yb, int relu,
+                                      int64_t timg = 0, int64_t yimg4 = 0) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
@@ -276,7 +308,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
     float o[4] = {v.x, v.y, v.z, v.w};
     float r4[4] = {0, 0, 0, 0};
     if (res) {
-      float4 r = lda4(res + 4 * i);
+      float4 r = ldr4<TR>(res, 4 * i, timg);
       r4[0] = r.x; r4[1] = r.y; r4[2] = r.z; r4[3] = r.w;
     }
 #pragma unroll
@@ -286,7 +318,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
       o[j] = fwd_act(t, relu);
     }
     if (y) reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
-    if (yb) yb[i] = bf16x4_rne(make_float4(o[0], o[1], o[2], o[3]));
+    if (yb) store_copy(yb, i, make_float4(o[0], o[1], o[2], o[3]), yimg4);
   }
 }
 
@@ -300,11 +332,11 @@ constexpr int kApplyUnroll = 4;
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
-template <typename TX>
+template <typename TX, typename TR = TX>
 __global__ void __launch_bounds__(256)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
-                  const TX *res, float *y, uint2 *yb, int act) {
+                  typename Act<TR>::ptr res, float *y, uint2 *yb, int act, int64_t timg = 0, int64_t yimg4 = 0) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -321,7 +353,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
       const bool ok = ru < r1;
       const int64_t e = (ok ? ru : r) * C + c0;
       v[u] = lda4(x + e);
-      q[u] = res ? lda4(res + e) : make_float4(0, 0, 0, 0);
+      q[u] = res ? ldr4<TR>(res, e, timg) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -333,17 +365,18 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
       o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
       o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
       if (y) st4(y + ru * C + c0, o);
-      if (yb) yb[(ru * C + c0) >> 2] = bf16x4_rne(o);
+      if (yb) store_copy(yb, (ru * C + c0) >> 2, o, yimg4);
     }
   }
 }
 
-template <typename TX>
+template <typename TX, typename TY = TX>
 __global__ void __launch_bounds__(256)
-bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, const TX *y, const TX *x,
-                      const float *__restrict__ w, const float *__restrict__ b, const float *__restrict__ mean,
-                      const float *__restrict__ invstd, const float *__restrict__ coef, float *dx, uint2 *dxb,
-                      float *dres, int rmode, int train) {
+bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, typename Act<TY>::ptr y,
+                      const TX *x, const float *__restrict__ w, const float *__restrict__ b,
+                      const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,
+                      float *dx, uint2 *dxb, float *dres, int rmode, int train, int64_t timg = 0,
+                      int64_t dimg4 = 0) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -364,7 +397,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
       const int64_t e = (ru < r1 ? ru : r) * C + c0;
       g[u] = ld4c(dy + e);
       v[u] = train ? lda4(x + e) : z4;
-      o4[u] = need_y ? lda4(y + e) : z4;
+      o4[u] = need_y ? ldr4<TY>(y, e, timg) : z4;
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -399,7 +432,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
         out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
       }
       if (dx) st4(dx + e, out);
-      if (dxb) dxb[e >> 2] = bf16x4_rne(out);
+      if (dxb) store_copy(dxb, e >> 2, out, dimg4);
     }
   }
 }
@@ -461,14 +494,17 @@ static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(tot
 
 namespace adaptseg {
 
-template <typename TX>
-int bn_bwd_launch(int64_t rows, int c, const float *dy, const TX *y, const TX *x, const float *weight,
+template <typename TX, typename TY = TX>
+int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
                          const float *bias, const float *save_mean, const float *save_invstd, float *dx,
                          uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
                          size_t ws_bytes, hipStream_t s) {
   float *coef = nullptr;
   int slot;
-  const double eb = sizeof(TX);   // bytes per activation element (x, y)
+  const double eb = sizeof(TX);   // bytes per activation element (x)
+  const bool terms = std::is_same<TY, X3>::value;   // y stored as F32X3 term images
+  const double ebt = terms ? 6.0 : eb;               // ... bytes per element of y
+  const int64_t timg = rows * c, dimg4 = copies_are_terms() && dx_bf16 ? rows * c / 4 : 0;
   if (train) {
     size_t need = bn_ws_bytes(rows, c);
     if (!ws || ws_bytes < need) {
@@ -479,9 +515,10 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, const TX *y, const TX *x
     float *partial = reinterpret_cast<float *>(ws);
     coef = partial + (size_t)r.splits * 2 * c;
     // dy, x (+ y for the mask from y) in
-    timing_begin(kTBnReduceBwd, s, (4.0 + eb * (1 + ((rmode == 1 || rmode == 3) ? 1 : 0))) * rows * c, &slot);
-    bn_reduce_kernel<1, TX><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean, save_invstd,
-                                                                     weight, bias, rmode, r.per, partial);
+    timing_begin(kTBnReduceBwd, s, (4.0 + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c, &slot);
+    bn_reduce_kernel<1, TX, TY><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
+                                                                         save_invstd, weight, bias, rmode, r.per,
+                                                                         partial, timg);
     timing_end(slot, s);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
@@ -490,15 +527,14 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, const TX *y, const TX *x
   }
   // dy, x (train), y (mask from y) in; dx, dres out
   timing_begin(kTBnBwdApply, s,
-               (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * ((train ? 1 : 0) + ((rmode == 1 || rmode == 3) ? 1 : 0))) *
-                       rows * c +
-                   (dx_bf16 ? 2.0 * rows * c : 0.0),
+               (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * (train ? 1 : 0) +
+                ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
+                   (dx_bf16 ? (dimg4 ? 6.0 : 2.0) * rows * c : 0.0),
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);
-  bn_bwd_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, dy, y, x, weight, bias,
-                                                                     save_mean, save_invstd, coef, dx,
-                                                                     reinterpret_cast<uint2 *>(dx_bf16), dres, rmode,
-                                                                     train);
+  bn_bwd_apply2d_kernel<TX, TY><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
+      rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
+      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, timg, dimg4);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
@@ -516,6 +552,50 @@ int adaptseg_bn_workspace_size(int64_t rows, int c, size_t *bytes) {
   return ADAPTSEG_OK;
 }
 
+// Shared checks and apply launch of the forward entry points.  Storage: x fp32 or bf16 (bf16
+// activation storage, BF16 maths); the residual stored like x — or, under the F32X3 maths, as
+// the three term images of an fp32 residual (res_bf16) beside an fp32 x.  Outputs y (fp32) and
+// / or its operand copy y_bf16 (bf16 RNE image, or the three term images under F32X3).
+static int check_fwd_storage(const char *who, const float *x, const uint16_t *x_bf16, const float *res,
+                             const uint16_t *res_bf16, const float *y, const uint16_t *y_bf16) {
+  AS_CHECK_ARG((x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16), "%s: exactly one of x / x_bf16, and y or y_bf16",
+               who);
+  AS_CHECK_ARG(!(res && res_bf16), "%s: one residual pointer", who);
+  if (copies_are_terms())
+    AS_CHECK_ARG(x, "%s: under the F32X3 conv maths x is fp32 (its copies are term images of fp32 tensors)", who);
+  else
+    AS_CHECK_ARG(x ? !res_bf16 : !res, "%s: the residual must be stored like x (fp32 or bf16)", who);
+  return ADAPTSEG_OK;
+}
+
+static double fwd_apply_bytes(int64_t rows, int c, const float *x, const float *res, const uint16_t *res_bf16,
+                              const float *y, const uint16_t *y_bf16) {
+  const bool terms = copies_are_terms();
+  const double copyb = terms ? 6.0 : 2.0;
+  return ((x ? 4.0 : 2.0) + (res ? 4.0 : res_bf16 ? copyb : 0.0) + (y ? 4.0 : 0.0) + (y_bf16 ? copyb : 0.0)) *
+         (double)rows * c;
+}
+
+static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *mean,
+                         const float *invstd, const float *weight, const float *bias, const float *res,
+                         const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu, hipStream_t s) {
+  const ApplyPlan ap = apply_plan(rows, c);
+  const dim3 g(ap.cblocks, ap.rsplits);
+  const int64_t timg = rows * c, yimg4 = copies_are_terms() && y_bf16 ? rows * c / 4 : 0;
+  uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
+  const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
+  if (x && rb)
+    bn_apply2d_kernel<float, X3><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, rb, y, yb,
+                                                   relu, timg, yimg4);
+  else if (x)
+    bn_apply2d_kernel<float, float><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, res, y,
+                                                      yb, relu, timg, yimg4);
+  else
+    bn_apply2d_kernel<__bf16, __bf16><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
+                                                        reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
+                                                        weight, bias, rb, y, yb, relu, timg, yimg4);
+}
+
 int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
                             const float *bias, float *running_mean, float *running_var, float momentum, float eps,
                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
@@ -524,9 +604,9 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
-  AS_CHECK_ARG((x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && save_mean && save_invstd,
-               "bn_fwd_train: exactly one of x / x_bf16, and y or y_bf16");
-  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_train: the residual must be stored like x (fp32 or bf16)");
+  AS_CHECK_ARG(save_mean && save_invstd, "bn_fwd_train: null statistics output");
+  int st = check_fwd_storage("bn_fwd_train", x, x_bf16, res, res_bf16, y, y_bf16);
+  if (st) return st;
   size_t need = bn_ws_bytes(rows, c);
   if (!ws || ws_bytes < need) {
     set_error("bn_fwd_train: workspace %zu < %zu", ws_bytes, need);
@@ -538,7 +618,7 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
   const double eb = x ? 4.0 : 2.0;   // bytes per activation element read
   int slot;  // x in
   timing_begin(kTBnReduceStats, s, eb * rows * c, &slot);
-  const __bf16 *xb = reinterpret_cast<const __bf16 *>(x_bf16), *rb = reinterpret_cast<const __bf16 *>(res_bf16);
+  const __bf16 *xb = reinterpret_cast<const __bf16 *>(x_bf16);
   if (x)
     bn_reduce_kernel<0, float><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
                                                                        nullptr, nullptr, nullptr, 0, r.per, partial);
@@ -554,17 +634,8 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
     bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, xb, partial, save_mean,
                                                                    save_invstd, running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
-  const ApplyPlan ap = apply_plan(rows, c);
-  timing_begin(kTBnApply, s, eb * rows * c * ((res || res_bf16) ? 2 : 1) + (y ? 4.0 * rows * c : 0.0) +
-                                 (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
-  if (x)
-    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                   weight, bias, res, y,
-                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
-  else
-    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, xb, save_mean, save_invstd,
-                                                                   weight, bias, rb, y,
-                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
+  timing_begin(kTBnApply, s, fwd_apply_bytes(rows, c, x, res, res_bf16, y, y_bf16), &slot);
+  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
@@ -584,28 +655,17 @@ int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int n
                                   float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
                                   float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
-  AS_CHECK_ARG(stats && ntiles > 0 && (x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && save_mean &&
-                   save_invstd,
-               "bn_fwd_train_tiles: null pointer (exactly one of x / x_bf16)");
-  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_train_tiles: the residual must be stored like x (fp32 or bf16)");
+  AS_CHECK_ARG(stats && ntiles > 0 && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
+  int st = check_fwd_storage("bn_fwd_train_tiles", x, x_bf16, res, res_bf16, y, y_bf16);
+  if (st) return st;
   hipStream_t s = as_stream(stream);
   bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
                                                                    running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_tiles_final");
-  const ApplyPlan ap = apply_plan(rows, c);
-  const double eb = x ? 4.0 : 2.0;
   int slot;  // x (+res) in, y out
-  timing_begin(kTBnApply, s, eb * rows * c * ((res || res_bf16) ? 2 : 1) + (y ? 4.0 * rows * c : 0.0) +
-                                 (y_bf16 ? 2.0 * rows * c : 0.0), &slot);
-  if (x)
-    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(rows, c, ap.tc, ap.per, x, save_mean, save_invstd,
-                                                                   weight, bias, res, y,
-                                                                   reinterpret_cast<uint2 *>(y_bf16), relu);
-  else
-    bn_apply2d_kernel<<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
-        rows, c, ap.tc, ap.per, reinterpret_cast<const __bf16 *>(x_bf16), save_mean, save_invstd, weight, bias,
-        reinterpret_cast<const __bf16 *>(res_bf16), y, reinterpret_cast<uint2 *>(y_bf16), relu);
+  timing_begin(kTBnApply, s, fwd_apply_bytes(rows, c, x, res, res_bf16, y, y_bf16), &slot);
+  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
@@ -624,20 +684,24 @@ int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t 
                             const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
                             adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
-  AS_CHECK_ARG((x != nullptr) != (x_bf16 != nullptr) && (y || y_bf16) && running_mean && running_var,
-               "bn_fwd_infer: null pointer (exactly one of x / x_bf16)");
-  AS_CHECK_ARG(x ? !res_bf16 : !res, "bn_fwd_infer: the residual must be stored like x (fp32 or bf16)");
+  AS_CHECK_ARG(running_mean && running_var, "bn_fwd_infer: null running statistics");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
+  int st = check_fwd_storage("bn_fwd_infer", x, x_bf16, res, res_bf16, y, y_bf16);
+  if (st) return st;
   hipStream_t s = as_stream(stream);
-  int64_t total4 = rows * c / 4;
-  if (x)
-    bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps, weight, bias,
-                                                           res, y, reinterpret_cast<uint2 *>(y_bf16), relu);
+  const int64_t total4 = rows * c / 4, timg = rows * c, yimg4 = copies_are_terms() && y_bf16 ? total4 : 0;
+  uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
+  const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
+  if (x && rb)
+    bn_infer_apply_kernel<float, X3><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
+                                                                      weight, bias, rb, y, yb, relu, timg, yimg4);
+  else if (x)
+    bn_infer_apply_kernel<float, float><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
+                                                                         weight, bias, res, y, yb, relu, timg, yimg4);
   else
-    bn_infer_apply_kernel<<<grid_for(total4), 256, 0, s>>>(total4, c, reinterpret_cast<const __bf16 *>(x_bf16),
-                                                           running_mean, running_var, eps, weight, bias,
-                                                           reinterpret_cast<const __bf16 *>(res_bf16), y,
-                                                           reinterpret_cast<uint2 *>(y_bf16), relu);
+    bn_infer_apply_kernel<__bf16, __bf16><<<grid_for(total4), 256, 0, s>>>(
+        total4, c, reinterpret_cast<const __bf16 *>(x_bf16), running_mean, running_var, eps, weight, bias, rb, y, yb,
+        relu, timg, yimg4);
   AS_CHECK_LAUNCH("bn_infer_apply");
   return ADAPTSEG_OK;
 }
@@ -654,10 +718,13 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
                        const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
                        float *dweight, float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
-  const bool xb = x_bf16 != nullptr;
+  const bool xb = x_bf16 != nullptr, terms = copies_are_terms();
   AS_CHECK_ARG(dy && (dx || dx_bf16) && save_invstd && (!train || ((x || x_bf16) && save_mean)), "bn_bwd: null pointer");
-  AS_CHECK_ARG(!(x && x_bf16) && !(y && y_bf16) && (xb ? !y : !y_bf16),
-               "bn_bwd: the saved x and y are both fp32 or both bf16 (one pointer each)");
+  AS_CHECK_ARG(!(x && x_bf16) && !(y && y_bf16), "bn_bwd: one pointer each for the saved x and y");
+  if (terms)   // F32X3 maths: x fp32, y fp32 or its three term images
+    AS_CHECK_ARG(!xb, "bn_bwd: under the F32X3 conv maths x is fp32 (y may be term images)");
+  else
+    AS_CHECK_ARG(xb ? !y : !y_bf16, "bn_bwd: the saved x and y are both fp32 or both bf16 (one pointer each)");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
   AS_CHECK_ARG(!relu || y || y_bf16 || train, "bn_bwd: activation without y needs train mode (mask from x)");
   AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
@@ -666,12 +733,16 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
   const bool has_y = y || y_bf16;
   const int rmode = relu == 0 ? 0 : relu == 1 ? (has_y ? 1 : 2) : (has_y ? 3 : 4);
   hipStream_t s = as_stream(stream);
+  if (terms && y_bf16)
+    return bn_bwd_launch<float, X3>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), x, weight, bias,
+                                    save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
+                                    ws_bytes, s);
   if (xb || (!x && y_bf16))
-    return bn_bwd_launch(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), reinterpret_cast<const __bf16 *>(x_bf16),
-                         weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
-                         ws_bytes, s);
-  return bn_bwd_launch(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
-                       dweight, dbias, ws, ws_bytes, s);
+    return bn_bwd_launch<__bf16>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16),
+                                 reinterpret_cast<const __bf16 *>(x_bf16), weight, bias, save_mean, save_invstd, dx,
+                                 dx_bf16, dres, rmode, train, dweight, dbias, ws, ws_bytes, s);
+  return bn_bwd_launch<float>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
+                              dweight, dbias, ws, ws_bytes, s);
 }
 
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,

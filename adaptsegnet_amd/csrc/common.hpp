@@ -68,6 +68,53 @@ __device__ __forceinline__ float epi_act_grad(float v, float a, int flags) {
 }
 constexpr int kEpiActGrad = ADAPTSEG_EPI_LEAKY_GRAD | ADAPTSEG_EPI_RELU_GRAD;
 
+// F32X3 operand split: v = hi + mid + lo EXACTLY, each term the RNE bf16 of what is left
+// (3 x 8 significant bits cover fp32's 24; bf16 has fp32's exponent range).  The conv kernels
+// split their staged operands with it and the BatchNorm passes write the term images the
+// LDS-DMA F32X3 kernels read (conv_x3.hpp, conv_x3r.hpp) with it, so both give the same bits.
+typedef float floatx2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// (a, b) -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32) and the two values it rounds to
+__device__ __forceinline__ uint32_t rne2(float a, float b, float &ra, float &rb) {
+  const floatx2v f = {a, b};
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
+  ra = __uint_as_float(u << 16);
+  rb = __uint_as_float(u & 0xffff0000u);
+  return u;
+}
+
+// v = hi + mid + lo exactly (each term RNE to bf16), for a pair of values: packed bf16 pairs
+__device__ __forceinline__ void split3_2(float a, float b, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
+  float ha, hb, ma, mb;
+  hi = rne2(a, b, ha, hb);
+  a -= ha;
+  b -= hb;
+  mid = rne2(a, b, ma, mb);
+  const floatx2v r = {a - ma, b - mb};
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+}
+
+// four elements -> three packed 4 x bf16
+__device__ __forceinline__ void split3(float4 v, uint2 &hi, uint2 &mid, uint2 &lo) {
+  split3_2(v.x, v.y, hi.x, mid.x, lo.x);
+  split3_2(v.z, v.w, hi.y, mid.y, lo.y);
+}
+
+// four elements back from their three term images (hi + mid is exact, + lo gives v exactly)
+__device__ __forceinline__ float4 join3(uint2 h, uint2 m, uint2 l) {
+  auto f = [](uint32_t u, bool up) { return __uint_as_float(up ? (u & 0xffff0000u) : (u << 16)); };
+  return make_float4((f(h.x, false) + f(m.x, false)) + f(l.x, false), (f(h.x, true) + f(m.x, true)) + f(l.x, true),
+                     (f(h.y, false) + f(m.y, false)) + f(l.y, false), (f(h.y, true) + f(m.y, true)) + f(l.y, true));
+}
+
+int conv_math();   // process-wide conv arithmetic (adaptseg_conv_set_math)
+// Operand copies of the _x entry points are three exact bf16 term images [3][rows][C] under the
+// F32X3 maths (one bf16 RNE image under the BF16 maths)
+inline bool copies_are_terms() {
+  return conv_math() == ADAPTSEG_MATH_F32X3 || conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT;
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Live timing (adaptseg_timing_*, conv_igemm.hip): hipEvent pair around one launch; `units` are

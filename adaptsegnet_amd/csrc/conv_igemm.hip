@@ -333,6 +333,16 @@ int plan_bm(const Plan &pl) {
   return (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
 }
 
+// F32X3 maths with the caller's term images of the activation operand(s) (the _x forms'
+// copies: three exact bf16 images [3][n][h][w][c]): the product moves to the x3r kernel, which
+// reads them by LDS-DMA instead of splitting fp32 rows in-kernel.  Re-plans the grid.
+static void x3_terms(Plan &pl) {
+  if (conv_math() != ADAPTSEG_MATH_F32X3 || !pl.fast || !pl.x3 || !pl.x3r_ok || !pl.act_ext) return;
+  if (pl.mode == MODE_WGRAD && !pl.act_ext2) return;
+  pl.x3g = pl.x3r = pl.x3ext = true;
+  set_splits(pl);
+}
+
 // Grid decomposition: tiles, then split K until the grid has ~2 blocks per CU while keeping
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
@@ -483,7 +493,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.bf16 = true;
   }
   // F32X3 conv math: the vector FAST cases whose 16-deep K tiles stay inside one tap
-  pl.x3 = pl.x3g = pl.x3r = false;
+  pl.x3 = pl.x3g = pl.x3r = pl.x3r_ok = pl.x3ext = false;
   pl.x3r_bm = 256;
   const bool x3_math = conv_math() == ADAPTSEG_MATH_F32X3 || conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT;
   if (x3_math && pl.fast && !pl.ae && !pl.be) {
@@ -492,13 +502,19 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.x3 = true;
     // pre-split operand images by LDS-DMA (conv_x3g.hpp): 16-B chunks of both weight-gradient
     // operands (Cin, Cout multiples of 8); every F32X3 forward / data gradient qualifies
+    // 256x128 tiles with 32-deep steps on pre-split term images (conv_x3r.hpp): a 32-deep
+    // step inside one tap; weight gradients in 16-B channel chunks of both operands
+    if (pl.x3) {
+      if (op == ADAPTSEG_CONV_FWD) pl.x3r_ok = d->c % kX3rBK == 0;
+      else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3r_ok = d->k % kX3rBK == 0;
+      else pl.x3r_ok = d->c % 8 == 0 && d->k % 8 == 0;
+      if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = d->k >= 256 ? 256 : 128;
+    }
+    // F32X3_PRESPLIT: every such product on the pre-split kernels, term images made per call
+    // unless the caller supplies them; F32X3 (default): on x3r only when it does (x3_terms)
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) {
       pl.x3g = op != ADAPTSEG_CONV_BWD_WEIGHT || (d->c % 8 == 0 && d->k % 8 == 0);
-      // 256x128 tiles with 32-deep steps (conv_x3r.hpp): a 32-deep step inside one tap
-      if (op == ADAPTSEG_CONV_FWD) pl.x3r = d->c % kX3rBK == 0;
-      else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3r = d->k % kX3rBK == 0;
-      else pl.x3r = pl.x3g;
-      if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = d->k >= 256 ? 256 : 128;
+      pl.x3r = pl.x3r_ok;
     }
   }
   if (pl.x3) pl.cfg = 0;
@@ -668,11 +684,28 @@ __global__ void bf16_out_copy_kernel(const float *__restrict__ y, __bf16 *__rest
     yb[i] = (__bf16)y[i];
 }
 
+// F32X3 maths: the three exact term images [3][n] of a finished fp32 output
+__global__ void x3_out_copy_kernel(const float *__restrict__ y, __bf16 *__restrict__ yb, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h, m, l;
+    split3_2(y[i], 0.f, h, m, l);
+    yb[i] = __builtin_bit_cast(__bf16, (uint16_t)h);
+    yb[i + n] = __builtin_bit_cast(__bf16, (uint16_t)m);
+    yb[i + 2 * n] = __builtin_bit_cast(__bf16, (uint16_t)l);
+  }
+}
+
+// The operand copy of a finished output (the paths whose kernels do not write it): a bf16 RNE
+// image, or the three term images under the F32X3 maths
 static int out_copy(const float *y, uint16_t *yb, int64_t n, hipStream_t s) {
   if (!yb || n == 0) return ADAPTSEG_OK;
-  bf16_out_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 8192), 256, 0, s>>>(
-      y, reinterpret_cast<__bf16 *>(yb), n);
-  AS_CHECK_LAUNCH("bf16_out_copy");
+  AS_CHECK_ARG(y, "conv: an operand copy needs the fp32 output on this path");
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n, 256), 8192);
+  if (copies_are_terms())
+    x3_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n);
+  else
+    bf16_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n);
+  AS_CHECK_LAUNCH("out_copy");
   return ADAPTSEG_OK;
 }
 
@@ -685,6 +718,7 @@ bool use_thin(const adaptseg_conv_desc *d, int op) { return thin_eligible(d, op)
 static bool copy_only(const Plan &pl, const adaptseg_conv_desc *d, int op) {
   if (use_thin(d, op)) return false;
   if (tapgemm_eligible(d)) return tapgemm_copy_only(d, op);
+  if (conv_math() == ADAPTSEG_MATH_F32X3) return pl.fast && pl.x3 && pl.x3r_ok;   // x3r on the caller's terms
   return pl.g16 || (pl.bf16 && op == ADAPTSEG_CONV_FWD);
 }
 
@@ -724,6 +758,12 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
     set_splits(g);
     b = std::max(b, g.slab_bytes);
   }
+  if (pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3) {   // the plan with the caller's term images
+    Plan t = pl;
+    t.x3g = t.x3r = t.x3ext = true;
+    set_splits(t);
+    b = std::max(b, t.slab_bytes);
+  }
   if (tapgemm_eligible(d)) b = std::max(b, tapgemm_workspace(d, op));
   if (use_thin(d, op)) b = std::max(b, thin_workspace(d, op));
   if (op == ADAPTSEG_CONV_BWD_WEIGHT) {
@@ -748,6 +788,19 @@ int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_i
     return ADAPTSEG_OK;
   }
   if (tapgemm_eligible(d)) return tapgemm_kernel_id(d, op, kernel_id, splits);
+  *kernel_id = ::adaptseg::kernel_id(pl, op);
+  *splits = pl.p.splits;
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_kernel_id_x(const adaptseg_conv_desc *d, int op, int with_copies, int *kernel_id, int *splits) {
+  AS_CHECK_ARG(kernel_id && splits, "conv2d_kernel_id_x: null");
+  if (!with_copies || use_thin(d, op) || tapgemm_eligible(d)) return adaptseg_conv2d_kernel_id(d, op, kernel_id, splits);
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  pl.act_ext = pl.act_ext2 = d;   // any non-NULL: the plan with the caller's operand copies
+  x3_terms(pl);
   *kernel_id = ::adaptseg::kernel_id(pl, op);
   *splits = pl.p.splits;
   return ADAPTSEG_OK;
@@ -839,17 +892,21 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
+  x3_terms(pl);
   // a misaligned weight clears pl.fast and, in set_splits, the bf16-operand kernel: only that
   // kernel reads the copy, so a NULL x needs it to survive the alignment checks too
   AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd: x is NULL but the plan (after the alignment checks) needs the fp32 input");
+  const bool terms = copies_are_terms();   // F32X3: term images of y by a pass after the GEMM
+  AS_CHECK_ARG(y || !terms, "conv fwd: under the F32X3 maths the output is fp32 (y_bf16 is its term images)");
   p.out = y;
-  p.outb = reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
   p.res = res;
   p.flags = flags;
   st = attach_wpack(pl, w_pack);
   if (st) return st;
-  return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
+  st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
+  return (st || !terms) ? st : out_copy(y, y_bf16, ny, as_stream(stream));
 }
 
 int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
@@ -864,12 +921,20 @@ int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
 }
 
 int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles) {
+  return adaptseg_conv2d_bnstats_tiles_x(d, 0, ntiles);
+}
+
+int adaptseg_conv2d_bnstats_tiles_x(const adaptseg_conv_desc *d, int with_copy, int *ntiles) {
   AS_CHECK_ARG(ntiles, "conv2d_bnstats_tiles: null");
   *ntiles = 0;
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
   if (tapgemm_eligible(d)) return ADAPTSEG_OK;
+  if (with_copy) {
+    pl.act_ext = d;   // any non-NULL: the plan with the caller's copy of x
+    x3_terms(pl);
+  }
   if (pl.fast && pl.p.splits == 1)
     *ntiles = (int)ceil_div(pl.p.M, plan_bm(pl));
   return ADAPTSEG_OK;
@@ -907,10 +972,13 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   if (reinterpret_cast<uintptr_t>(x) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(x_bf16) ? x_bf16 : nullptr;
+  x3_terms(pl);
   AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd_bnstats: x is NULL but the plan (after the alignment checks) needs the fp32 input");
+  const bool terms = copies_are_terms();
+  AS_CHECK_ARG(y || !terms, "conv fwd_bnstats: under the F32X3 maths the output is fp32");
   p.out = y;
-  p.outb = reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
     const int nt = (int)ceil_div(p.M, plan_bm(pl));
@@ -922,7 +990,8 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   }
   st = attach_wpack(pl, w_pack);
   if (st) return st;
-  return run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
+  st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
+  return (st || !terms) ? st : out_copy(y, y_bf16, (int64_t)d->n * d->oh * d->ow * d->k, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
@@ -965,16 +1034,19 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   if (reinterpret_cast<uintptr_t>(dy) & 15) pl.va = pl.fast = false;
   set_splits(pl);
   pl.act_ext = aligned16(dy_bf16) ? dy_bf16 : nullptr;
-  AS_CHECK_ARG(dy || (pl.g16 && pl.act_ext),
+  x3_terms(pl);
+  AS_CHECK_ARG(dy || ((pl.g16 || pl.x3ext) && pl.act_ext),
                "conv bwd_data: dy is NULL but the plan (after the alignment checks) needs the fp32 dY");
+  const bool terms = copies_are_terms();
   p.out = dx;
-  p.outb = reinterpret_cast<__bf16 *>(dx_bf16);
+  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(dx_bf16);
   p.res = res;
   p.aux = aux;
   p.flags = flags;
   st = attach_wpack(pl, w_pack);
   if (st) return st;
-  return run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
+  st = run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
+  return (st || !terms) ? st : out_copy(dx, dx_bf16, nx, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
@@ -1016,7 +1088,8 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
       pl.act_ext = dy_bf16;
       pl.act_ext2 = x_bf16;
     }
-    AS_CHECK_ARG((dy && x) || (pl.g16 && pl.act_ext),
+    x3_terms(pl);
+    AS_CHECK_ARG((dy && x) || ((pl.g16 || pl.x3ext) && pl.act_ext),
                  "conv bwd_weight: dy / x is NULL but the plan (after the alignment checks) needs the fp32 operands");
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
     st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);

@@ -27,7 +27,7 @@ size_t x3_wpack_bytes(const Plan &pl) {
 // dY) and, for the weight gradient, of x
 size_t x3g_act_elems(const Plan &pl) {
   const ConvParams &p = pl.p;
-  if (!pl.x3g) return 0;
+  if (!pl.x3g) return 0;   // (x3ext: the caller's images have this size too, see launch_x3)
   return pl.mode == MODE_FWD ? (size_t)p.n * p.h * p.w * p.c : (size_t)p.n * p.oh * p.ow * p.k;
 }
 size_t x3g_act2_elems(const Plan &pl) {
@@ -39,6 +39,7 @@ static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 // workspace ahead of the split-K slabs: [weight pack][three term images of the activation
 // operand (+ of x for the weight gradient) when the caller supplied none]
 size_t x3_pre_bytes(const Plan &pl) {
+  if (pl.x3ext && pl.x3r) return al256(x3_wpack_bytes(pl));   // the caller's term images
   return al256(x3_wpack_bytes(pl)) + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)) +
          al256(3 * x3g_act2_elems(pl) * sizeof(__bf16));
 }

@@ -58,34 +58,8 @@ __device__ __forceinline__ bf16x8 kc16_frag(const char *img, int r0, int lane) {
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef float floatx2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-// (a, b) -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32) and the two values it rounds to
-__device__ __forceinline__ uint32_t rne2(float a, float b, float &ra, float &rb) {
-  const floatx2v f = {a, b};
-  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
-  ra = __uint_as_float(u << 16);
-  rb = __uint_as_float(u & 0xffff0000u);
-  return u;
-}
-
-// v = hi + mid + lo exactly (each term RNE to bf16), for a pair of values: packed bf16 pairs
-__device__ __forceinline__ void split3_2(float a, float b, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
-  float ha, hb, ma, mb;
-  hi = rne2(a, b, ha, hb);
-  a -= ha;
-  b -= hb;
-  mid = rne2(a, b, ma, mb);
-  const floatx2v r = {a - ma, b - mb};
-  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
-}
-
-// four elements -> three packed 4 x bf16
-__device__ __forceinline__ void split3(float4 v, uint2 &hi, uint2 &mid, uint2 &lo) {
-  split3_2(v.x, v.y, hi.x, mid.x, lo.x);
-  split3_2(v.z, v.w, hi.y, mid.y, lo.y);
-}
+// the exact three-term split (rne2 / split3_2 / split3) lives in common.hpp: the BatchNorm
+// passes that write F32X3 term images use the same arithmetic
 
 template <int MODE, bool S2>
 __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {

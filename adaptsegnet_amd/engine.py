@@ -74,15 +74,24 @@ class WgradStream:
 
 
 def bf16_operands() -> bool:
-    """Under the bf16 conv math (config c5) the BN passes that produce conv operands also write
-    a bf16 copy of them, which the bf16 LDS-DMA conv kernel reads instead of converting the
-    fp32 tensor itself (adaptseg_conv2d_*_x): one pass over every such activation less.
+    """Operand copies are on: the BN passes that produce conv operands (BN+ReLU outputs, block
+    outputs, BN-backward outputs) write them, and the conv kernels read them instead of the fp32
+    tensor (adaptseg_conv2d_*_x); an fp32 tensor is written only where a consumer still reads
+    fp32 (bf16_only).
+      * BF16 math (config c5): a bf16 copy, which the bf16 LDS-DMA kernels read instead of
+        converting the operand themselves.  The generator's activations are also STORED in bf16
+        (lowp_storage), as torch.autocast(bfloat16) does.
+      * F32X3 math (c2-c4): the operand's three exact bf16 term images [3, *shape]
+        (kernels.copies_are_terms), which the 256x128x32 F32X3 kernel (conv_x3r.hpp) reads by
+        LDS-DMA instead of splitting fp32 rows in-kernel — the same products, bitwise the same
+        results.  Conv outputs stay fp32 (the BN passes read them)."""
+    return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE, K.MATH_F32X3)
 
-    It also stores the generator's activations in bf16, as torch.autocast(bfloat16) does: every
-    Bottleneck conv output (c1, c2, c3, the downsample's), the BN outputs and the residual
-    stream (the block outputs) are bf16 tensors; BatchNorm normalises them in fp32 with fp32
-    statistics (from the conv's fp32 accumulators); the gradients stay fp32.  An fp32 copy of
-    a BN output / block output is written only where a consumer kernel still reads fp32."""
+
+def lowp_storage() -> bool:
+    """bf16 activation storage (the BF16 math only): Bottleneck conv outputs, BN outputs and the
+    residual stream are bf16 tensors; BatchNorm normalises them in fp32 with fp32 statistics
+    (from the conv's fp32 accumulators); the gradients stay fp32."""
     return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
 
 
@@ -194,21 +203,22 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     oh, ow = g1.out_hw(h, w)
     conv = _conv_bn if training else _conv_plain
-    sh = bf16_operands()   # bf16 conv math: bf16 activation storage + operand copies
+    sh = bf16_operands()   # operand copies (bf16 or F32X3 term images)
+    lp = lowp_storage()    # bf16 math: conv outputs stored in bf16
     # y1 / y2 are read only by the next conv's forward and weight gradient (the BN backward
     # recomputes its ReLU mask from x in train mode, reads the bf16 y in eval mode) — with both
     # on bf16-operand kernels, only their bf16 copies are written
     thin1 = sh and bf16_only(g2, n, oh, ow, (0, 2))
     thin2 = sh and bf16_only(g3, n, oh, ow, (0, 2))
-    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=sh)
+    c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=lp)
     y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh, fp32=not thin1)
-    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=sh)
+    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
     y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
-    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=sh)
+    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
     cd = sd = None
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
-        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight, xb=xb, bf16_only=sh)
+        cd, td = conv(dconv.geom(), x, n, h, w, dconv.weight, xb=xb, bf16_only=lp)
         r, sd, rb = bn_forward_b(dbn, cd, None, False, training, td, bf16=sh, fp32=not sh)
         if sh:
             r = rb   # the residual stream is bf16
@@ -515,7 +525,7 @@ class _FCDiscriminatorFn(torch.autograd.Function):
         convs = model._convs()
         n, c, h, w = x.shape
         xs = _input_strides(x)
-        sh = bf16_operands()   # bf16 conv math: each conv epilogue also writes the next conv's operand copy
+        sh = lowp_storage()   # bf16 math: each conv epilogue also writes the next conv's operand copy
         acts, actsb, dims = [], [], []
         cur, curb, ch, cw, cs = x, None, h, w, xs
         for i, conv in enumerate(convs):
@@ -542,7 +552,7 @@ class _FCDiscriminatorFn(torch.autograd.Function):
             return None, None, None, None
         model, acts, actsb, dims, n = ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n
         convs = model._convs()
-        sh = bf16_operands()
+        sh = lowp_storage()   # (F32X3 term images would cost the D convs a separate copy pass)
         need_w = ctx.need_w
         if need_w:
             model._arena.claim(model._pidx["all"])

@@ -195,10 +195,11 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weights, bias
     return (out, outb) if bf16_out else out
 
 
-def conv_bnstats_tiles(g: ConvGeom, n: int, h: int, w: int, strides) -> int:
+def conv_bnstats_tiles(g: ConvGeom, n: int, h: int, w: int, strides, with_copy: bool = False) -> int:
     d = _desc(g, n, h, w, tuple(strides))[0]
     nt = ctypes.c_int(0)
-    check(_lib.lib().adaptseg_conv2d_bnstats_tiles(ctypes.byref(d), ctypes.byref(nt)), "conv2d_bnstats_tiles")
+    check(_lib.lib().adaptseg_conv2d_bnstats_tiles_x(ctypes.byref(d), 1 if with_copy else 0, ctypes.byref(nt)),
+          "conv2d_bnstats_tiles")
     return nt.value
 
 
@@ -209,7 +210,7 @@ def conv_fwd_bnstats(g: ConvGeom, x: torch.Tensor, n: int, h: int, w: int, weigh
     only (bf16 activation storage, config c5; the statistics still come from the fp32
     accumulators)."""
     strides = tuple(strides or nhwc_strides(n, h, w, g.cin))
-    nt = conv_bnstats_tiles(g, n, h, w, strides)
+    nt = conv_bnstats_tiles(g, n, h, w, strides, with_copy=xb is not None and _aligned16(xb))
     # the tile count is planned for 16-byte aligned operands; an unaligned view (a storage
     # offset) takes a kernel without fused statistics, so plan the plain forward for it
     if nt == 0 or not _aligned16(x, *weights):
@@ -260,8 +261,17 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w
 # ---------------------------------------------------------------------------------------
 # BatchNorm (x as [rows, C])
 # ---------------------------------------------------------------------------------------
+def copies_are_terms() -> bool:
+    """Under the F32X3 maths an operand copy is the three exact bf16 term images of an fp32
+    tensor, [3, *shape] (adaptseg.h: the _x forms' copies); under BF16 one bf16 (RNE) image."""
+    return _ops._CONV_MATH[0] in (MATH_F32X3, MATH_F32X3_PRESPLIT)
+
+
 def _bf16_like(t, want):
-    return torch.empty(t.shape, device=t.device, dtype=torch.bfloat16) if want else None
+    if not want:
+        return None
+    shape = ((3,) if copies_are_terms() else ()) + tuple(t.shape)
+    return torch.empty(shape, device=t.device, dtype=torch.bfloat16)
 
 
 def _f32_like(t):
@@ -515,13 +525,14 @@ def as_nchw(t: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------
 # Live kernel timing (bench.py roofline)
 # ---------------------------------------------------------------------------------------
-def conv_kernel_id(g: ConvGeom, n, h, w, op, strides=None):
-    """(selector, splits) of the igemm kernel that runs this conv product."""
+def conv_kernel_id(g: ConvGeom, n, h, w, op, strides=None, copies: bool = False):
+    """(selector, splits) of the igemm kernel that runs this conv product (copies: called with
+    the operand copies of the _x forms — F32X3 term images, bf16 copies)."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
     d = _desc(g, n, h, w, tuple(strides))[0]
     kid, sp = ctypes.c_int(0), ctypes.c_int(0)
-    check(_lib.lib().adaptseg_conv2d_kernel_id(ctypes.byref(d), op, ctypes.byref(kid), ctypes.byref(sp)),
-          "conv2d_kernel_id")
+    check(_lib.lib().adaptseg_conv2d_kernel_id_x(ctypes.byref(d), op, 1 if copies else 0, ctypes.byref(kid),
+                                                 ctypes.byref(sp)), "conv2d_kernel_id")
     return kid.value, sp.value
 
 

@@ -63,10 +63,13 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
     from adaptsegnet_amd import engine
     inv = {}
 
-    def add(geom, n, h, w, op, strides=None, count=1, algo=None):
+    copies = engine.bf16_operands()   # the Bottleneck products get their operand copies
+
+    def add(geom, n, h, w, op, strides=None, count=1, algo=None, cp=False):
         # geom: the geometry the engine launches; algo: the reference's (unpadded) one, whose
-        # FLOPs are counted
-        kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides)
+        # FLOPs are counted; cp: the engine passes the operand copies (engine.block_forward /
+        # block_backward under bf16_operands)
+        kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides, copies=cp and copies)
         inv[kid] = inv.get(kid, 0.0) + count * (algo or geom).flops(n, h, w)
         if products is not None:
             products.add((op, kid, sp > 1))
@@ -108,17 +111,18 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
                 if backward and "l5" in heads_bwd:
                     add(g5, batch, h, w, 1)
                     add(g5, batch, h, w, 2)
-            for blk in layer:
-                convs = [(blk.conv1, h, w)]
+            for bi, blk in enumerate(layer):
+                first = li == 1 and bi == 0   # its input (the max-pool output) has no copy
+                convs = [(blk.conv1, h, w, not first)]
                 oh, ow = blk.conv1.geom().out_hw(h, w)
-                convs += [(blk.conv2, oh, ow), (blk.conv3, oh, ow)]
+                convs += [(blk.conv2, oh, ow, True), (blk.conv3, oh, ow, True)]
                 if blk.downsample is not None:
-                    convs.append((blk.downsample[0], h, w))
-                for conv, ch, cw in convs:
-                    add(conv.geom(), batch, ch, cw, 0)
+                    convs.append((blk.downsample[0], h, w, not first))
+                for conv, ch, cw, xcp in convs:
+                    add(conv.geom(), batch, ch, cw, 0, cp=xcp)
                     if backward and (li < 4 or "l6" in heads_bwd):
-                        add(conv.geom(), batch, ch, cw, 1)
-                        add(conv.geom(), batch, ch, cw, 2)
+                        add(conv.geom(), batch, ch, cw, 1, cp=True)
+                        add(conv.geom(), batch, ch, cw, 2, cp=xcp)
                 h, w = oh, ow
         g6 = engine.aspp_geom(model.layer6)
         add(g6, batch, h, w, 0)

@@ -92,6 +92,10 @@ int adaptseg_conv_get_math(int *math);
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
 /* Kernel selector (see adaptseg_timing_enable) and K-split count the library would use. */
 int adaptseg_conv2d_kernel_id(const adaptseg_conv_desc *d, int op, int *kernel_id, int *splits);
+/* The same for a call of the _x forms that passes the operand copies (with_copies != 0): under
+   the F32X3 maths the products the 256x128x32 term-image kernel covers move to it (selector
+   100*op + 88, + 89 for the stride-2 parity path / 128-row weight gradients). */
+int adaptseg_conv2d_kernel_id_x(const adaptseg_conv_desc *d, int op, int with_copies, int *kernel_id, int *splits);
 
 /* y[n,oh,ow,k] = sum_seg conv(x, w[seg]) + sum_seg bias[seg]   (bias may be NULL) */
 int adaptseg_conv2d_fwd(const adaptseg_conv_desc *d, const float *x, const float *const *w,
@@ -110,6 +114,9 @@ int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes);
    statistics for this geometry), assuming 16-byte aligned operands: lets a caller size and
    plan the BatchNorm that follows before launching (host-side, no GPU). */
 int adaptseg_conv2d_bnstats_tiles(const adaptseg_conv_desc *d, int *ntiles);
+/* ... for adaptseg_conv2d_fwd_bnstats_x called with (with_copy != 0) or without x's copy: under
+   the F32X3 maths the copy moves the product to a kernel with 256-row tiles. */
+int adaptseg_conv2d_bnstats_tiles_x(const adaptseg_conv_desc *d, int with_copy, int *ntiles);
 int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, const float *const *w,
                                 float *y, float *stats, size_t stats_bytes, int *ntiles, void *ws,
                                 size_t ws_bytes, adaptseg_stream_t stream);

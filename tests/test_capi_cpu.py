@@ -129,8 +129,16 @@ def test_bf16_operand_abi_checks_on_host():
     L = _lib.lib()
     d = K._desc(K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,)), 4, 64, 128, K.nhwc_strides(4, 64, 128, 256))[0]
     w = _lib.ptr_array([16])
-    # F32X3 math: no bf16-operand kernel, so the fp32 input is required
+    # F32X3 math: the copy is the operand's three term images, which the 256x128x32 kernel reads
+    # in place of x (the call passes the host checks and stops at the missing workspace) ...
     st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, ctypes.c_void_p(256), w, None, None, None,
+                                 ctypes.c_void_p(512), None, 0, None, 0, None)
+    assert st == 4, L.adaptseg_last_error()   # ADAPTSEG_ERR_WORKSPACE
+    assert K.conv_kernel_id(K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,)), 4, 64, 128, 0, copies=True)[0] == 88
+    # ... but a product that kernel does not cover (Cin 48: a 32-deep step would cross a tap)
+    # needs the fp32 input
+    d48 = K._desc(K.ConvGeom(48, 64, 3, 3, 1, (1,), (1,)), 4, 64, 128, K.nhwc_strides(4, 64, 128, 48))[0]
+    st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d48), None, ctypes.c_void_p(256), w, None, None, None,
                                  ctypes.c_void_p(512), None, 0, None, 0, None)
     assert st == 1 and b"fp32 input" in L.adaptseg_last_error()
     st = L.adaptseg_conv2d_fwd_x(ctypes.byref(d), None, None, w, None, None, None, ctypes.c_void_p(512), None, 0, None,

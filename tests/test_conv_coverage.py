@@ -48,8 +48,11 @@ def test_every_step_conv_variant_is_oracle_checked(config):
         # fp32 kernels, which the fp32 cases cover under bf16 math as well
         for c in CONV_CASES + LARGE_CASES:
             covered |= case_products(K, c, K.MATH_BF16)
-    else:   # the fp32 cases run under both fp32 conv maths (tests/test_ops_gpu.py::conv_math)
+    else:   # the fp32 cases run under the three fp32 conv maths (tests/test_ops_gpu.py::conv_math);
+        # F32X3_PRESPLIT runs the term-image kernel (conv_x3r.hpp) the F32X3 step uses on the
+        # Bottleneck products' operand copies
         for c in CONV_CASES + LARGE_CASES:
-            covered |= case_products(K, c, K.MATH_F32) | case_products(K, c, K.MATH_F32X3)
+            covered |= (case_products(K, c, K.MATH_F32) | case_products(K, c, K.MATH_F32X3) |
+                        case_products(K, c, K.MATH_F32X3_PRESPLIT))
     missing = sorted(prods - covered)
     assert not missing, f"{config}: step conv products without an fp64 parity case: {missing}"

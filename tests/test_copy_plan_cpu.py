@@ -75,8 +75,9 @@ def test_skip_decisions_match_across_geometries_but_the_kernel_variants_do_not()
 def test_copy_operand_only_matches_the_lds_dma_selectors():
     """adaptseg_conv2d_copy_operand_only (what engine.bf16_only asks) is exactly the set of
     products the planner puts on the LDS-DMA kernels (selectors 100*op + 94 / 97-99, 192 / 193)
-    or the register-staged bf16 forward (90-93), for every conv geometry of the c5 step; and it
-    is never true under the fp32 conv maths."""
+    or the register-staged bf16 forward (90-93), for every conv geometry of the c5 step; under
+    F32X3 it is exactly the set the term-image kernel takes when the copies are passed
+    (selectors 100*op + 88 / 89, conv_x3r.hpp); under the fp32-input MFMA math never."""
     import bench
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
@@ -84,9 +85,9 @@ def test_copy_operand_only_matches_the_lds_dma_selectors():
     geoms = []
     orig = K.conv_kernel_id
 
-    def spy(g, n, h, w, op, strides=None):
+    def spy(g, n, h, w, op, strides=None, copies=False):
         geoms.append((g, n, h, w, op, strides))
-        return orig(g, n, h, w, op, strides)
+        return orig(g, n, h, w, op, strides, copies=copies)
 
     prev = K.get_conv_math()
     K.conv_kernel_id = spy
@@ -111,6 +112,14 @@ def test_copy_operand_only_matches_the_lds_dma_selectors():
             seen.add(lds_dma)
         assert seen == {True, False}
         K.set_conv_math(K.MATH_F32X3)
+        seen = set()
+        for g, n, h, w, op, st in geoms:
+            kid, _ = K.conv_kernel_id(g, n, h, w, op, st, copies=True)
+            x3r = kid % 100 in (88, 89)
+            assert K.conv_copy_operand_only(g, n, h, w, op, st) == x3r, (g, n, h, w, op, kid)
+            seen.add(x3r)
+        assert seen == {True, False}
+        K.set_conv_math(K.MATH_F32)
         for g, n, h, w, op, st in geoms[:200]:
             assert not K.conv_copy_operand_only(g, n, h, w, op, st)
     finally:
