@@ -59,20 +59,34 @@ __device__ __forceinline__ float4 lda4(const __bf16 *p) {
 __device__ __forceinline__ float lda1(const float *p) { return *p; }
 __device__ __forceinline__ float lda1(const __bf16 *p) { return (float)*p; }
 
-// Under the F32X3 conv maths the operand copies are three exact bf16 term images [3][rows][C]
-// (common.hpp split3), `timg` elements apart: the residual and the saved output (the ReLU mask
-// source) of a BN may then be stored as terms only, read back exactly (join3).  X3 tags that
-// storage; its pointer is term 0.
+// Under the F32X3 conv maths an operand copy holds the three bf16 terms of each fp32 value
+// (common.hpp split3), pixel-interleaved: [rows][3][C] (x3_off) — a row's three term rows are
+// adjacent, so a pass that writes or reads them streams one region.  The residual and the
+// saved output (the ReLU mask source) of a BN may then be stored as terms only, read back as
+// hi + mid + lo (join3).  X3 tags that storage; its pointer is the copy's base.
 struct X3 {};
 template <typename T> struct Act { typedef const T *ptr; };
 template <> struct Act<X3> { typedef const __bf16 *ptr; };
+__device__ __forceinline__ int64_t x3_off(int64_t row, int c, int C) { return row * 3 * C + c; }
 template <typename T>
-__device__ __forceinline__ float4 ldr4(typename Act<T>::ptr p, int64_t e, int64_t timg) {
+__device__ __forceinline__ float4 ldr4(typename Act<T>::ptr p, int64_t row, int c, int C) {
+  if constexpr (std::is_same<T, X3>::value) {
+    const __bf16 *q = p + x3_off(row, c, C);
+    return join3(*reinterpret_cast<const uint2 *>(q), *reinterpret_cast<const uint2 *>(q + C),
+                 *reinterpret_cast<const uint2 *>(q + 2 * C));
+  } else {
+    return lda4(p + row * C + c);
+  }
+}
+// The ReLU / LeakyReLU mask source: only its sign is used.  From terms the hi term alone has it:
+// hi = RNE_bf16(v) is nonzero with v's sign unless |v| < 2^-134, and then mid and lo round to
+// zero as well, so the stored value (hi + mid + lo) is 0 too — hi > 0 <=> stored value > 0.
+template <typename T>
+__device__ __forceinline__ float4 ldm4(typename Act<T>::ptr p, int64_t row, int c, int C) {
   if constexpr (std::is_same<T, X3>::value)
-    return join3(*reinterpret_cast<const uint2 *>(p + e), *reinterpret_cast<const uint2 *>(p + e + timg),
-                 *reinterpret_cast<const uint2 *>(p + e + 2 * timg));
+    return lda4(p + x3_off(row, c, C));
   else
-    return lda4(p + e);
+    return lda4(p + row * C + c);
 }
 
 constexpr int kReduceUnroll = 4;
@@ -94,7 +108,7 @@ __global__ void __launch_bounds__(256)
 bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
                  typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
-                 int64_t rows_per_split, float *__restrict__ partial, int64_t timg = 0) {
+                 int64_t rows_per_split, float *__restrict__ partial) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc;   // channel quad within block
   const int rl = threadIdx.x / tc;   // row lane
@@ -122,11 +136,11 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const fl
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t ru = r + (int64_t)u * tr;
-        const int64_t e = (ru < r1 ? ru : r) * C + c0;
+        const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
         v[u] = lda4(x + e);
         if (MODE == 1) {
           g[u] = *reinterpret_cast<const float4 *>(dy + e);
-          if (relu == 1 || relu == 3) o[u] = ldr4<TY>(y, e, timg);
+          if (relu == 1 || relu == 3) o[u] = ldm4<TY>(y, row, c0, C);
         }
       }
 #pragma unroll
@@ -281,17 +295,18 @@ __device__ __forceinline__ uint2 bf16x4_rne(float4 v) {
   return __builtin_bit_cast(uint2, __builtin_convertvector(f, b4v));
 }
 
-// The operand copy of four outputs at uint2 index k: one bf16 RNE image (img4 == 0, BF16 maths)
-// or the three exact term images, img4 uint2 apart (F32X3 maths)
-__device__ __forceinline__ void store_copy(uint2 *yb, int64_t k, float4 o, int64_t img4) {
-  if (img4) {
+// The operand copy of the four outputs (row, c .. c+3): one bf16 RNE image [rows][C] (BF16
+// maths) or their three terms in the pixel-interleaved [rows][3][C] copy (terms, F32X3 maths)
+__device__ __forceinline__ void store_copy(uint2 *yb, int64_t row, int c, int C, float4 o, bool terms) {
+  if (terms) {
     uint2 h, m, l;
     split3(o, h, m, l);
+    const int64_t k = x3_off(row, c, C) >> 2;
     yb[k] = h;
-    yb[k + img4] = m;
-    yb[k + 2 * img4] = l;
+    yb[k + (C >> 2)] = m;
+    yb[k + (C >> 1)] = l;
   } else {
-    yb[k] = bf16x4_rne(o);
+    yb[(row * C + c) >> 2] = bf16x4_rne(o);
   }
 }
 
@@ -300,15 +315,16 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
                                       typename Act<TR>::ptr __restrict__ res, float *__restrict__ y, uint2 *yb, int relu,
-                                      int64_t timg = 0, int64_t yimg4 = 0) {
+                                      bool terms = false) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
+    const int64_t row = i * 4 / C;
     float4 v = lda4(x + 4 * i);
     float o[4] = {v.x, v.y, v.z, v.w};
     float r4[4] = {0, 0, 0, 0};
     if (res) {
-      float4 r = ldr4<TR>(res, 4 * i, timg);
+      float4 r = ldr4<TR>(res, row, c, C);
       r4[0] = r.x; r4[1] = r.y; r4[2] = r.z; r4[3] = r.w;
     }
 #pragma unroll
@@ -318,7 +334,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
       o[j] = fwd_act(t, relu);
     }
     if (y) reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
-    if (yb) store_copy(yb, i, make_float4(o[0], o[1], o[2], o[3]), yimg4);
+    if (yb) store_copy(yb, row, c, C, make_float4(o[0], o[1], o[2], o[3]), terms);
   }
 }
 
@@ -336,7 +352,7 @@ template <typename TX, typename TR = TX>
 __global__ void __launch_bounds__(256)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
-                  typename Act<TR>::ptr res, float *y, uint2 *yb, int act, int64_t timg = 0, int64_t yimg4 = 0) {
+                  typename Act<TR>::ptr res, float *y, uint2 *yb, int act, bool terms = false) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -351,9 +367,9 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
     for (int u = 0; u < kApplyUnroll; ++u) {
       const int64_t ru = r + (int64_t)u * tr;
       const bool ok = ru < r1;
-      const int64_t e = (ok ? ru : r) * C + c0;
+      const int64_t row = ok ? ru : r, e = row * C + c0;
       v[u] = lda4(x + e);
-      q[u] = res ? ldr4<TR>(res, e, timg) : make_float4(0, 0, 0, 0);
+      q[u] = res ? ldr4<TR>(res, row, c0, C) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -365,7 +381,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
       o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
       o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
       if (y) st4(y + ru * C + c0, o);
-      if (yb) store_copy(yb, (ru * C + c0) >> 2, o, yimg4);
+      if (yb) store_copy(yb, ru, c0, C, o, terms);
     }
   }
 }
@@ -375,8 +391,7 @@ __global__ void __launch_bounds__(256)
 bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, typename Act<TY>::ptr y,
                       const TX *x, const float *__restrict__ w, const float *__restrict__ b,
                       const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,
-                      float *dx, uint2 *dxb, float *dres, int rmode, int train, int64_t timg = 0,
-                      int64_t dimg4 = 0) {
+                      float *dx, uint2 *dxb, float *dres, int rmode, int train, bool terms = false) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4;
@@ -394,10 +409,10 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
       const int64_t ru = r + (int64_t)u * tr;
-      const int64_t e = (ru < r1 ? ru : r) * C + c0;
+      const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
       g[u] = ld4c(dy + e);
       v[u] = train ? lda4(x + e) : z4;
-      o4[u] = need_y ? ldr4<TY>(y, e, timg) : z4;
+      o4[u] = need_y ? ldm4<TY>(y, row, c0, C) : z4;
     }
 #pragma unroll
     for (int u = 0; u < kApplyUnroll; ++u) {
@@ -432,7 +447,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
         out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
       }
       if (dx) st4(dx + e, out);
-      if (dxb) store_copy(dxb, e >> 2, out, dimg4);
+      if (dxb) store_copy(dxb, ru, c0, C, out, terms);
     }
   }
 }
@@ -503,8 +518,8 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y,
   int slot;
   const double eb = sizeof(TX);   // bytes per activation element (x)
   const bool terms = std::is_same<TY, X3>::value;   // y stored as F32X3 term images
-  const double ebt = terms ? 6.0 : eb;               // ... bytes per element of y
-  const int64_t timg = rows * c, dimg4 = copies_are_terms() && dx_bf16 ? rows * c / 4 : 0;
+  const double ebt = terms ? 2.0 : eb;               // ... bytes per element of y (terms: the hi term, ldm4)
+  const bool dterms = copies_are_terms() && dx_bf16;
   if (train) {
     size_t need = bn_ws_bytes(rows, c);
     if (!ws || ws_bytes < need) {
@@ -518,7 +533,7 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y,
     timing_begin(kTBnReduceBwd, s, (4.0 + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c, &slot);
     bn_reduce_kernel<1, TX, TY><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
                                                                          save_invstd, weight, bias, rmode, r.per,
-                                                                         partial, timg);
+                                                                         partial);
     timing_end(slot, s);
     AS_CHECK_LAUNCH("bn_reduce<bwd>");
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
@@ -529,12 +544,12 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y,
   timing_begin(kTBnBwdApply, s,
                (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * (train ? 1 : 0) +
                 ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
-                   (dx_bf16 ? (dimg4 ? 6.0 : 2.0) * rows * c : 0.0),
+                   (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0),
                &slot);
   const ApplyPlan ap = apply_plan(rows, c);
   bn_bwd_apply2d_kernel<TX, TY><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
       rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
-      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, timg, dimg4);
+      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_bwd_apply");
   return ADAPTSEG_OK;
@@ -581,19 +596,19 @@ static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_
                          const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu, hipStream_t s) {
   const ApplyPlan ap = apply_plan(rows, c);
   const dim3 g(ap.cblocks, ap.rsplits);
-  const int64_t timg = rows * c, yimg4 = copies_are_terms() && y_bf16 ? rows * c / 4 : 0;
+  const bool terms = copies_are_terms() && y_bf16;
   uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
   if (x && rb)
     bn_apply2d_kernel<float, X3><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, rb, y, yb,
-                                                   relu, timg, yimg4);
+                                                   relu, terms);
   else if (x)
     bn_apply2d_kernel<float, float><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, res, y,
-                                                      yb, relu, timg, yimg4);
+                                                      yb, relu, terms);
   else
     bn_apply2d_kernel<__bf16, __bf16><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
                                                         reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
-                                                        weight, bias, rb, y, yb, relu, timg, yimg4);
+                                                        weight, bias, rb, y, yb, relu, terms);
 }
 
 int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
@@ -689,19 +704,20 @@ int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t 
   int st = check_fwd_storage("bn_fwd_infer", x, x_bf16, res, res_bf16, y, y_bf16);
   if (st) return st;
   hipStream_t s = as_stream(stream);
-  const int64_t total4 = rows * c / 4, timg = rows * c, yimg4 = copies_are_terms() && y_bf16 ? total4 : 0;
+  const int64_t total4 = rows * c / 4;
+  const bool terms = copies_are_terms() && y_bf16;
   uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
   if (x && rb)
     bn_infer_apply_kernel<float, X3><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
-                                                                      weight, bias, rb, y, yb, relu, timg, yimg4);
+                                                                      weight, bias, rb, y, yb, relu, terms);
   else if (x)
     bn_infer_apply_kernel<float, float><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
-                                                                         weight, bias, res, y, yb, relu, timg, yimg4);
+                                                                         weight, bias, res, y, yb, relu, terms);
   else
     bn_infer_apply_kernel<__bf16, __bf16><<<grid_for(total4), 256, 0, s>>>(
         total4, c, reinterpret_cast<const __bf16 *>(x_bf16), running_mean, running_var, eps, weight, bias, rb, y, yb,
-        relu, timg, yimg4);
+        relu, terms);
   AS_CHECK_LAUNCH("bn_infer_apply");
   return ADAPTSEG_OK;
 }

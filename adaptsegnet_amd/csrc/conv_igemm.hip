@@ -500,8 +500,6 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     if (op == ADAPTSEG_CONV_FWD) pl.x3 = d->c % kX3BK == 0;
     else if (op == ADAPTSEG_CONV_BWD_DATA) pl.x3 = d->k % kX3BK == 0;
     else pl.x3 = true;
-    // pre-split operand images by LDS-DMA (conv_x3g.hpp): 16-B chunks of both weight-gradient
-    // operands (Cin, Cout multiples of 8); every F32X3 forward / data gradient qualifies
     // 256x128 tiles with 32-deep steps on pre-split term images (conv_x3r.hpp): a 32-deep
     // step inside one tap; weight gradients in 16-B channel chunks of both operands
     if (pl.x3) {
@@ -510,12 +508,9 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       else pl.x3r_ok = d->c % 8 == 0 && d->k % 8 == 0;
       if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = d->k >= 256 ? 256 : 128;
     }
-    // F32X3_PRESPLIT: every such product on the pre-split kernels, term images made per call
-    // unless the caller supplies them; F32X3 (default): on x3r only when it does (x3_terms)
-    if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) {
-      pl.x3g = op != ADAPTSEG_CONV_BWD_WEIGHT || (d->c % 8 == 0 && d->k % 8 == 0);
-      pl.x3r = pl.x3r_ok;
-    }
+    // F32X3_PRESPLIT: every such product on the term-image kernel, the images made per call
+    // unless the caller supplies them; F32X3 (default): on it only when the caller does (x3_terms)
+    if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
@@ -560,7 +555,6 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 int kernel_id(const Plan &pl, int mode) {
   // 88 / 89: the FAST cfg-8 stride-2 ids, which never occur (cfg 8 has no stride-2 form)
   if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
-  if (pl.x3g) return 100 * mode + 86 + (pl.s2 ? 1 : 0);
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
@@ -684,25 +678,26 @@ __global__ void bf16_out_copy_kernel(const float *__restrict__ y, __bf16 *__rest
     yb[i] = (__bf16)y[i];
 }
 
-// F32X3 maths: the three exact term images [3][n] of a finished fp32 output
-__global__ void x3_out_copy_kernel(const float *__restrict__ y, __bf16 *__restrict__ yb, int64_t n) {
+// F32X3 maths: the pixel-interleaved term images [rows][3][C] of a finished fp32 output
+__global__ void x3_out_copy_kernel(const float *__restrict__ y, __bf16 *__restrict__ yb, int64_t n, int C) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t h, m, l;
     split3_2(y[i], 0.f, h, m, l);
-    yb[i] = __builtin_bit_cast(__bf16, (uint16_t)h);
-    yb[i + n] = __builtin_bit_cast(__bf16, (uint16_t)m);
-    yb[i + 2 * n] = __builtin_bit_cast(__bf16, (uint16_t)l);
+    const int64_t o = (i / C) * 3 * C + i % C;
+    yb[o] = __builtin_bit_cast(__bf16, (uint16_t)h);
+    yb[o + C] = __builtin_bit_cast(__bf16, (uint16_t)m);
+    yb[o + 2 * C] = __builtin_bit_cast(__bf16, (uint16_t)l);
   }
 }
 
-// The operand copy of a finished output (the paths whose kernels do not write it): a bf16 RNE
-// image, or the three term images under the F32X3 maths
-static int out_copy(const float *y, uint16_t *yb, int64_t n, hipStream_t s) {
+// The operand copy of a finished output [n / C][C] (the paths whose kernels do not write it): a
+// bf16 RNE image, or the three term images under the F32X3 maths
+static int out_copy(const float *y, uint16_t *yb, int64_t n, int C, hipStream_t s) {
   if (!yb || n == 0) return ADAPTSEG_OK;
   AS_CHECK_ARG(y, "conv: an operand copy needs the fp32 output on this path");
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n, 256), 8192);
   if (copies_are_terms())
-    x3_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n);
+    x3_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n, C);
   else
     bf16_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n);
   AS_CHECK_LAUNCH("out_copy");
@@ -876,10 +871,10 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   const int64_t ny = (int64_t)d->n * d->oh * d->ow * d->k;
   if (use_thin(d, ADAPTSEG_CONV_FWD) &&
       thin_fwd(d, x, w[0], bias ? bias[0] : nullptr, res, y, flags, as_stream(stream)) == ADAPTSEG_OK)
-    return out_copy(y, y_bf16, ny, as_stream(stream));
+    return out_copy(y, y_bf16, ny, d->k, as_stream(stream));
   if (tapgemm_eligible(d) && aligned16(x) && segs_aligned(w, d->nseg)) {
     st = tapgemm_fwd(d, x, x_bf16, w, bias, res, y, flags, ws, ws_bytes, as_stream(stream));
-    return st ? st : out_copy(y, y_bf16, ny, as_stream(stream));
+    return st ? st : out_copy(y, y_bf16, ny, d->k, as_stream(stream));
   }
   ConvParams &p = pl.p;
   p.x = x;
@@ -906,7 +901,7 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(y, y_bf16, ny, as_stream(stream));
+  return (st || !terms) ? st : out_copy(y, y_bf16, ny, d->k, as_stream(stream));
 }
 
 int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
@@ -991,7 +986,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(y, y_bf16, (int64_t)d->n * d->oh * d->ow * d->k, as_stream(stream));
+  return (st || !terms) ? st : out_copy(y, y_bf16, (int64_t)d->n * d->oh * d->ow * d->k, d->k, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
@@ -1018,11 +1013,11 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   const int64_t nx = (int64_t)d->n * d->h * d->w * d->c;
   if (use_thin(d, ADAPTSEG_CONV_BWD_DATA) &&
       thin_dgrad(d, dy, w[0], res, aux, dx, flags, as_stream(stream)) == ADAPTSEG_OK)
-    return out_copy(dx, dx_bf16, nx, as_stream(stream));
+    return out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
   if (tapgemm_eligible(d) && aligned16(dy) && aligned16(dx) && segs_aligned(w, d->nseg) &&
       (!res || aligned16(res)) && (!aux || aligned16(aux))) {
     st = tapgemm_bwd_data(d, dy, w, res, aux, dx, flags, ws, ws_bytes, as_stream(stream));
-    return st ? st : out_copy(dx, dx_bf16, nx, as_stream(stream));
+    return st ? st : out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
   }
   ConvParams &p = pl.p;
   p.dy = dy;
@@ -1046,7 +1041,7 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(dx, dx_bf16, nx, as_stream(stream));
+  return (st || !terms) ? st : out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,

@@ -1318,8 +1318,8 @@ struct Plan {
   bool s2;     // stride-2 data gradient by output-pixel parity class (grid.z = 4)
   bool bf16;   // bf16-MFMA path (conv_bf16.hpp): 128x{128,256}x64 tiles, packed bf16 weights
   bool x3;     // F32X3 path (conv_x3.hpp): fp32 via exact 3-term bf16 splits, 128x128x16 tiles
-  bool x3g;    // ... on pre-split operand images by LDS-DMA (conv_x3g.hpp), MATH_F32X3_PRESPLIT
-  bool x3r;    // ... the 256x128x32 one-block-per-CU form of x3g (conv_x3r.hpp); x3g is set too
+  bool x3g;    // ... on pre-split term images by LDS-DMA (the caller's or made per call); with x3r
+  bool x3r;    // ... the 256x128x32 one-block-per-CU term-image kernel (conv_x3r.hpp)
   int x3r_bm;  // its row tile (256; weight gradients with Cout < 256: 128)
   bool x3r_ok; // F32X3 product the x3r kernel covers (a 32-deep step inside one tap, 16-B chunks)
   bool x3ext;  // x3r on the caller's term images (F32X3 maths): no per-call split copies
@@ -1381,7 +1381,7 @@ hipError_t launch_bf16(const Plan &pl, void *ws, hipStream_t s);
 // F32X3 conv math: three-image weight-pack bytes and launcher (conv_launch_x3.hip)
 size_t x3_wpack_bytes(const Plan &pl);
 int plan_bm(const Plan &pl);
-size_t x3_pre_bytes(const Plan &pl);   // workspace ahead of the slabs: weight pack + x3g term images
+size_t x3_pre_bytes(const Plan &pl);   // workspace ahead of the slabs: weight pack + per-call term images
 hipError_t prep_x3(const Plan &pl, void *wpack, hipStream_t s);    // the weight pack (unless wpack_ext) + copies
 hipError_t prep_x3_wpack(const Plan &pl, void *pack, hipStream_t s);  // the weight pack alone
 hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s);  // the GEMM

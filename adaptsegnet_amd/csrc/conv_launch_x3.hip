@@ -1,4 +1,4 @@
-// Kernel instantiations and host launcher of the F32X3 conv math (conv_x3.hpp, conv_x3g.hpp):
+// Kernel instantiations and host launcher of the F32X3 conv math (conv_x3.hpp, conv_x3r.hpp):
 // fp32 convs on the bf16 MFMA through exact three-term bf16 splits.
 #include "conv_x3r.hpp"
 
@@ -23,8 +23,9 @@ size_t x3_wpack_bytes(const Plan &pl) {
   return 3 * (size_t)rows_pad * ktot * sizeof(__bf16);
 }
 
-// elements of ONE term image of the x3g kernel's activation operand (FWD: x, DGRAD / WGRAD:
-// dY) and, for the weight gradient, of x
+// elements of the x3r kernel's activation operand (FWD: x, DGRAD / WGRAD: dY) and, for the
+// weight gradient, of x: their term images (made per call when the caller supplies none) are
+// three times that many bf16
 size_t x3g_act_elems(const Plan &pl) {
   const ConvParams &p = pl.p;
   if (!pl.x3g) return 0;   // (x3ext: the caller's images have this size too, see launch_x3)
@@ -48,7 +49,7 @@ static void split_copy(const float *x, int n, int h, int w, int c, int sxn, int 
                        hipStream_t s) {
   const int64_t n8 = (int64_t)n * h * w * c / 8;
   x3_split_copy_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n8, 256), 8192), 256, 0, s>>>(
-      x, n, h, w, c / 8, sxn, sxh, sxw, reinterpret_cast<uint4 *>(out), n8);
+      x, n, h, w, c / 8, sxn, sxh, sxw, reinterpret_cast<uint4 *>(out));
 }
 
 hipError_t prep_x3_wpack(const Plan &pl, void *pack, hipStream_t s) {
@@ -85,30 +86,17 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
   const ConvParams &p = pl.p;
   const __bf16 *wb = reinterpret_cast<const __bf16 *>(pl.wpack_ext ? pl.wpack_ext : wpack);
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(x3_threads(pl.mode));
-  if (pl.x3g) {
+  if (pl.x3r) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(x3_wpack_bytes(pl));
     const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext) : reinterpret_cast<const __bf16 *>(base);
-    const uint32_t img = (uint32_t)x3g_act_elems(pl);
-    if (pl.x3r) {
-      if (pl.mode == MODE_FWD) igemm_x3r_kernel<MODE_FWD, false><<<grid, 512, 0, s>>>(p, act, img, wb);
-      else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3r_kernel<MODE_DGRAD, true><<<grid, 512, 0, s>>>(p, act, img, wb);
-      else if (pl.mode == MODE_DGRAD) igemm_x3r_kernel<MODE_DGRAD, false><<<grid, 512, 0, s>>>(p, act, img, wb);
-      else {
-        const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
-                                         : reinterpret_cast<const __bf16 *>(base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)));
-        const uint32_t img2 = (uint32_t)x3g_act2_elems(pl);
-        if (pl.x3r_bm == 256) igemm_x3r_wgrad_kernel<256><<<grid, 512, 0, s>>>(p, act, img, act2, img2);
-        else igemm_x3r_wgrad_kernel<128><<<grid, 512, 0, s>>>(p, act, img, act2, img2);
-      }
-      return hipGetLastError();
-    }
-    if (pl.mode == MODE_FWD) igemm_x3g_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, act, img, wb);
-    else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3g_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, act, img, wb);
-    else if (pl.mode == MODE_DGRAD) igemm_x3g_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, act, img, wb);
+    if (pl.mode == MODE_FWD) igemm_x3r_kernel<MODE_FWD, false><<<grid, 512, 0, s>>>(p, act, wb);
+    else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3r_kernel<MODE_DGRAD, true><<<grid, 512, 0, s>>>(p, act, wb);
+    else if (pl.mode == MODE_DGRAD) igemm_x3r_kernel<MODE_DGRAD, false><<<grid, 512, 0, s>>>(p, act, wb);
     else {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)));
-      igemm_x3g_wgrad_kernel<<<grid, block, 0, s>>>(p, act, img, act2, (uint32_t)x3g_act2_elems(pl));
+      if (pl.x3r_bm == 256) igemm_x3r_wgrad_kernel<256><<<grid, 512, 0, s>>>(p, act, act2);
+      else igemm_x3r_wgrad_kernel<128><<<grid, 512, 0, s>>>(p, act, act2);
     }
     return hipGetLastError();
   }

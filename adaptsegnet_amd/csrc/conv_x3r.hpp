@@ -1,11 +1,11 @@
 // F32X3 convolution on 256x128 tiles with 32-deep K steps, fed by LDS-DMA from pre-split
 // operands ("x3r").
 //
-// Same arithmetic as igemm_x3_kernel / igemm_x3g_kernel (conv_x3.hpp, conv_x3g.hpp): every fp32
+// Same arithmetic as igemm_x3_kernel (conv_x3.hpp): every fp32
 // operand is three exact bf16 terms (hi + mid + lo), six products a0b0, a0b1, a1b0, a0b2, a1b1,
 // a2b0 per 16-deep K sub-step, a0b0 in one accumulator and the five cross terms in a second one,
-// summed once in the epilogue — so the results are bitwise those of the other two F32X3
-// kernels (same products, same per-accumulator k order).  What changes is the schedule:
+// summed once in the epilogue — so the results are bitwise those of the register-staged kernel
+// wherever neither splits K (same products, same per-accumulator k order).  The schedule differs:
 //
 //   * igemm_x3_kernel (128x128x16, 16 waves per CU) meets a barrier every 12 MFMAs per wave and
 //     splits its activation operand in-kernel (weight gradients: both operands);
@@ -18,28 +18,48 @@
 //     ring of 72 KB: step kt+1 is issued right after the barrier that opens step kt and has the
 //     whole of step kt's MFMAs (~3,000 cycles per SIMD) to land.
 //
+// Operand term images are pixel-interleaved, [n][h][w][3][C] (the BatchNorm passes write them so,
+// bn.hip x3_off): element (pixel, c) of term t at pixel * 3C + t * C + c.
 // FWD / DGRAD (K-contiguous): a stage holds, per term t, the A image [256 rows][32 k] (64-B rows,
 // conv_bf16g.hpp's g16_off<32> swizzle: conflict-free ds_read_b128 fragments) and, per 16-deep
 // sub-step s, the B image [128 rows][16 k] (kc16 layout, conv_x3.hpp).  A rows are gathered per
-// tap from the activation's term images [3][n][h][w][c], 16 rows x 64 B per LDS-DMA instruction
-// (four lanes per row; the swizzle goes on the source chunk); the 32-deep step stays inside one tap (C % 32 == 0 for the forward, Cout % 32
-// == 0 for the data gradient).  B is conv_wpack_x3v_kernel's pack, whose two consecutive 16-deep
+// tap from the activation's term images, 16 rows x 64 B per LDS-DMA instruction (four lanes per
+// row; the swizzle goes on the source chunk); the 32-deep step stays inside one tap (C % 32 == 0
+// for the forward, Cout % 32 == 0 for the data gradient).  B is conv_wpack_x3v_kernel's pack, whose two consecutive 16-deep
 // steps are 24 contiguous KB in exactly the stage's B byte order.
 // WGRAD (k = output pixel, both operands M/N-contiguous [32 k][128] images, conv_bf16.hpp's mc
 // layout read with ds_read_b64_tr_b16): dY rows contiguous, x columns per-lane gathers (each 16-B
 // chunk = 8 input channels of one tap: Cin % 8 == 0, Cout % 8 == 0).  BM 256 (Cout >= 256: dY
 // two images per term) or 128.
 #pragma once
-#include "conv_x3g.hpp"
+#include "conv_bf16g.hpp"
+#include "conv_x3.hpp"
 
 namespace adaptseg {
+
+// conv_x3.hpp's six products of one 16-deep step: a0*b0 into acc, the five cross terms into accs
+template <int TM, int TN>
+__device__ __forceinline__ void x3_products(const bf16x8 (&a)[3][TM], const bf16x8 (&b)[3][TN], floatx16 (&acc)[TM][TN],
+                                            floatx16 (&accs)[TM][TN]) {
+  constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
+  constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
+#pragma unroll
+  for (int u = 0; u < 6; ++u)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        else accs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[TA[u]][i], b[TB[u]][j], accs[i][j], 0, 0, 0);
+      }
+}
 
 constexpr int kX3rStages = 2;
 constexpr int x3r_stage_bytes(int bm) { return 3 * (bm + 128) * kX3rBK * 2; }   // 72 KB at BM 256
 
 template <int MODE, bool S2>
 __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, const __bf16 *__restrict__ a3,
-                                                           uint32_t aimg, const __bf16 *__restrict__ wb) {
+                                                           const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products");
   static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
   constexpr int BM = 256, BN = 128, BK = kX3rBK;
@@ -77,6 +97,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
   const int kt1 = min(nkt, kt0 + p.ktiles_per_split);
   const int ktot = p.ntaps * (MODE == MODE_FWD ? p.c : p.k);  // packed weight row length
   const int ca = MODE == MODE_FWD ? p.c : p.k;                 // channels of the activation images
+  const int ps = 3 * ca;                                       // pixel stride of its term images
 
   // A: wave w loads rows 32w .. 32w+31 of every A image (64-B rows of 32 k, g16_off<32>'s
   // swizzle), 16 rows per instruction: lane -> row 32w + 16h + lane/4, LDS slot lane&3, whose
@@ -95,7 +116,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       const int ii = t2 % Hc, b = t2 / Hc;
       a_y[h] = ii;
       a_x[h] = j;
-      a_pix[h] = ((b * p.oh + ii) * p.ow + j) * ca + chs;
+      a_pix[h] = ((b * p.oh + ii) * p.ow + j) * ps + chs;
     } else if constexpr (MODE == MODE_FWD) {
       uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
       const int ow = mm - (int)t * p.ow;
@@ -103,7 +124,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       const int oh = (int)t - (int)b * p.oh;
       a_y[h] = oh * p.stride;
       a_x[h] = ow * p.stride;
-      a_pix[h] = (((int)b * p.h + a_y[h]) * p.w + a_x[h]) * ca + chs;
+      a_pix[h] = (((int)b * p.h + a_y[h]) * p.w + a_x[h]) * ps + chs;
     } else {
       uint32_t t = fdiv((uint32_t)mm, p.fd_w);
       const int iw = mm - (int)t * p.w;
@@ -111,7 +132,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       const int ih = (int)t - (int)b * p.h;
       a_y[h] = ih;
       a_x[h] = iw;
-      a_pix[h] = (((int)b * p.oh + ih) * p.ow + iw) * ca + chs;
+      a_pix[h] = (((int)b * p.oh + ih) * p.ow + iw) * ps + chs;
     }
   }
   // B: the packed tiles of this column tile, [16-deep step][term][4 KB image]; two 16-deep steps
@@ -130,7 +151,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       seg_geom(p, sr, tap, seg, t, dy, dx);
       dy = uni(dy);
       dx = uni(dx);
-      soff = uni((dy * p.w + dx) * ca + kbase - tap * p.c);
+      soff = uni((dy * p.w + dx) * ps + kbase - tap * p.c);
       wkt = 2 * kt;
     } else if constexpr (S2) {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
@@ -139,7 +160,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       const int kh = kh0 + 2 * u, kw = kw0 + 2 * v;
       dy = uni((py + p.pad_[0] - kh) >> 1);
       dx = uni((px + p.pad_[0] - kw) >> 1);
-      soff = uni((dy * p.ow + dx) * ca + co0);
+      soff = uni((dy * p.ow + dx) * ps + co0);
       wkt = uni(((kh * p.kw_ + kw) * p.k + co0) / kX3BK);   // packed 16-deep step of (tap, co0)
     } else {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
@@ -147,7 +168,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
       seg_geom(p, sr, tap, seg, t, dy, dx);
       dy = uni(-dy);
       dx = uni(-dx);
-      soff = uni((dy * p.ow + dx) * ca + kbase - tap * p.k);
+      soff = uni((dy * p.ow + dx) * ps + kbase - tap * p.k);
       wkt = 2 * kt;
     }
     bool v[2];
@@ -164,7 +185,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
     for (int h = 0; h < 2; ++h) {
       const __bf16 *src = a3 + a_pix[h] + soff;
 #pragma unroll
-      for (int t = 0; t < 3; ++t) glds16(v[h] ? src + (size_t)t * aimg : zero, adst + t * IMGA + h * 1024);
+      for (int t = 0; t < 3; ++t) glds16(v[h] ? src + t * ca : zero, adst + t * IMGA + h * 1024);
     }
     const char *bsrc = wtile + (size_t)wkt * 3 * IMGB;
 #pragma unroll
@@ -227,8 +248,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
 // 64x64; BM 128 -> 2x4 of 64x32.
 template <int BM>
 __global__ void __launch_bounds__(512, 1) igemm_x3r_wgrad_kernel(const ConvParams p, const __bf16 *__restrict__ dy3,
-                                                                 uint32_t dyimg, const __bf16 *__restrict__ x3,
-                                                                 uint32_t ximg) {
+                                                                 const __bf16 *__restrict__ x3) {
   constexpr int BN = 128, BKP = kX3rBK, IMG = BKP * 256;
   constexpr int NA = BM / 128;                                    // dY images per term
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
@@ -275,14 +295,14 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_wgrad_kernel(const ConvParam
     const int oh = (int)qq - (int)b * p.oh;
     const int iy = oh * p.stride + tdy, ix = ow * p.stride + tdx;
     const bool bv = rv & b_col & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
-    const __bf16 *asrc = dy3 + (size_t)mm * p.k + bm + chs;
-    const __bf16 *bsrc = x3 + (((int)b * p.h + iy) * p.w + ix) * p.c + ci;
+    const __bf16 *asrc = dy3 + (size_t)mm * 3 * p.k + bm + chs;
+    const __bf16 *bsrc = x3 + (size_t)(((int)b * p.h + iy) * p.w + ix) * 3 * p.c + ci;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
 #pragma unroll
       for (int i = 0; i < NA; ++i)
-        glds16((rv & a_col[i]) ? asrc + (size_t)q * dyimg + 128 * i : zero, sbase + (q * (NA + 1) + i) * IMG);
-      glds16(bv ? bsrc + (size_t)q * ximg : zero, sbase + (q * (NA + 1) + NA) * IMG);
+        glds16((rv & a_col[i]) ? asrc + q * p.k + 128 * i : zero, sbase + (q * (NA + 1) + i) * IMG);
+      glds16(bv ? bsrc + q * p.c : zero, sbase + (q * (NA + 1) + NA) * IMG);
     }
   };
 
@@ -331,6 +351,30 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_wgrad_kernel(const ConvParam
     for (int j = 0; j < TN; ++j) acc[i][j] += accs[i][j];
   igemm_epilogue<MODE_WGRAD, BM, BN, WAVES_M, WAVES_N, false>(p, acc, bm, bn, tm, tn, split, p.M, p.h, p.w, 0, 0,
                                                               reinterpret_cast<float *>(lds));
+}
+
+// fp32 NHWC (pixel strides sxn / sxh / sxw, unit channel stride) -> its pixel-interleaved term
+// images [n][h][w][3][c], 8 channels per thread: the operand copy of the x3r kernels when the
+// caller supplied none (F32X3_PRESPLIT).
+__global__ void __launch_bounds__(256) x3_split_copy_kernel(const float *__restrict__ x, int n, int h, int w, int c8,
+                                                            int sxn, int sxh, int sxw, uint4 *__restrict__ out) {
+  const int64_t total = (int64_t)n * h * w * c8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cq = (int)(i % c8);
+    const int64_t pix = i / c8;
+    const int xx = (int)(pix % w);
+    const int64_t t = pix / w;
+    const int yy = (int)(t % h), b = (int)(t / h);
+    const float *src = x + (int64_t)b * sxn + (int64_t)yy * sxh + (int64_t)xx * sxw + 8 * cq;
+    const float4 v0 = ld4(src), v1 = ld4(src + 4);
+    uint2 h0, m0, l0, h1, m1, l1;
+    split3(v0, h0, m0, l0);
+    split3(v1, h1, m1, l1);
+    uint4 *o = out + pix * 3 * c8 + cq;
+    o[0] = make_uint4(h0.x, h0.y, h1.x, h1.y);
+    o[c8] = make_uint4(m0.x, m0.y, m1.x, m1.y);
+    o[2 * c8] = make_uint4(l0.x, l0.y, l1.x, l1.y);
+  }
 }
 
 }  // namespace adaptseg

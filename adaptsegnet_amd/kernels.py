@@ -262,15 +262,16 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w
 # BatchNorm (x as [rows, C])
 # ---------------------------------------------------------------------------------------
 def copies_are_terms() -> bool:
-    """Under the F32X3 maths an operand copy is the three exact bf16 term images of an fp32
-    tensor, [3, *shape] (adaptseg.h: the _x forms' copies); under BF16 one bf16 (RNE) image."""
+    """Under the F32X3 maths an operand copy holds the three bf16 terms of an fp32 tensor
+    [..., C], pixel-interleaved as [..., 3, C] (adaptseg.h: the _x forms' copies); under BF16 it
+    is one bf16 (RNE) image of the same shape."""
     return _ops._CONV_MATH[0] in (MATH_F32X3, MATH_F32X3_PRESPLIT)
 
 
 def _bf16_like(t, want):
     if not want:
         return None
-    shape = ((3,) if copies_are_terms() else ()) + tuple(t.shape)
+    shape = tuple(t.shape[:-1]) + ((3,) if copies_are_terms() else ()) + (t.shape[-1],)
     return torch.empty(shape, device=t.device, dtype=torch.bfloat16)
 
 

@@ -166,7 +166,7 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
 
 def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
-    if sel % 100 in (86, 87, 88, 89, 95, 96):
+    if sel % 100 in (88, 89, 95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
     if sel % 100 >= 90:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
@@ -181,8 +181,6 @@ def selector_symbol(sel):
         if op == 2:
             return f"igemm_x3r_wgrad_kernel<{256 if var == 8 else 128}>"
         return f"igemm_x3r_kernel<{op}, {'true' if var == 9 else 'false'}>"
-    if sel % 100 in (86, 87):   # F32X3 on pre-split operand images by LDS-DMA (conv_x3g.hpp)
-        return "igemm_x3g_wgrad_kernel" if op == 2 else f"igemm_x3g_kernel<{op}, {'true' if var == 7 else 'false'}>"
     if sel % 100 in (92, 93) and op == 1:   # bf16 LDS-DMA stride-2 data gradient (parity classes)
         bm, bn = (128, 256) if var == 2 else (256, 128)
         return f"igemm_bf16g_kernel<1, {bm}, {bn}, 32, true>"

@@ -32,7 +32,7 @@ def test_default_conv_math_selects_f32x3():
     per-element products keep their fp32 kernels.  F32X3_PRESPLIT moves the products whose
     operands come in 16-B chunks to the LDS-DMA kernels on pre-split images: 256x128x32 tiles
     (conv_x3r.hpp, 100*op + 88, + 89 for the stride-2 parity path / 128-row weight gradients)
-    where a 32-deep step stays inside one tap, else 128x128x16 (conv_x3g.hpp, 100*op + 86 / 87);
+    where a 32-deep step stays inside one tap (else the staged kernel);
     the stem's channel-padded weight gradient (Cin 4) stays on the staged one."""
     from adaptsegnet_amd import kernels as K
     assert K.get_conv_math() == K.MATH_F32X3
@@ -52,7 +52,7 @@ def test_default_conv_math_selects_f32x3():
         g128 = K.ConvGeom(64, 128, 3, 3, 1, (1,), (1,))
         assert K.conv_kernel_id(g128, 4, 64, 128, 2)[0] == 289   # Cout < 256: 128-row tiles
         g16 = K.ConvGeom(48, 64, 3, 3, 1, (1,), (1,))
-        assert [K.conv_kernel_id(g16, 4, 64, 128, op)[0] for op in (0, 1)] == [86, 188]
+        assert [K.conv_kernel_id(g16, 4, 64, 128, op)[0] for op in (0, 1)] == [95, 188]
         assert K.conv_kernel_id(stem4, 4, 512, 1024, 2, (4 * 512 * 1024, 1, 4 * 1024, 4))[0] == 295
     finally:
         K.set_conv_math(K.MATH_F32X3)

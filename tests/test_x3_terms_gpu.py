@@ -1,8 +1,9 @@
 """F32X3 operand copies: the three exact bf16 term images of an fp32 activation.
 
 Under the default F32X3 conv math the BatchNorm passes that produce conv operands write, beside
-(or instead of) the fp32 tensor, its three term images [3, *shape] (hi + mid + lo == v exactly,
-each the RNE bf16 of what is left: common.hpp split3), and the Bottleneck convs read them through
+(or instead of) the fp32 tensor, its three bf16 terms, pixel-interleaved [..., 3, C] (hi + mid +
+lo == v exactly for |v| >= 2^-126, each the RNE bf16 of what is left: common.hpp split3), and the
+Bottleneck convs read them through
 the 256x128x32 LDS-DMA kernel (conv_x3r.hpp, selectors 100*op + 88 / 89) instead of splitting
 fp32 rows in-kernel (conv_x3.hpp).  Checked here:
   * the BN passes write exactly torch's RNE split, and read terms (residual, ReLU-mask source)
@@ -27,16 +28,17 @@ def K():
 
 
 def terms(t):
-    """torch's exact three-term RNE split of an fp32 tensor -> [3, *shape] bf16."""
+    """torch's three-term RNE split of an fp32 tensor [..., C] -> its pixel-interleaved copy
+    [..., 3, C] bf16 (bn.hip x3_off)."""
     hi = t.to(torch.bfloat16)
     r = t - hi.float()
     mid = r.to(torch.bfloat16)
     lo = (r - mid.float()).to(torch.bfloat16)
-    return torch.stack([hi, mid, lo])
+    return torch.stack([hi, mid, lo], dim=-2)
 
 
 def join(tb):
-    return (tb[0].float() + tb[1].float()) + tb[2].float()
+    return (tb[..., 0, :].float() + tb[..., 1, :].float()) + tb[..., 2, :].float()
 
 
 def rel(a, b):
@@ -75,7 +77,7 @@ def test_bn_forward_writes_and_reads_exact_terms(relu):
     # fp32 residual, fp32 output + its terms
     y, mean, invstd, yb = k.bn_fwd_train(x, w, b, rm.clone(), rv.clone(), 0.1, 1e-5, res=res, relu=bool(relu),
                                          bf16_out=True)
-    assert yb.shape == (3, rows, c) and yb.dtype == torch.bfloat16
+    assert yb.shape == (rows, 3, c) and yb.dtype == torch.bfloat16
     assert torch.equal(yb, terms(y)) and torch.equal(join(yb), y)
     # the residual as terms only: bitwise the same output
     y2, _, _, yb2 = k.bn_fwd_train(x, w, b, rm.clone(), rv.clone(), 0.1, 1e-5, res=terms(res),
@@ -97,7 +99,7 @@ def test_bn_backward_reads_mask_terms_and_writes_dx_terms():
     y, mean, invstd = k.bn_fwd_train(x, w, b, None, None, 0.1, 1e-5, res=res, relu=True)
     dy = torch.randn(rows, c, generator=g).to(DEV)
     dx, dxb = k.bn_bwd(dy, y, x, w, mean, invstd, relu=True, dres=None, bias=b, bf16_out=True)
-    assert dxb.shape == (3, rows, c) and torch.equal(dxb, terms(dx))
+    assert dxb.shape == (rows, 3, c) and torch.equal(dxb, terms(dx))
     dx2, dxb2 = k.bn_bwd(dy, terms(y), x, w, mean, invstd, relu=True, bias=b, bf16_out=True)
     assert torch.equal(dx2, dx) and torch.equal(dxb2, dxb)
     # eval mode: mask from the saved output's terms
