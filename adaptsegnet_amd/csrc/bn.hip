@@ -90,6 +90,16 @@ __device__ __forceinline__ float4 ldm4(typename Act<T>::ptr p, int64_t row, int 
 }
 
 constexpr int kReduceUnroll = 4;
+// The BN passes run beside the weight-gradient GEMMs of the side stream.  A term-image F32X3
+// block (conv_x3r.hpp: 8 waves at ~200 VGPRs, one per CU) leaves 96 VGPRs per SIMD free, so
+// under the F32X3_PRESPLIT program the BN blocks fit beside it only at <= 96 VGPRs
+// (ADAPTSEG_BN_MIN_BLOCKS=5 with ADAPTSEG_BN_APPLY_UNROLL=2: 26.79 vs 26.50 images/s there).
+// The default program (register-staged F32X3 convs) runs faster with the x4-unrolled passes at
+// their natural ~126 VGPRs: 27.44 vs 27.18 images/s (profiles/r3/x3_copies_ab.txt).
+#ifndef ADAPTSEG_BN_MIN_BLOCKS
+#define ADAPTSEG_BN_MIN_BLOCKS 1
+#endif
+constexpr int kBnMinBlocks = ADAPTSEG_BN_MIN_BLOCKS;
 // ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
 // GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
 constexpr int kReduceBlocks = 512, kApplyBlocks = 512;
@@ -104,7 +114,7 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
 // Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
 // Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
 template <int MODE, typename TX, typename TY = TX>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
                  typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
@@ -342,14 +352,17 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
 // loads its channels' parameters once and walks rows (no per-element channel modulo); rows
 // are unrolled x4 with all loads issued before any store (dx / dres / y may alias dy / x:
 // every element is still read before it is written, by the same thread).
-constexpr int kApplyUnroll = 4;
+#ifndef ADAPTSEG_BN_APPLY_UNROLL
+#define ADAPTSEG_BN_APPLY_UNROLL 4
+#endif
+constexpr int kApplyUnroll = ADAPTSEG_BN_APPLY_UNROLL;
 
 
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
 template <typename TX, typename TR = TX>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
                   typename Act<TR>::ptr res, float *y, uint2 *yb, int act, bool terms = false) {
@@ -387,7 +400,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
 }
 
 template <typename TX, typename TY = TX>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, typename Act<TY>::ptr y,
                       const TX *x, const float *__restrict__ w, const float *__restrict__ b,
                       const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,

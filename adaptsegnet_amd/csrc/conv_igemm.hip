@@ -334,10 +334,11 @@ int plan_bm(const Plan &pl) {
 }
 
 // F32X3 maths with the caller's term images of the activation operand(s) (the _x forms'
-// copies: three exact bf16 images [3][n][h][w][c]): the product moves to the x3r kernel, which
-// reads them by LDS-DMA instead of splitting fp32 rows in-kernel.  Re-plans the grid.
+// copies: the three bf16 terms, pixel-interleaved [n][h][w][3][c]): the product moves to the x3r
+// kernel, which reads them by LDS-DMA instead of splitting fp32 rows in-kernel (F32X3_PRESPLIT:
+// it is there already; it then skips its per-call copy).  Re-plans the grid.
 static void x3_terms(Plan &pl) {
-  if (conv_math() != ADAPTSEG_MATH_F32X3 || !pl.fast || !pl.x3 || !pl.x3r_ok || !pl.act_ext) return;
+  if (!copies_are_terms() || !pl.fast || !pl.x3 || !pl.x3r_ok || !pl.act_ext) return;
   if (pl.mode == MODE_WGRAD && !pl.act_ext2) return;
   pl.x3g = pl.x3r = pl.x3ext = true;
   set_splits(pl);
@@ -383,7 +384,15 @@ void set_splits(Plan &pl) {
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
   constexpr int kG16WgradTarget = 256;
-  const int target = (pl.mode == MODE_WGRAD && (pl.g16 || pl.x3r)) ? kG16WgradTarget
+  // The term-image F32X3 weight gradient (one 8-wave block per CU, side stream): its blocks hold
+  // their CUs against the main stream's term-image convs (neither fits beside the other), so
+  // more, shorter blocks let the main chain in sooner.
+#ifndef ADAPTSEG_X3R_WGRAD_TARGET
+#define ADAPTSEG_X3R_WGRAD_TARGET 256
+#endif
+  constexpr int kX3rWgradTarget = ADAPTSEG_X3R_WGRAD_TARGET;
+  const int target = (pl.mode == MODE_WGRAD && pl.x3r) ? kX3rWgradTarget
+                     : (pl.mode == MODE_WGRAD && pl.g16) ? kG16WgradTarget
                      : (pl.mode == MODE_WGRAD && pl.x3)            ? kX3WgradTarget
                                                                    : kSplitTarget;
   // the LDS-DMA bf16 / x3r kernels run one block per CU: split only grids under half the CUs
@@ -713,7 +722,7 @@ bool use_thin(const adaptseg_conv_desc *d, int op) { return thin_eligible(d, op)
 static bool copy_only(const Plan &pl, const adaptseg_conv_desc *d, int op) {
   if (use_thin(d, op)) return false;
   if (tapgemm_eligible(d)) return tapgemm_copy_only(d, op);
-  if (conv_math() == ADAPTSEG_MATH_F32X3) return pl.fast && pl.x3 && pl.x3r_ok;   // x3r on the caller's terms
+  if (copies_are_terms()) return pl.fast && pl.x3 && pl.x3r_ok;   // x3r on the caller's terms
   return pl.g16 || (pl.bf16 && op == ADAPTSEG_CONV_FWD);
 }
 
@@ -753,7 +762,7 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
     set_splits(g);
     b = std::max(b, g.slab_bytes);
   }
-  if (pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3) {   // the plan with the caller's term images
+  if (pl.x3r_ok && copies_are_terms()) {   // the plan with the caller's term images
     Plan t = pl;
     t.x3g = t.x3r = t.x3ext = true;
     set_splits(t);

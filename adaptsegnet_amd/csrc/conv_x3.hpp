@@ -58,11 +58,14 @@ __device__ __forceinline__ bf16x8 kc16_frag(const char *img, int r0, int lane) {
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16 zero bytes: the source of every operand float4 outside the image (padding taps, rows past
+// M / K), so the staged values need no mask before they are split and stored
+static __device__ __attribute__((aligned(16))) float g_x3_zero4[4];
 // the exact three-term split (rne2 / split3_2 / split3) lives in common.hpp: the BatchNorm
 // passes that write F32X3 term images use the same arithmetic
 
 template <int MODE, bool S2>
-__global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+__global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
   constexpr bool MC = MODE == MODE_WGRAD;   // both operands M/N-contiguous (k = output pixel)
   constexpr int BM = 128, BN = 128, BK = kX3BK, NT = x3_threads(MODE);
   constexpr int WAVES_M = 2, WAVES_N = NT / 128;        // 2x2 (WGRAD) or 2x4 waves
@@ -161,7 +164,30 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
   float4 ra[NQ];           // A: one float4 per slot
   float4 rbf[MC ? NQ : 1]; // MC: B float4 per slot
   BChunk rbh[MC ? 1 : 3];  // K-contiguous B: this thread's BPT bytes of each packed term image
-  bool ma[NQ], mb[NQ];
+  const float *zero4 = g_x3_zero4;
+
+  // WGRAD: this thread's output pixel m = 16 kt + krow0 walks forward one K step at a time, its
+  // (image, row, column) and element offsets advanced incrementally instead of two divisions and
+  // a 3-term address per step (the weight gradient splits both operands in-kernel: its VALU,
+  // not its MFMA, sets its pace — profiles/r2/pmc/x3_l3conv2_counters.txt)
+  int w_kt = kt0;          // the K step the walk stands at (first load: kt0)
+  int w_pos = 0;           // (output row << 16) | output column of this thread's pixel
+  int w_tap = 0;           // (tap row offset << 16) + tap column offset of this thread's x column
+  int w_dy = 0, w_x = 0;   // element offsets of this thread's dY and x float4s (column included)
+  const int w_dcol = p.stride * p.sxw;                     // x offset per output column
+  const int w_drow = p.stride * p.sxh - p.ow * w_dcol;     // ... at a row wrap
+  const int w_dimg = p.sxn - p.oh * p.stride * p.sxh;      // ... at an image wrap
+  if constexpr (MC) {
+    w_tap = b_dy[0] * 65536 + b_dx[0];
+    const int m = kt0 * BK + (tid >> 5);
+    uint32_t t = fdiv((uint32_t)m, p.fd_ow);
+    const int ow = m - (int)t * p.ow;
+    uint32_t b = fdiv(t, p.fd_oh);
+    const int oh = (int)t - (int)b * p.oh;
+    w_pos = (oh << 16) | ow;
+    w_dy = m * p.k + a_pix[0];
+    w_x = (int)b * p.sxn + oh * p.stride * p.sxh + ow * w_dcol + b_dy[0] * p.sxh + b_dx[0] * p.sxw + b_off[0];
+  }
 
   auto load_tile = [&](int kt) {
     const int kbase = kt * BK;
@@ -175,8 +201,7 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const bool v = a_ok[i] && (unsigned)(a_y[i] + dy) < (unsigned)p.h && (unsigned)(a_x[i] + dx) < (unsigned)p.w;
-        ma[i] = v;
-        ra[i] = ld4(p.x + (v ? a_pix[i] + soff : 0));
+        ra[i] = ld4(v ? p.x + a_pix[i] + soff : zero4);
       }
 #pragma unroll
       for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const BChunk *>(wtile + (size_t)(kt * 3 + s) * IMGB);
@@ -201,46 +226,50 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const bool v = a_ok[i] && (unsigned)(a_y[i] - dy) < (unsigned)p.oh && (unsigned)(a_x[i] - dx) < (unsigned)p.ow;
-        ma[i] = v;
-        ra[i] = ld4(p.dy + (v ? a_pix[i] + soff : 0));
+        ra[i] = ld4(v ? p.dy + a_pix[i] + soff : zero4);
       }
       const int wkt = wk / BK;
 #pragma unroll
       for (int s = 0; s < 3; ++s) rbh[s] = *reinterpret_cast<const BChunk *>(wtile + (size_t)(wkt * 3 + s) * IMGB);
     } else {  // WGRAD: k = output pixel
-      const int krow0 = tid >> 5;
-#pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        const int m = kbase + krow0 + (NT / 32) * i;
-        const bool rv = m < K;
-        ma[i] = rv && a_ok[i];
-        ra[i] = ld4(p.dy + (size_t)(rv ? m : 0) * p.k + a_pix[i]);
-        const int mm = min(m, K - 1);
-        uint32_t t = fdiv((uint32_t)mm, p.fd_ow);
-        const int ow = mm - (int)t * p.ow;
-        uint32_t b = fdiv(t, p.fd_oh);
-        const int oh = (int)t - (int)b * p.oh;
-        const int iy = oh * p.stride + b_dy[i], ix = ow * p.stride + b_dx[i];
-        const bool v = b_ok[i] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
-        mb[i] = v;
-        rbf[i] = ld4(p.x + (v ? (int)b * p.sxn + iy * p.sxh + ix * p.sxw + b_off[i] : 0));
+      static_assert(NQ == 1 && NT == 512, "one slot: k-row tid / 32 of a 16-deep step");
+      if (kt != w_kt) {   // kt == w_kt + 1 (kt == w_kt: the re-read of the last step, T14 order below)
+        {                 // 16 pixels on (images are < 2^15 pixels wide and high)
+          w_dy += BK * p.k;
+          w_pos += BK;
+          w_x += BK * w_dcol;
+          while ((w_pos & 0xffff) >= p.ow) {
+            w_pos += (1 << 16) - p.ow;
+            w_x += w_drow;
+            if ((w_pos >> 16) == p.oh) {   // next image: row 0, same column
+              w_pos &= 0xffff;
+              w_x += w_dimg;
+            }
+          }
+        }
+        w_kt = kt;
       }
+      const bool rv = kbase + (tid >> 5) < K;
+      ra[0] = ld4(rv && a_ok[0] ? p.dy + w_dy : zero4);
+      const int iy = (w_pos >> 16) * p.stride + ((w_tap + 32768) >> 16);
+      const int ix = (w_pos & 0xffff) * p.stride + (int)(short)(w_tap & 0xffff);
+      const bool v = b_ok[0] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+      rbf[0] = ld4(v ? p.x + w_x : zero4);
     }
   };
 
   auto store_tile = [&](int buf) {
     char *As = lds + buf * STAGE;
     char *Bs = As + 3 * IMG;
-    const uint2 z2 = make_uint2(0, 0);
     if constexpr (!MC) {
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const int o = kc16_off((tid >> 2) + 64 * i, sj >> 1) + 8 * (sj & 1);
         uint2 h, m, l;
         split3(ra[i], h, m, l);
-        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? h : z2;
-        *reinterpret_cast<uint2 *>(As + IMG + o) = ma[i] ? m : z2;
-        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
+        *reinterpret_cast<uint2 *>(As + o) = h;
+        *reinterpret_cast<uint2 *>(As + IMG + o) = m;
+        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = l;
       }
 #pragma unroll
       for (int s = 0; s < 3; ++s) *reinterpret_cast<BChunk *>(Bs + s * IMGB + BPT * tid) = rbh[s];
@@ -252,13 +281,13 @@ __global__ void __launch_bounds__(x3_threads(MODE), 2) igemm_x3_kernel(const Con
         const int o = mc_off(kr, col >> 3) + 8 * ((col >> 2) & 1);
         uint2 h, m, l;
         split3(ra[i], h, m, l);
-        *reinterpret_cast<uint2 *>(As + o) = ma[i] ? h : z2;
-        *reinterpret_cast<uint2 *>(As + IMG + o) = ma[i] ? m : z2;
-        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = ma[i] ? l : z2;
+        *reinterpret_cast<uint2 *>(As + o) = h;
+        *reinterpret_cast<uint2 *>(As + IMG + o) = m;
+        *reinterpret_cast<uint2 *>(As + 2 * IMG + o) = l;
         split3(rbf[i], h, m, l);
-        *reinterpret_cast<uint2 *>(Bs + o) = mb[i] ? h : z2;
-        *reinterpret_cast<uint2 *>(Bs + IMGB + o) = mb[i] ? m : z2;
-        *reinterpret_cast<uint2 *>(Bs + 2 * IMGB + o) = mb[i] ? l : z2;
+        *reinterpret_cast<uint2 *>(Bs + o) = h;
+        *reinterpret_cast<uint2 *>(Bs + IMGB + o) = m;
+        *reinterpret_cast<uint2 *>(Bs + 2 * IMGB + o) = l;
       }
     }
   };

@@ -81,11 +81,15 @@ def bf16_operands() -> bool:
       * BF16 math (config c5): a bf16 copy, which the bf16 LDS-DMA kernels read instead of
         converting the operand themselves.  The generator's activations are also STORED in bf16
         (lowp_storage), as torch.autocast(bfloat16) does.
-      * F32X3 math (c2-c4): the operand's three exact bf16 term images [3, *shape]
+      * F32X3_PRESPLIT math: the operand's three bf16 terms, pixel-interleaved [..., 3, C]
         (kernels.copies_are_terms), which the 256x128x32 F32X3 kernel (conv_x3r.hpp) reads by
         LDS-DMA instead of splitting fp32 rows in-kernel — the same products, bitwise the same
-        results.  Conv outputs stay fp32 (the BN passes read them)."""
-    return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE, K.MATH_F32X3)
+        results where neither splits K.  Conv outputs stay fp32 (the BN passes read them).  Not
+        the default for c2-c4 (F32X3): the term-image kernels are 13 % faster per conv in
+        isolation, but one of their blocks fills a CU, so the weight-gradient stream and the
+        main chain no longer share CUs, and the BN passes move 6-byte copies — the step measured
+        2.4 % slower (profiles/r3/x3_copies_ab.txt)."""
+    return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE, K.MATH_F32X3_PRESPLIT)
 
 
 def lowp_storage() -> bool:

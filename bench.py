@@ -294,7 +294,7 @@ def main():
                     help="c2 (default, BASELINE metric at N=1), c3 multi-level, c4 DeeplabVGG, "
                          "c5 multi-level LS bf16 batch 4")
     ap.add_argument("--batch", type=int, default=None, help="override batch per GPU")
-    ap.add_argument("--conv-math", default="f32x3", choices=("f32x3", "f32"),
+    ap.add_argument("--conv-math", default="f32x3", choices=("f32x3", "f32x3_presplit", "f32"),
                     help="conv arithmetic of the fp32 configs: f32x3 (default, fp32-accurate on the "
                          "bf16 MFMA) or f32 (the fp32-input MFMA kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -322,7 +322,8 @@ def main():
 
     level, gan, batch, src_wh, tgt_wh, gen, math = CONFIGS[args.config]
     conv_math = "bf16" if math == "bf16" else args.conv_math
-    K.set_conv_math({"bf16": K.MATH_BF16, "f32x3": K.MATH_F32X3, "f32": K.MATH_F32}[conv_math])
+    K.set_conv_math({"bf16": K.MATH_BF16, "f32x3": K.MATH_F32X3, "f32x3_presplit": K.MATH_F32X3_PRESPLIT,
+                     "f32": K.MATH_F32}[conv_math])
     if args.batch:
         batch = args.batch
     torch.manual_seed(1338 + rank)

@@ -58,11 +58,18 @@ def w_cl(w):
     return w.permute(0, 2, 3, 1).contiguous().float().to(DEV)
 
 
-def test_default_math_is_f32x3_with_term_copies():
+def test_engine_writes_term_copies_only_under_presplit():
+    """F32X3 (default): the engine passes no copies (register-staged kernels); F32X3_PRESPLIT:
+    the BN passes write term copies and the Bottleneck convs read them."""
     k = K()
-    assert k.get_conv_math() == k.MATH_F32X3 and k.copies_are_terms()
     from adaptsegnet_amd import engine
-    assert engine.bf16_operands() and not engine.lowp_storage()
+    assert k.get_conv_math() == k.MATH_F32X3 and k.copies_are_terms()
+    assert not engine.bf16_operands() and not engine.lowp_storage()
+    k.set_conv_math(k.MATH_F32X3_PRESPLIT)
+    try:
+        assert engine.bf16_operands() and not engine.lowp_storage()
+    finally:
+        k.set_conv_math(k.MATH_F32X3)
 
 
 @pytest.mark.parametrize("relu", [0, 1])
