@@ -520,6 +520,21 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // F32X3_PRESPLIT: every such product on the term-image kernel, the images made per call
     // unless the caller supplies them; F32X3 (default): on it only when the caller does (x3_terms)
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
+#ifndef ADAPTSEG_X3R_WGRAD_TAPS
+#define ADAPTSEG_X3R_WGRAD_TAPS 0
+#endif
+    // F32X3 (default) multi-tap weight gradients on the 128-row term-image kernel, the images
+    // made per call on the side stream: 9 taps amortise the copies (a 1x1 weight gradient's
+    // copies cost more than the kernel saves), and a 96 KB / <=128-VGPR block leaves room on
+    // its CU for one register-staged main-stream block (the 256-row one does not).  Off: the
+    // step is bound by the main stream's chain, which this leaves as is — same box, c2 26.75 /
+    // 26.74 img/s off vs 26.38 / 26.32 on (target 384: 26.25 / 26.22), c3 17.18 / 17.18 vs
+    // 16.88 / 16.91 (profiles/r3/x3r_wgrad_taps_ab.txt)
+    if (ADAPTSEG_X3R_WGRAD_TAPS && pl.x3 && op == ADAPTSEG_CONV_BWD_WEIGHT && pl.x3r_ok &&
+        d->kh * d->kw > 1 && conv_math() == ADAPTSEG_MATH_F32X3) {
+      pl.x3g = pl.x3r = true;
+      pl.x3r_bm = 128;
+    }
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
