@@ -10,7 +10,9 @@
 // HBM-bound.
 #include "common.hpp"
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
+#include <initializer_list>
 #include <type_traits>
 
 namespace adaptseg {
@@ -89,7 +91,65 @@ __device__ __forceinline__ float4 ldm4(typename Act<T>::ptr p, int64_t row, int 
     return lda4(p + row * C + c);
 }
 
+// A thread owns QN channel quads (4*QN consecutive channels) of a row: QN = 1 for fp32
+// storage, 2 for bf16 storage (one 16-B load of 8 bf16 — at one quad per thread the bf16 passes
+// issue as many memory instructions as the fp32 ones for half the bytes, and measured no faster
+// per launch: l3.bn3 apply 74 us bf16 vs 69 us fp32, tools/bn_bench.py)
+__device__ __forceinline__ float4 bf4(unsigned a, unsigned b) {
+  return make_float4(__uint_as_float(a << 16), __uint_as_float(a & 0xffff0000u), __uint_as_float(b << 16),
+                     __uint_as_float(b & 0xffff0000u));
+}
+template <int QN> __device__ __forceinline__ void ldq(const float *p, float4 (&o)[QN]) {
+#pragma unroll
+  for (int h = 0; h < QN; ++h) o[h] = *reinterpret_cast<const float4 *>(p + 4 * h);
+}
+template <int QN> __device__ __forceinline__ void ldq(const __bf16 *p, float4 (&o)[QN]) {
+  if constexpr (QN == 2) {
+    const uint4 u = *reinterpret_cast<const uint4 *>(p);
+    o[0] = bf4(u.x, u.y);
+    o[1] = bf4(u.z, u.w);
+  } else {
+#pragma unroll
+    for (int h = 0; h < QN; ++h) o[h] = lda4(p + 4 * h);
+  }
+}
+// the residual (TR) / the mask source y (TY) of a row: plain storage or F32X3 term images
+template <typename T, int QN>
+__device__ __forceinline__ void ldrq(typename Act<T>::ptr p, int64_t row, int c, int C, float4 (&o)[QN]) {
+  if constexpr (std::is_same<T, X3>::value) {
+#pragma unroll
+    for (int h = 0; h < QN; ++h) o[h] = ldr4<X3>(p, row, c + 4 * h, C);
+  } else {
+    ldq<QN>(p + row * C + c, o);
+  }
+}
+template <typename T, int QN>
+__device__ __forceinline__ void ldmq(typename Act<T>::ptr p, int64_t row, int c, int C, float4 (&o)[QN]) {
+  if constexpr (std::is_same<T, X3>::value) {
+#pragma unroll
+    for (int h = 0; h < QN; ++h) o[h] = ldm4<X3>(p, row, c + 4 * h, C);
+  } else {
+    ldq<QN>(p + row * C + c, o);
+  }
+}
+template <int QN> __device__ __forceinline__ void zq(float4 (&o)[QN]) {
+#pragma unroll
+  for (int h = 0; h < QN; ++h) o[h] = make_float4(0, 0, 0, 0);
+}
+template <int QN> __device__ __forceinline__ void ldpq(const float *p, int c, float4 (&o)[QN], float dflt) {
+#pragma unroll
+  for (int h = 0; h < QN; ++h)
+    o[h] = p ? *reinterpret_cast<const float4 *>(p + c + 4 * h) : make_float4(dflt, dflt, dflt, dflt);
+}
+
 constexpr int kReduceUnroll = 4;
+// rows in flight per thread of the bf16-storage passes (two quads a row): 2 rows at <= 128
+// VGPRs beat 4 rows at ~200 (c5 40.90 / 40.95 vs 40.57 / 40.63 images/s, one quad x 4 rows
+// 38.06 / 38.21; experiments/ab_bn_bf16.sh)
+#ifndef ADAPTSEG_BN_BF16_ROWS
+#define ADAPTSEG_BN_BF16_ROWS 2
+#endif
+constexpr int kBf16Rows = ADAPTSEG_BN_BF16_ROWS;
 // The BN passes run beside the weight-gradient GEMMs of the side stream.  A term-image F32X3
 // block (conv_x3r.hpp: 8 waves at ~200 VGPRs, one per CU) leaves 96 VGPRs per SIMD free, so
 // under the F32X3_PRESPLIT program the BN blocks fit beside it only at <= 96 VGPRs
@@ -111,81 +171,96 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
   return v;
 }
 
-// Block = 256 threads laid out as TC channel-quads x TR row lanes (TC*TR = 256).
-// Grid = (ceil(C / (4*TC)), splits).  Partial sums land in ws[split][2][C] (float).
-template <int MODE, typename TX, typename TY = TX>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
+// Block = 256 threads laid out as TC channel groups (QN quads each) x TR row lanes (TC*TR =
+// 256).  Grid = (ceil(C / (4*QN*TC)), splits).  Partial sums land in ws[2][C][splits] (float).
+template <int MODE, typename TX, typename TY = TX, int QN = 1>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
 __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
                  typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
                  int64_t rows_per_split, float *__restrict__ partial) {
   const int tr = 256 / tc;
-  const int cq = threadIdx.x % tc;   // channel quad within block
+  const int cq = threadIdx.x % tc;   // channel group within block
   const int rl = threadIdx.x / tc;   // row lane
-  const int c0 = (blockIdx.x * tc + cq) * 4;
+  const int c0 = (blockIdx.x * tc + cq) * 4 * QN;
   const bool cok = c0 < C;
   const int64_t r0 = blockIdx.y * rows_per_split;
   const int64_t r1 = min(rows, r0 + rows_per_split);
-  float4 s1 = make_float4(0, 0, 0, 0), s2 = make_float4(0, 0, 0, 0);
-  float4 piv = make_float4(0, 0, 0, 0);
-  float4 is = make_float4(0, 0, 0, 0), ww = is, bb = is;
+  float4 s1[QN], s2[QN], piv[QN], is[QN], ww[QN], bb[QN];
+  zq<QN>(s1);
+  zq<QN>(s2);
+  zq<QN>(is);
+  zq<QN>(ww);
+  zq<QN>(bb);
   if (cok) {
-    if (MODE == 0) piv = lda4(x + c0);
-    else piv = *reinterpret_cast<const float4 *>(mean + c0);
+    if (MODE == 0) ldq<QN>(x + c0, piv);
+    else ldpq<QN>(mean, c0, piv, 0.f);
     if (MODE == 1 && (relu == 2 || relu == 4)) {
-      is = *reinterpret_cast<const float4 *>(invstd + c0);
-      ww = w ? *reinterpret_cast<const float4 *>(w + c0) : make_float4(1, 1, 1, 1);
-      bb = b ? *reinterpret_cast<const float4 *>(b + c0) : make_float4(0, 0, 0, 0);
+      ldpq<QN>(invstd, c0, is, 0.f);
+      ldpq<QN>(w, c0, ww, 1.f);
+      ldpq<QN>(b, c0, bb, 0.f);
     }
-    // rows unrolled x kReduceUnroll with every load issued before any use (memory-level
-    // parallelism: one float4 per tensor in flight per thread measured 3-4 TB/s); tail rows
-    // re-read row r and are masked out of the sums
-    constexpr int U = kReduceUnroll;
+    // rows unrolled with every load issued before any use (memory-level parallelism: one
+    // float4 per tensor in flight per thread measured 3-4 TB/s); tail rows re-read row r and
+    // are masked out of the sums
+    constexpr int U = QN == 2 ? kBf16Rows : kReduceUnroll;
     for (int64_t r = r0 + rl; r < r1; r += U * tr) {
-      float4 v[U], g[U], o[U];
+      float4 v[U][QN], g[U][QN], o[U][QN];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t ru = r + (int64_t)u * tr;
         const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
-        v[u] = lda4(x + e);
+        ldq<QN>(x + e, v[u]);
         if (MODE == 1) {
-          g[u] = *reinterpret_cast<const float4 *>(dy + e);
-          if (relu == 1 || relu == 3) o[u] = ldm4<TY>(y, row, c0, C);
+          ldq<QN>(dy + e, g[u]);
+          if (relu == 1 || relu == 3) ldmq<TY, QN>(y, row, c0, C, o[u]);
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (r + (int64_t)u * tr >= r1) break;
-        const float4 d = make_float4(v[u].x - piv.x, v[u].y - piv.y, v[u].z - piv.z, v[u].w - piv.w);
-        if (MODE == 0) {
-          s1.x += d.x; s1.y += d.y; s1.z += d.z; s1.w += d.w;
-          s2.x += d.x * d.x; s2.y += d.y * d.y; s2.z += d.z * d.z; s2.w += d.w * d.w;
-        } else {
-          float4 gg = g[u];
-          if (relu == 2) gg = relu_mask_from_x(gg, v[u], piv, is, ww, bb);
-          else if (relu) gg = act_mask_o(gg, relu, o[u], v[u], piv, is, ww, bb);
-          s1.x += gg.x; s1.y += gg.y; s1.z += gg.z; s1.w += gg.w;
-          s2.x += gg.x * d.x; s2.y += gg.y * d.y; s2.z += gg.z * d.z; s2.w += gg.w * d.w;
+#pragma unroll
+        for (int h = 0; h < QN; ++h) {
+          const float4 vv = v[u][h], pv = piv[h];
+          const float4 d = make_float4(vv.x - pv.x, vv.y - pv.y, vv.z - pv.z, vv.w - pv.w);
+          float4 &a1 = s1[h], &a2 = s2[h];
+          if (MODE == 0) {
+            a1.x += d.x; a1.y += d.y; a1.z += d.z; a1.w += d.w;
+            a2.x += d.x * d.x; a2.y += d.y * d.y; a2.z += d.z * d.z; a2.w += d.w * d.w;
+          } else {
+            float4 gg = g[u][h];
+            if (relu == 2) gg = relu_mask_from_x(gg, vv, pv, is[h], ww[h], bb[h]);
+            else if (relu) gg = act_mask_o(gg, relu, o[u][h], vv, pv, is[h], ww[h], bb[h]);
+            a1.x += gg.x; a1.y += gg.y; a1.z += gg.z; a1.w += gg.w;
+            a2.x += gg.x * d.x; a2.y += gg.y * d.y; a2.z += gg.z * d.z; a2.w += gg.w * d.w;
+          }
         }
       }
     }
   }
-  __shared__ float4 red1[256], red2[256];
-  red1[threadIdx.x] = s1;
-  red2[threadIdx.x] = s2;
+  __shared__ float4 red1[QN][256], red2[QN][256];
+#pragma unroll
+  for (int h = 0; h < QN; ++h) {
+    red1[h][threadIdx.x] = s1[h];
+    red2[h][threadIdx.x] = s2[h];
+  }
   __syncthreads();
   if (rl == 0 && cok) {
-    float4 a = red1[threadIdx.x], b = red2[threadIdx.x];
-    for (int i = 1; i < tr; ++i) {
-      float4 u = red1[threadIdx.x + i * tc], v = red2[threadIdx.x + i * tc];
-      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
-    }
-    // transposed [2][C][splits]: a channel's partials are contiguous for the finalize wave
     const size_t S = gridDim.y, sp = blockIdx.y;
-    float *p1 = partial + (size_t)c0 * S + sp, *p2 = partial + ((size_t)C + c0) * S + sp;
-    p1[0] = a.x; p1[S] = a.y; p1[2 * S] = a.z; p1[3 * S] = a.w;
-    p2[0] = b.x; p2[S] = b.y; p2[2 * S] = b.z; p2[3 * S] = b.w;
+#pragma unroll
+    for (int h = 0; h < QN; ++h) {
+      float4 a = red1[h][threadIdx.x], b2 = red2[h][threadIdx.x];
+      for (int i = 1; i < tr; ++i) {
+        float4 u = red1[h][threadIdx.x + i * tc], v = red2[h][threadIdx.x + i * tc];
+        a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+        b2.x += v.x; b2.y += v.y; b2.z += v.z; b2.w += v.w;
+      }
+      // transposed [2][C][splits]: a channel's partials are contiguous for the finalize wave
+      const int c = c0 + 4 * h;
+      float *p1 = partial + (size_t)c * S + sp, *p2 = partial + ((size_t)C + c) * S + sp;
+      p1[0] = a.x; p1[S] = a.y; p1[2 * S] = a.z; p1[3 * S] = a.w;
+      p2[0] = b2.x; p2[S] = b2.y; p2[2 * S] = b2.z; p2[3 * S] = b2.w;
+    }
   }
 }
 
@@ -357,110 +432,208 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
 #endif
 constexpr int kApplyUnroll = ADAPTSEG_BN_APPLY_UNROLL;
 
-
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
 
-template <typename TX, typename TR = TX>
+template <int QN> __device__ __forceinline__ void stq(float *p, const float4 (&v)[QN]) {
+#pragma unroll
+  for (int h = 0; h < QN; ++h) st4(p + 4 * h, v[h]);
+}
+// the operand copy of a thread's 4*QN outputs of a row: one 16-B store of eight bf16 (QN 2) or
+// store_copy per quad (bf16 image or F32X3 term images)
+template <int QN>
+__device__ __forceinline__ void store_copyq(uint2 *yb, int64_t row, int c, int C, const float4 (&o)[QN], bool terms) {
+  if constexpr (QN == 2) {
+    if (!terms) {
+      const uint2 lo = bf16x4_rne(o[0]), hi = bf16x4_rne(o[1]);
+      *reinterpret_cast<uint4 *>(yb + ((row * C + c) >> 2)) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      return;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < QN; ++h) store_copy(yb, row, c + 4 * h, C, o[h], terms);
+}
+
+template <typename TX, int QN> constexpr int apply_rows() { return QN == 2 ? kBf16Rows : kApplyUnroll; }
+
+template <typename TX, typename TR = TX, int QN = 1>
 __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
                   typename Act<TR>::ptr res, float *y, uint2 *yb, int act, bool terms = false) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
-  const int c0 = (blockIdx.x * tc + cq) * 4;
+  const int c0 = (blockIdx.x * tc + cq) * 4 * QN;
   if (c0 >= C) return;
   const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
-  const float4 m = ld4c(mean + c0), is = ld4c(invstd + c0);
-  const float4 ww = w ? ld4c(w + c0) : make_float4(1, 1, 1, 1);
-  const float4 bb = b ? ld4c(b + c0) : make_float4(0, 0, 0, 0);
-  for (int64_t r = r0 + rl; r < r1; r += kApplyUnroll * tr) {
-    float4 v[kApplyUnroll], q[kApplyUnroll];
+  float4 m[QN], is[QN], ww[QN], bb[QN];
+  ldpq<QN>(mean, c0, m, 0.f);
+  ldpq<QN>(invstd, c0, is, 0.f);
+  ldpq<QN>(w, c0, ww, 1.f);
+  ldpq<QN>(b, c0, bb, 0.f);
+  constexpr int U = apply_rows<TX, QN>();
+  for (int64_t r = r0 + rl; r < r1; r += U * tr) {
+    float4 v[U][QN], q[U][QN];
 #pragma unroll
-    for (int u = 0; u < kApplyUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t ru = r + (int64_t)u * tr;
       const bool ok = ru < r1;
       const int64_t row = ok ? ru : r, e = row * C + c0;
-      v[u] = lda4(x + e);
-      q[u] = res ? ldr4<TR>(res, row, c0, C) : make_float4(0, 0, 0, 0);
+      ldq<QN>(x + e, v[u]);
+      if (res) ldrq<TR, QN>(res, row, c0, C, q[u]);
+      else zq<QN>(q[u]);
     }
 #pragma unroll
-    for (int u = 0; u < kApplyUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t ru = r + (int64_t)u * tr;
       if (ru >= r1) break;
-      float4 o;
-      o.x = fwd_act(bn_affine(v[u].x, m.x, is.x, ww.x, bb.x) + q[u].x, act);
-      o.y = fwd_act(bn_affine(v[u].y, m.y, is.y, ww.y, bb.y) + q[u].y, act);
-      o.z = fwd_act(bn_affine(v[u].z, m.z, is.z, ww.z, bb.z) + q[u].z, act);
-      o.w = fwd_act(bn_affine(v[u].w, m.w, is.w, ww.w, bb.w) + q[u].w, act);
-      if (y) st4(y + ru * C + c0, o);
-      if (yb) store_copy(yb, ru, c0, C, o, terms);
+      float4 o[QN];
+#pragma unroll
+      for (int h = 0; h < QN; ++h) {
+        o[h].x = fwd_act(bn_affine(v[u][h].x, m[h].x, is[h].x, ww[h].x, bb[h].x) + q[u][h].x, act);
+        o[h].y = fwd_act(bn_affine(v[u][h].y, m[h].y, is[h].y, ww[h].y, bb[h].y) + q[u][h].y, act);
+        o[h].z = fwd_act(bn_affine(v[u][h].z, m[h].z, is[h].z, ww[h].z, bb[h].z) + q[u][h].z, act);
+        o[h].w = fwd_act(bn_affine(v[u][h].w, m[h].w, is[h].w, ww[h].w, bb[h].w) + q[u][h].w, act);
+      }
+      if (y) stq<QN>(y + ru * C + c0, o);
+      if (yb) store_copyq<QN>(yb, ru, c0, C, o, terms);
     }
   }
 }
 
-template <typename TX, typename TY = TX>
+template <typename TX, typename TY = TX, int QN = 1>
 __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, typename Act<TY>::ptr y,
                       const TX *x, const float *__restrict__ w, const float *__restrict__ b,
                       const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,
                       float *dx, uint2 *dxb, float *dres, int rmode, int train, bool terms = false) {
-  const int tr = 256 / tc;
-  const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
-  const int c0 = (blockIdx.x * tc + cq) * 4;
-  if (c0 >= C) return;
-  const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
-  const float4 z4 = make_float4(0, 0, 0, 0);
-  const float4 is = ld4c(invstd + c0);
-  const float4 ww = w ? ld4c(w + c0) : make_float4(1, 1, 1, 1);
-  const float4 m = train ? ld4c(mean + c0) : z4;
-  const float4 mg = train ? ld4c(coef + c0) : z4, mgx = train ? ld4c(coef + C + c0) : z4;
-  const float4 bb = ((rmode == 2 || rmode == 4) && b) ? ld4c(b + c0) : z4;
-  const bool need_y = rmode == 1 || rmode == 3;
-  for (int64_t r = r0 + rl; r < r1; r += kApplyUnroll * tr) {
-    float4 g[kApplyUnroll], v[kApplyUnroll], o4[kApplyUnroll];
+  if constexpr (QN == 1) {   // (the grouped body below takes 130 VGPRs here: 3 waves per SIMD)
+    const int tr = 256 / tc;
+    const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
+    const int c0 = (blockIdx.x * tc + cq) * 4;
+    if (c0 >= C) return;
+    const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    const float4 z4 = make_float4(0, 0, 0, 0);
+    const float4 is = ld4c(invstd + c0);
+    const float4 ww = w ? ld4c(w + c0) : make_float4(1, 1, 1, 1);
+    const float4 m = train ? ld4c(mean + c0) : z4;
+    const float4 mg = train ? ld4c(coef + c0) : z4, mgx = train ? ld4c(coef + C + c0) : z4;
+    const float4 bb = ((rmode == 2 || rmode == 4) && b) ? ld4c(b + c0) : z4;
+    const bool need_y = rmode == 1 || rmode == 3;
+    constexpr int U = apply_rows<TX, 1>();
+    for (int64_t r = r0 + rl; r < r1; r += U * tr) {
+      float4 g[U], v[U], o4[U];
 #pragma unroll
-    for (int u = 0; u < kApplyUnroll; ++u) {
-      const int64_t ru = r + (int64_t)u * tr;
-      const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
-      g[u] = ld4c(dy + e);
-      v[u] = train ? lda4(x + e) : z4;
-      o4[u] = need_y ? ldm4<TY>(y, row, c0, C) : z4;
-    }
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + (int64_t)u * tr;
+        const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
+        g[u] = ld4c(dy + e);
+        v[u] = train ? lda4(x + e) : z4;
+        o4[u] = need_y ? ldm4<TY>(y, row, c0, C) : z4;
+      }
 #pragma unroll
-    for (int u = 0; u < kApplyUnroll; ++u) {
-      const int64_t ru = r + (int64_t)u * tr;
-      if (ru >= r1) break;
-      const int64_t e = ru * C + c0;
-      float4 gg = g[u];
-      if (rmode) {
-        float4 o;
-        if (need_y) {
-          o = o4[u];
-        } else {
-          o.x = bn_affine(v[u].x, m.x, is.x, ww.x, bb.x);
-          o.y = bn_affine(v[u].y, m.y, is.y, ww.y, bb.y);
-          o.z = bn_affine(v[u].z, m.z, is.z, ww.z, bb.z);
-          o.w = bn_affine(v[u].w, m.w, is.w, ww.w, bb.w);
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + (int64_t)u * tr;
+        if (ru >= r1) break;
+        const int64_t e = ru * C + c0;
+        float4 gg = g[u];
+        if (rmode) {
+          float4 o;
+          if (need_y) {
+            o = o4[u];
+          } else {
+            o.x = bn_affine(v[u].x, m.x, is.x, ww.x, bb.x);
+            o.y = bn_affine(v[u].y, m.y, is.y, ww.y, bb.y);
+            o.z = bn_affine(v[u].z, m.z, is.z, ww.z, bb.z);
+            o.w = bn_affine(v[u].w, m.w, is.w, ww.w, bb.w);
+          }
+          const float k = rmode <= 2 ? 0.f : 0.2f;
+          gg.x = o.x > 0.f ? gg.x : k * gg.x;
+          gg.y = o.y > 0.f ? gg.y : k * gg.y;
+          gg.z = o.z > 0.f ? gg.z : k * gg.z;
+          gg.w = o.w > 0.f ? gg.w : k * gg.w;
         }
-        const float k = rmode <= 2 ? 0.f : 0.2f;
-        gg.x = o.x > 0.f ? gg.x : k * gg.x;
-        gg.y = o.y > 0.f ? gg.y : k * gg.y;
-        gg.z = o.z > 0.f ? gg.z : k * gg.z;
-        gg.w = o.w > 0.f ? gg.w : k * gg.w;
+        if (dres) st4(dres + e, gg);
+        float4 out;
+        if (train) {
+          out.x = ww.x * is.x * (gg.x - mg.x - (v[u].x - m.x) * is.x * mgx.x);
+          out.y = ww.y * is.y * (gg.y - mg.y - (v[u].y - m.y) * is.y * mgx.y);
+          out.z = ww.z * is.z * (gg.z - mg.z - (v[u].z - m.z) * is.z * mgx.z);
+          out.w = ww.w * is.w * (gg.w - mg.w - (v[u].w - m.w) * is.w * mgx.w);
+        } else {
+          out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
+        }
+        if (dx) st4(dx + e, out);
+        if (dxb) store_copy(dxb, ru, c0, C, out, terms);
       }
-      if (dres) st4(dres + e, gg);
-      float4 out;
-      if (train) {
-        out.x = ww.x * is.x * (gg.x - mg.x - (v[u].x - m.x) * is.x * mgx.x);
-        out.y = ww.y * is.y * (gg.y - mg.y - (v[u].y - m.y) * is.y * mgx.y);
-        out.z = ww.z * is.z * (gg.z - mg.z - (v[u].z - m.z) * is.z * mgx.z);
-        out.w = ww.w * is.w * (gg.w - mg.w - (v[u].w - m.w) * is.w * mgx.w);
-      } else {
-        out.x = gg.x * ww.x * is.x; out.y = gg.y * ww.y * is.y; out.z = gg.z * ww.z * is.z; out.w = gg.w * ww.w * is.w;
+    }
+  } else {
+    const int tr = 256 / tc;
+    const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
+    const int c0 = (blockIdx.x * tc + cq) * 4 * QN;
+    if (c0 >= C) return;
+    const int64_t r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    float4 is[QN], ww[QN], m[QN], mg[QN], mgx[QN], bb[QN];
+    ldpq<QN>(invstd, c0, is, 0.f);
+    ldpq<QN>(w, c0, ww, 1.f);
+    ldpq<QN>(train ? mean : nullptr, c0, m, 0.f);
+    ldpq<QN>(train ? coef : nullptr, c0, mg, 0.f);
+    ldpq<QN>(train ? coef + C : nullptr, c0, mgx, 0.f);
+    ldpq<QN>((rmode == 2 || rmode == 4) ? b : nullptr, c0, bb, 0.f);
+    const bool need_y = rmode == 1 || rmode == 3;
+    constexpr int U = apply_rows<TX, QN>();
+    for (int64_t r = r0 + rl; r < r1; r += U * tr) {
+      float4 g[U][QN], v[U][QN], o4[U][QN];
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + (int64_t)u * tr;
+        const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
+        ldq<QN>(dy + e, g[u]);
+        if (train) ldq<QN>(x + e, v[u]);
+        else zq<QN>(v[u]);
+        if (need_y) ldmq<TY, QN>(y, row, c0, C, o4[u]);
+        else zq<QN>(o4[u]);
       }
-      if (dx) st4(dx + e, out);
-      if (dxb) store_copy(dxb, ru, c0, C, out, terms);
+  #pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + (int64_t)u * tr;
+        if (ru >= r1) break;
+        const int64_t e = ru * C + c0;
+        float4 out[QN];
+  #pragma unroll
+        for (int h = 0; h < QN; ++h) {
+          float4 gg = g[u][h];
+          const float4 vv = v[u][h];
+          if (rmode) {
+            float4 o;
+            if (need_y) {
+              o = o4[u][h];
+            } else {
+              o.x = bn_affine(vv.x, m[h].x, is[h].x, ww[h].x, bb[h].x);
+              o.y = bn_affine(vv.y, m[h].y, is[h].y, ww[h].y, bb[h].y);
+              o.z = bn_affine(vv.z, m[h].z, is[h].z, ww[h].z, bb[h].z);
+              o.w = bn_affine(vv.w, m[h].w, is[h].w, ww[h].w, bb[h].w);
+            }
+            const float k = rmode <= 2 ? 0.f : 0.2f;
+            gg.x = o.x > 0.f ? gg.x : k * gg.x;
+            gg.y = o.y > 0.f ? gg.y : k * gg.y;
+            gg.z = o.z > 0.f ? gg.z : k * gg.z;
+            gg.w = o.w > 0.f ? gg.w : k * gg.w;
+          }
+          if (dres) st4(dres + e + 4 * h, gg);
+          const float4 W = ww[h], I = is[h], M = m[h], G = mg[h], X = mgx[h];
+          if (train) {
+            out[h].x = W.x * I.x * (gg.x - G.x - (vv.x - M.x) * I.x * X.x);
+            out[h].y = W.y * I.y * (gg.y - G.y - (vv.y - M.y) * I.y * X.y);
+            out[h].z = W.z * I.z * (gg.z - G.z - (vv.z - M.z) * I.z * X.z);
+            out[h].w = W.w * I.w * (gg.w - G.w - (vv.w - M.w) * I.w * X.w);
+          } else {
+            out[h].x = gg.x * W.x * I.x; out[h].y = gg.y * W.y * I.y; out[h].z = gg.z * W.z * I.z; out[h].w = gg.w * W.w * I.w;
+          }
+          if (dx) st4(dx + e + 4 * h, out[h]);
+        }
+        if (dxb) store_copyq<QN>(dxb, ru, c0, C, out, terms);
+      }
     }
   }
 }
@@ -470,17 +643,18 @@ struct ApplyPlan {
   int64_t per;
 };
 
-static ApplyPlan apply_plan(int64_t rows, int C) {
+static ApplyPlan apply_plan(int64_t rows, int C, int qn = 1) {
   ApplyPlan a;
-  a.tc = std::min(C / 4, 64);
+  const int groups = C / (4 * qn);   // channel groups of qn quads
+  a.tc = std::min(groups, 64);
   if (a.tc < 1) a.tc = 1;
   while (256 % a.tc) --a.tc;
-  a.cblocks = (int)ceil_div(C / 4, a.tc);
+  a.cblocks = (int)ceil_div(groups, a.tc);
   const int tr = 256 / a.tc;
   // ~2 blocks per CU: the apply passes run beside the weight-gradient GEMMs; 512 blocks measured
   // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (two runs each)
   const int want = std::max(1, kApplyBlocks / a.cblocks);
-  const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * kApplyUnroll));
+  const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * (qn == 2 ? kBf16Rows : kApplyUnroll)));
   a.rsplits = (int)std::min<int64_t>(want, maxs);
   a.per = ceil_div(rows, a.rsplits);
   a.rsplits = (int)ceil_div(rows, a.per);
@@ -492,13 +666,14 @@ struct ReducePlan {
   int64_t per;
 };
 
-static ReducePlan reduce_plan(int64_t rows, int C) {
+static ReducePlan reduce_plan(int64_t rows, int C, int qn = 1) {
   ReducePlan r;
-  r.tc = std::min(C / 4, 64);
+  const int groups = C / (4 * qn);
+  r.tc = std::min(groups, 64);
   if (r.tc < 1) r.tc = 1;
   // tc must divide 256
   while (256 % r.tc) --r.tc;
-  r.cblocks = (int)ceil_div(C, 4 * r.tc);
+  r.cblocks = (int)ceil_div(groups, r.tc);
   // 512 blocks: 256 / 1024 measured -2 % / -4.5 % at c2 — the reduction shares the chip with
   // the weight-gradient GEMMs, more blocks take CUs from them
   int want = std::max(1, kReduceBlocks / r.cblocks);
@@ -510,10 +685,23 @@ static ReducePlan reduce_plan(int64_t rows, int C) {
   return r;
 }
 
+// bf16 storage with 8-channel groups: C % 8 and 16-B aligned operands (else one quad a thread)
+static int bf16_qn(int C, std::initializer_list<const void *> ptrs) {
+  if (C % 8) return 1;
+  for (const void *p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 16) return 1;
+  return 2;
+}
+
+// The reductions take 8-channel groups only on wide tensors: at C = 256 the halved block
+// count cost more than the wider loads gained (l3.bn2 backward sums 13.2 -> 15.9 us, l3.bn3
+// 62.9 -> 58.9 us; statistics 34.2 -> 25.1 us at C = 1024, tools/bn_bench.py --bf16)
+static int reduce_qn(int qn, int C) { return qn == 2 && C >= 512 ? 2 : 1; }
+
 static size_t bn_ws_bytes(int64_t rows, int C) {
-  ReducePlan r = reduce_plan(rows, C);
-  // partial [splits][2][C] + coef [2][C]
-  return ((size_t)r.splits * 2 * C + 2 * (size_t)C) * sizeof(float);
+  // partial [2][C][splits] + coef [2][C], for either channel grouping
+  const int splits = std::max(reduce_plan(rows, C, 1).splits, C % 8 ? 0 : reduce_plan(rows, C, 2).splits);
+  return ((size_t)splits * 2 * C + 2 * (size_t)C) * sizeof(float);
 }
 
 static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(total4, 256), 8192); }
@@ -522,49 +710,71 @@ static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(tot
 
 namespace adaptseg {
 
+template <typename TX, typename TY, int QN>
+static void bn_bwd_kernels(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y, const TX *x,
+                           const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                           float *dx, uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight,
+                           float *dbias, float *partial, float *coef, double reduce_bytes, double apply_bytes,
+                           bool dterms, hipStream_t s) {
+  int slot;
+  if (train) {
+    const int rqn = reduce_qn(QN, c);
+    const ReducePlan r = reduce_plan(rows, c, rqn);
+    timing_begin(kTBnReduceBwd, s, reduce_bytes, &slot);
+    if (rqn == 2)
+      bn_reduce_kernel<1, TX, TY, QN><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
+          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
+    else
+      bn_reduce_kernel<1, TX, TY, 1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
+          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
+    timing_end(slot, s);
+    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd, coef,
+                                                                   dweight, dbias);
+  }
+  timing_begin(kTBnBwdApply, s, apply_bytes, &slot);
+  const ApplyPlan ap = apply_plan(rows, c, QN);
+  bn_bwd_apply2d_kernel<TX, TY, QN><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
+      rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
+      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms);
+  timing_end(slot, s);
+}
+
 template <typename TX, typename TY = TX>
 int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
                          const float *bias, const float *save_mean, const float *save_invstd, float *dx,
                          uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
                          size_t ws_bytes, hipStream_t s) {
-  float *coef = nullptr;
-  int slot;
+  float *partial = reinterpret_cast<float *>(ws), *coef = nullptr;
   const double eb = sizeof(TX);   // bytes per activation element (x)
   const bool terms = std::is_same<TY, X3>::value;   // y stored as F32X3 term images
   const double ebt = terms ? 2.0 : eb;               // ... bytes per element of y (terms: the hi term, ldm4)
   const bool dterms = copies_are_terms() && dx_bf16;
+  const int qn = (sizeof(TX) == 2 && !terms && !dterms) ? bf16_qn(c, {dy, y, x, dx, dx_bf16, dres}) : 1;
   if (train) {
     size_t need = bn_ws_bytes(rows, c);
     if (!ws || ws_bytes < need) {
       set_error("bn_bwd: workspace %zu < %zu", ws_bytes, need);
       return ADAPTSEG_ERR_WORKSPACE;
     }
-    ReducePlan r = reduce_plan(rows, c);
-    float *partial = reinterpret_cast<float *>(ws);
-    coef = partial + (size_t)r.splits * 2 * c;
-    // dy, x (+ y for the mask from y) in
-    timing_begin(kTBnReduceBwd, s, (4.0 + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c, &slot);
-    bn_reduce_kernel<1, TX, TY><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, dy, y, save_mean,
-                                                                         save_invstd, weight, bias, rmode, r.per,
-                                                                         partial);
-    timing_end(slot, s);
-    AS_CHECK_LAUNCH("bn_reduce<bwd>");
-    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd,
-                                                                   coef, dweight, dbias);
-    AS_CHECK_LAUNCH("bn_bwd_final");
+    coef = partial + (size_t)reduce_plan(rows, c, reduce_qn(qn, c)).splits * 2 * c;
   }
-  // dy, x (train), y (mask from y) in; dx, dres out
-  timing_begin(kTBnBwdApply, s,
-               (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * (train ? 1 : 0) +
-                ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
-                   (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0),
-               &slot);
-  const ApplyPlan ap = apply_plan(rows, c);
-  bn_bwd_apply2d_kernel<TX, TY><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
-      rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
-      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms);
-  timing_end(slot, s);
-  AS_CHECK_LAUNCH("bn_bwd_apply");
+  // reduce: dy, x (+ y for the mask from y) in; apply: dy, x (train), y (mask from y) in; dx,
+  // dres out
+  const double reduce_bytes = (4.0 + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
+  const double apply_bytes = (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * (train ? 1 : 0) +
+                              ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
+                             (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0);
+  if constexpr (sizeof(TX) == 2 && !std::is_same<TY, X3>::value) {
+    if (qn == 2) {
+      bn_bwd_kernels<TX, TY, 2>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
+                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+      AS_CHECK_LAUNCH("bn_bwd");
+      return ADAPTSEG_OK;
+    }
+  }
+  bn_bwd_kernels<TX, TY, 1>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
+                            dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+  AS_CHECK_LAUNCH("bn_bwd");
   return ADAPTSEG_OK;
 }
 
@@ -607,17 +817,22 @@ static double fwd_apply_bytes(int64_t rows, int c, const float *x, const float *
 static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *mean,
                          const float *invstd, const float *weight, const float *bias, const float *res,
                          const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu, hipStream_t s) {
-  const ApplyPlan ap = apply_plan(rows, c);
-  const dim3 g(ap.cblocks, ap.rsplits);
   const bool terms = copies_are_terms() && y_bf16;
   uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
+  const int qn = (!x && !terms) ? bf16_qn(c, {x_bf16, res_bf16, y, y_bf16}) : 1;
+  const ApplyPlan ap = apply_plan(rows, c, qn);
+  const dim3 g(ap.cblocks, ap.rsplits);
   if (x && rb)
     bn_apply2d_kernel<float, X3><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, rb, y, yb,
                                                    relu, terms);
   else if (x)
     bn_apply2d_kernel<float, float><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, res, y,
                                                       yb, relu, terms);
+  else if (qn == 2)
+    bn_apply2d_kernel<__bf16, __bf16, 2><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
+                                                           reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
+                                                           weight, bias, rb, y, yb, relu, terms);
   else
     bn_apply2d_kernel<__bf16, __bf16><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
                                                         reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
@@ -641,7 +856,8 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
     return ADAPTSEG_ERR_WORKSPACE;
   }
   hipStream_t s = as_stream(stream);
-  ReducePlan r = reduce_plan(rows, c);
+  ReducePlan r = reduce_plan(rows, c), r2 = {0, 0, 0, 0};
+  if (!x && reduce_qn(bf16_qn(c, {x_bf16}), c) == 2) r2 = reduce_plan(rows, c, 2);   // bf16 x: 8-channel groups
   float *partial = reinterpret_cast<float *>(ws);
   const double eb = x ? 4.0 : 2.0;   // bytes per activation element read
   int slot;  // x in
@@ -650,6 +866,9 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
   if (x)
     bn_reduce_kernel<0, float><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
                                                                        nullptr, nullptr, nullptr, 0, r.per, partial);
+  else if (r2.splits)
+    bn_reduce_kernel<0, __bf16, __bf16, 2><<<dim3(r2.cblocks, r2.splits), 256, 0, s>>>(
+        rows, c, r2.tc, xb, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, r2.per, partial);
   else
     bn_reduce_kernel<0, __bf16><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, xb, nullptr, nullptr, nullptr,
                                                                         nullptr, nullptr, nullptr, 0, r.per, partial);
@@ -659,7 +878,7 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
     bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, x, partial, save_mean, save_invstd,
                                                                    running_mean, running_var, momentum, eps);
   else
-    bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, xb, partial, save_mean,
+    bn_stats_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r2.splits ? r2.splits : r.splits, xb, partial, save_mean,
                                                                    save_invstd, running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
   timing_begin(kTBnApply, s, fwd_apply_bytes(rows, c, x, res, res_bf16, y, y_bf16), &slot);

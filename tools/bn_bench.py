@@ -2,7 +2,10 @@
 """Isolated timing of the BN passes at the c2 step's shapes (batch 4, layer1 129x257 /
 layer2-4 65x129), through the library's own HBM timing ids (algorithmic bytes / event time).
 
-    python tools/bn_bench.py
+    python tools/bn_bench.py [--bf16]
+
+--bf16: the c5 program's storage (bf16 activations x / residual / y, fp32 gradients in, the
+backward writing only the bf16 copy of dx and the fp32 residual gradient).
 """
 import os
 import sys
@@ -22,6 +25,9 @@ REPS = 20
 
 
 def main():
+    lp = "--bf16" in sys.argv
+    if lp:
+        K.set_conv_math(K.MATH_BF16)   # bf16 activation storage is the bf16 maths' (c5)
     g = torch.Generator(device=DEV).manual_seed(0)
     print(f"{'bn':8s} {'rows':>7s} {'C':>5s}  {'kernel':36s} {'us':>8s} {'GB/s':>7s}")
     for name, rows, c, mode in SHAPES:
@@ -31,17 +37,35 @@ def main():
         b = torch.randn(c, device=DEV, generator=g) * 0.1
         rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
         res = torch.randn(rows, c, device=DEV, generator=g) if mode == "res" else None
-        y, mean, invstd = K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True)
+        if lp:
+            x = x.to(torch.bfloat16)
+            res = res.to(torch.bfloat16) if res is not None else None
         dres = torch.empty_like(dy) if mode == "res" else None
+
+        def fwd():
+            if lp:
+                return K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True, bf16_out=True,
+                                      fp32_out=False)[3]
+            return K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True, out=y)[0]
+
+        def bwd():
+            K.bn_bwd(dy, y if mode == "res" else None, x, w, mean, invstd, relu=True, dres=dres, bias=b,
+                     bf16_out=lp, fp32_out=not lp)
+
+        if lp:
+            _, mean, invstd, y = K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True, bf16_out=True,
+                                                fp32_out=False)
+        else:
+            y, mean, invstd = K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True)
         for _ in range(3):
-            K.bn_bwd(dy, y if mode == "res" else None, x, w, mean, invstd, relu=True, dres=dres, bias=b)
+            bwd()
         torch.cuda.synchronize()
         K.timing_enable(-1)
         K.timing_enable(-1, enable=False)   # resets the record
         K.timing_enable_mem(True)
         for _ in range(REPS):
-            K.bn_fwd_train(x, w, b, rm, rv, 0.1, 1e-5, res=res, relu=True, out=y)
-            K.bn_bwd(dy, y if mode == "res" else None, x, w, mean, invstd, relu=True, dres=dres, bias=b)
+            fwd()
+            bwd()
         torch.cuda.synchronize()
         K.timing_enable_mem(False)
         for kid, kname in K.MEM_KERNELS.items():
