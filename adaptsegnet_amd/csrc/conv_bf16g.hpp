@@ -55,17 +55,21 @@ __device__ __forceinline__ int g16_off(int r, int ch) {
 // prologue overlap the other's K loop (short-K 1x1 products).
 // S2: the stride-2 data gradient by output-pixel parity class (blockIdx.z = 2 py + px), each a
 // dense stride-1 GEMM over its subgrid with only its taps, as igemm_x3_kernel / igemm_bf16_kernel.
+// 256x256 (BK 32 only: a 3 x 32 KB ring): 8 waves of 64x128, 128 accumulator VGPRs, one block per
+// CU — half the operand bytes per MFMA of the 128x256 tile, for products whose M x N fills the
+// chip with such tiles.
 template <int MODE, int BM, int BN, int BK, bool S2 = false>
-__global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(const ConvParams p,
+__global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 2 : 1) igemm_bf16g_kernel(const ConvParams p,
                                                                               const __bf16 *__restrict__ ab,
                                                                               const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
   static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
   static_assert(BK == 64 || BK == 32, "K step");
   constexpr int NT = 512;
-  constexpr int WAVES_M = BM / 64, WAVES_N = BN / 64;  // 64x64 wave tiles
-  static_assert(WAVES_M * WAVES_N == 8, "8 waves");
-  constexpr int WTM = 64, WTN = 64, TM = 2, TN = 2;
+  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;  // 64 x (BN / WAVES_N) wave tiles
+  static_assert(WAVES_M * WAVES_N == 8 && BN % (32 * WAVES_N) == 0, "8 waves");
+  static_assert(BM * BN < 65536 || BK == 32, "256x256 tiles: K step 32 (LDS ring)");
+  constexpr int WTM = 64, WTN = BN / WAVES_N, TM = 2, TN = WTN / 32;
   constexpr int LPR = BK / 8;                          // lanes per image row (16 B each)
   constexpr int RPI = 64 / LPR;                        // rows per LDS-DMA instruction
   constexpr int NA = BM / (8 * RPI), NB = BN / (8 * RPI);  // instructions per wave and K step
@@ -241,8 +245,9 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       // this wave's DMAs of step kt are done (step kt+1's NA + NB stay in flight) ...
-      static_assert(NA + NB == 6 || NA + NB == 3, "vmcnt below counts 6 or 3 instructions per step");
+      static_assert(NA + NB == 6 || NA + NB == 4 || NA + NB == 3, "vmcnt below counts 6, 4 or 3 instructions per step");
       if constexpr (NA + NB == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (NA + NB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       // ... and after the barrier every wave's are, and every wave has finished reading the
       // stage that step kt+2 overwrites (step kt-1's)
@@ -269,16 +274,20 @@ __global__ void __launch_bounds__(512, BK == 32 ? 2 : 1) igemm_bf16g_kernel(cons
 // lane's 16-B column chunk (8 input channels, Cin % 8 == 0) has its own tap, so a 128-column
 // tile may span taps (Cin 64: two); a chunk of a tap outside the image loads zeros.  BM 256 (Cout >= 256) reads dY once per column
 // tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
-// KB, two blocks per CU.
-template <int BM>
-__global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvParams p, const __bf16 *__restrict__ dyb,
-                                                                    const __bf16 *__restrict__ xb) {
-  constexpr int BKP = 32, BN = 128;
+// KB, two blocks per CU.  BN 256 (with BM 256): two B images, 8 waves of 64x128, a 3 x 32 KB ring
+// and one block per CU — half the operand bytes per MFMA of 256x128.
+template <int BM, int BN = 128>
+__global__ void __launch_bounds__(512, BN == 256 ? 1 : 2) igemm_bf16g_wgrad_kernel(const ConvParams p,
+                                                                                   const __bf16 *__restrict__ dyb,
+                                                                                   const __bf16 *__restrict__ xb) {
+  constexpr int BKP = 32;
+  static_assert(BN == 128 || (BN == 256 && BM == 256), "wgrad tiles 128x128, 256x128, 256x256");
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   constexpr int WTM = 64, WTN = BN / WAVES_N, TM = 2, TN = WTN / 32;
   constexpr int NA = BM / 128;                // A images / instructions per wave and K step
+  constexpr int NB = BN / 128;                // B images
   constexpr int IMG = BKP * 256;              // one [32 k][128] bf16 image
-  constexpr int STAGE = (NA + 1) * IMG;
+  constexpr int STAGE = (NA + NB) * IMG;
 
   __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
 
@@ -303,14 +312,19 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
   bool a_col[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) a_col[i] = bm + 128 * i + chs < p.M;   // Cout % 8 == 0
-  // this lane's column chunk: its tap (per lane: with Cin % 128 != 0 a tile spans taps) and
-  // input channel
-  const bool b_col = bn + chs < p.N;
-  const int ncol = b_col ? bn + chs : 0;
-  const int tap = (int)fdiv((uint32_t)ncol, p.fd_c);
-  int seg, t, tdy, tdx;
-  seg_geom(p, sr, tap, seg, t, tdy, tdx);
-  const int ci = ncol - tap * p.c;
+  // this lane's column chunk of each B image: its tap (per lane: with Cin % 128 != 0 a tile
+  // spans taps) and input channel
+  bool b_col[NB];
+  int tdy[NB], tdx[NB], ci[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    b_col[j] = bn + 128 * j + chs < p.N;
+    const int ncol = b_col[j] ? bn + 128 * j + chs : 0;
+    const int tap = (int)fdiv((uint32_t)ncol, p.fd_c);
+    int seg, t;
+    seg_geom(p, sr, tap, seg, t, tdy[j], tdx[j]);
+    ci[j] = ncol - tap * p.c;
+  }
   const __bf16 *zero = reinterpret_cast<const __bf16 *>(g_bf16g_zero);
 
   auto issue = [&](int kt, int st) {
@@ -322,12 +336,15 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
     const int ow = mm - (int)q * p.ow;
     uint32_t b = fdiv(q, p.fd_oh);
     const int oh = (int)q - (int)b * p.oh;
-    const int iy = oh * p.stride + tdy, ix = ow * p.stride + tdx;
-    const bool bv = rv & b_col & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
       glds16((rv & a_col[i]) ? dyb + (size_t)mm * p.k + bm + 128 * i + chs : zero, As + i * IMG);
-    glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci : zero, As + NA * IMG);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int iy = oh * p.stride + tdy[j], ix = ow * p.stride + tdx[j];
+      const bool bv = rv & b_col[j] & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
+      glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci[j] : zero, As + (NA + j) * IMG);
+    }
   };
 
   const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
@@ -341,14 +358,14 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
 
   auto compute = [&](int st) {
     const char *Ai = lds + st * STAGE + (wm * WTM / 128) * IMG;   // the A image of this wave's rows
-    const char *Bs = lds + st * STAGE + NA * IMG;
-    const int ar = (wm * WTM) % 128;
+    const char *Bs = lds + st * STAGE + (NA + (wn * WTN) / 128) * IMG;   // this wave's columns' B image
+    const int ar = (wm * WTM) % 128, bc = (wn * WTN) % 128;
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) a[slot][i] = mc_frag(Ai, ar + i * 32, ks, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[slot][j] = mc_frag(Bs, wn * WTN + j * 32, ks, lane);
+      for (int j = 0; j < TN; ++j) b[slot][j] = mc_frag(Bs, bc + j * 32, ks, lane);
     };
     read_frags(0, 0);
 #pragma unroll
@@ -369,9 +386,11 @@ __global__ void __launch_bounds__(512, 2) igemm_bf16g_wgrad_kernel(const ConvPar
     issue(min(kt0 + 1, klast), 1);
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
-      // step kt landed, step kt+1's NA + 1 instructions in flight
-      if constexpr (NA == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      // step kt landed, step kt+1's NA + NB instructions in flight
+      static_assert(NA + NB >= 2 && NA + NB <= 4, "vmcnt below counts 2-4 instructions per step");
+      if constexpr (NA + NB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (NA + NB == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");   // no LDS access moves above the barrier
       issue(min(kt + 2, klast), st == 0 ? 2 : st - 1);

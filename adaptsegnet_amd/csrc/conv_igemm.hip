@@ -413,6 +413,21 @@ void set_splits(Plan &pl) {
   if (pl.x3) pl.slab_bytes += x3_pre_bytes(pl);
 }
 
+// 256x256 bf16 LDS-DMA tiles (conv_bf16g.hpp), built but off: one 8-wave
+// block per CU hides the DMA ring's latency worse than two 128x256 blocks — per shape slower
+// (l3.conv3 fwd 44.6 -> 57.0 us, l3.ds fwd 60.1 -> 71.0), c5 41.22 / 41.33 images/s off vs
+// 37.27 / 37.25 with both, 40.28 / 40.30 with the weight gradients only, same box
+// (profiles/r3/bf16_wide_tiles_ab.txt).  -DADAPTSEG_G16_WIDE_MIN_TILES=256 /
+// -DADAPTSEG_G16_WIDE_WGRAD=1 build them (tests/test_bf16_gpu.py::test_bf16_wide_tile_products).
+#ifndef ADAPTSEG_G16_WIDE_MIN_TILES
+#define ADAPTSEG_G16_WIDE_MIN_TILES 0
+#endif
+constexpr int64_t kG16WideMinTiles = ADAPTSEG_G16_WIDE_MIN_TILES;   // 0: no 256x256 tiles
+#ifndef ADAPTSEG_G16_WIDE_WGRAD
+#define ADAPTSEG_G16_WIDE_WGRAD 0
+#endif
+constexpr bool kG16WideWgrad = ADAPTSEG_G16_WIDE_WGRAD;   // 256x256 bf16 weight-gradient tiles
+
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   int st = validate(d);
   if (st) return st;
@@ -554,13 +569,20 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
+      // 256x256x32 (half the operand bytes per MFMA of 128x256; one block per CU) where such
+      // tiles still give every CU one
+      if (kG16WideMinTiles > 0 && !pl.s2 && p.N >= 256 &&
+          ceil_div(p.M, 256) * ceil_div(p.N, 256) >= kG16WideMinTiles) {
+        pl.g16_bm = pl.g16_bn = 256;
+        pl.g16_bk = 32;
+      }
     }
     // weight gradients with 16-B channel chunks (Cin % 8 == 0, Cout % 8 == 0) on the LDS-DMA
     // weight-gradient kernel: {128,256}x128 tiles, K steps of 32 output pixels
     if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 8 == 0 && d->k % 8 == 0) {
       pl.g16 = true;
       pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
-      pl.g16_bn = 128;
+      pl.g16_bn = (kG16WideWgrad && d->k >= 256 && p.N >= 256) ? 256 : 128;   // 256x256: x once per row tile
       pl.g16_bk = 32;
     }
   }
@@ -579,8 +601,9 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 int kernel_id(const Plan &pl, int mode) {
   // 88 / 89: the FAST cfg-8 stride-2 ids, which never occur (cfg 8 has no stride-2 form)
   if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
-  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
+  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bn == 256 ? 82 : pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
+  if (pl.g16 && pl.g16_bm == 256 && pl.g16_bn == 256) return 100 * mode + 82;   // (a free FAST id: cfg 7 ends at 81)
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
