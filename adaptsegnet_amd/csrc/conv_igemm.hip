@@ -379,7 +379,10 @@ void set_splits(Plan &pl) {
   // 2-per-CU grid of 16-wave blocks holds every CU for a whole split, and the main stream's
   // short BN / split-K kernels then wait for CU slots.  384 measured c2 +2.4 %, c3 +2.6 %
   // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2, tools/dbg/ab_bench_many.sh).
-  constexpr int kX3WgradTarget = 384;
+#ifndef ADAPTSEG_X3_WGRAD_TARGET
+#define ADAPTSEG_X3_WGRAD_TARGET 384
+#endif
+  constexpr int kX3WgradTarget = ADAPTSEG_X3_WGRAD_TARGET;
   // The LDS-DMA bf16 weight gradient (side stream) to ~256 blocks: half the split-K slab
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
@@ -399,7 +402,13 @@ void set_splits(Plan &pl) {
   const int split_below = pl.mode == MODE_WGRAD ? target : pl.x3r ? 256 : pl.g16 ? 128 : 257;
   int splits = 1;
   if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
+#ifndef ADAPTSEG_X3_WGRAD_ROUND_NEAREST
+#define ADAPTSEG_X3_WGRAD_ROUND_NEAREST 0
+#endif
+    if (ADAPTSEG_X3_WGRAD_ROUND_NEAREST && pl.mode == MODE_WGRAD && pl.x3 && !pl.x3r)
+      splits = std::max(1, (target + pl.tiles / 2) / pl.tiles);
+    else
+      splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
