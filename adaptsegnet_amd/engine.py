@@ -180,6 +180,17 @@ def _conv_plain(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
     return K.conv_fwd(g, x, n, h, w, [weight], strides=strides, xb=xb, bf16_only=bf16_only), None
 
 
+def x3_forward_terms(g) -> bool:
+    """F32X3 (default maths, no operand copies): run this conv's forward on the term-image
+    kernel (conv_x3r.hpp, 256x128x32 LDS-DMA) with the producing BN writing its input's three
+    bf16 terms beside the fp32 tensor — the dilated 3x3 conv2 of layers 3-4 (Cin >= 256).  The
+    forward runs without the weight-gradient stream beside it, so the kernel's one-block-per-CU
+    footprint costs nothing there (it does in the backward, §3.2).  Same box: c2 26.95 / 26.91
+    -> 27.33 / 27.25 images/s, c3 17.35 / 17.36 -> 17.66 / 17.66; extending it to Cin 128 / 64
+    (layers 1-2) measured no further gain (profiles/r3/x3r_forward_ab.txt)."""
+    return K.get_conv_math() == K.MATH_F32X3 and g.kh * g.kw > 1 and g.cin >= 256 and g.cin % 32 == 0
+
+
 def block_input_fp32(blk, n, h, w) -> bool:
     """Under bf16 activation storage: does some consumer of this block's INPUT (its conv1 and
     downsample conv: forward and weight gradient) still read fp32?  Then its producer (the
@@ -215,7 +226,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     thin1 = sh and bf16_only(g2, n, oh, ow, (0, 2))
     thin2 = sh and bf16_only(g3, n, oh, ow, (0, 2))
     c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=lp)
-    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh, fp32=not thin1)
+    terms2 = not sh and x3_forward_terms(g2)   # conv2's forward on y1's term images
+    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2, fp32=not thin1)
     c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
     y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
     c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
@@ -235,7 +247,7 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
-        rec.xb, rec.y1b, rec.y2b = xb, y1b, y2b   # the weight gradients' bf16 x operands
+        rec.xb, rec.y1b, rec.y2b = xb, y1b if sh else None, y2b   # the weight gradients' bf16 x operands
         if sh:
             rec.out = outb   # bf16 storage: the BN3 backward's mask source is the bf16 output
     return out, rec, outb

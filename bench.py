@@ -65,11 +65,12 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
 
     copies = engine.bf16_operands()   # the Bottleneck products get their operand copies
 
-    def add(geom, n, h, w, op, strides=None, count=1, algo=None, cp=False):
+    def add(geom, n, h, w, op, strides=None, count=1, algo=None, cp=False, terms=False):
         # geom: the geometry the engine launches; algo: the reference's (unpadded) one, whose
         # FLOPs are counted; cp: the engine passes the operand copies (engine.block_forward /
-        # block_backward under bf16_operands)
-        kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides, copies=cp and copies)
+        # block_backward under bf16_operands); terms: it passes them for this product alone
+        # (engine.x3_forward_terms)
+        kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides, copies=(cp and copies) or terms)
         inv[kid] = inv.get(kid, 0.0) + count * (algo or geom).flops(n, h, w)
         if products is not None:
             products.add((op, kid, sp > 1))
@@ -119,7 +120,8 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
                 if blk.downsample is not None:
                     convs.append((blk.downsample[0], h, w, not first))
                 for conv, ch, cw, xcp in convs:
-                    add(conv.geom(), batch, ch, cw, 0, cp=xcp)
+                    fwd_terms = conv is blk.conv2 and not copies and engine.x3_forward_terms(conv.geom())
+                    add(conv.geom(), batch, ch, cw, 0, cp=xcp, terms=fwd_terms)
                     if backward and (li < 4 or "l6" in heads_bwd):
                         add(conv.geom(), batch, ch, cw, 1, cp=True)
                         add(conv.geom(), batch, ch, cw, 2, cp=xcp)

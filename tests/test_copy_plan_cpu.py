@@ -184,3 +184,33 @@ def test_weight_pack_sizes_follow_the_plan():
         assert size(g, 0) == 0
     finally:
         K.set_conv_math(prev)
+
+
+def test_f32x3_forward_term_images_only_for_the_wide_dilated_convs():
+    """Under the default F32X3 maths the engine writes one operand copy: y1's three bf16 terms,
+    for the forward of conv2 in layers 3-4 (dilated 3x3, Cin >= 256), which then runs on the
+    term-image kernel (selector 88, conv_x3r.hpp); every other product keeps the register-staged
+    kernel on fp32 operands.  bench.conv_inventory books those FLOPs under selector 88."""
+    import bench
+    from adaptsegnet_amd import engine
+    from adaptsegnet_amd import kernels as K
+    from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
+    assert K.get_conv_math() == K.MATH_F32X3 and not engine.bf16_operands()
+    model, D = DeeplabMulti(num_classes=19), FCDiscriminator(num_classes=19)
+    want = set()
+    for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4), 1):
+        for blk in layer:
+            for conv in (blk.conv1, blk.conv2, blk.conv3):
+                on = engine.x3_forward_terms(conv.geom())
+                assert on == (conv is blk.conv2 and li >= 3), (li, conv)
+                if on:
+                    want.add(conv.geom())
+    inv = bench.conv_inventory(model, D, "single-level", 4, (1024, 512), (1024, 512), (1024, 512))
+    n, h, w = 4, 64, 128   # layers 3-4 at 1024x512 (stem /2, max-pool /2 floor, layer2 /2)
+    flops = 2 * sum(g.flops(n, h, w) for g in [b.conv2.geom() for b in list(model.layer3) + list(model.layer4)])
+    assert abs(inv[88] - flops) <= 1e-6 * flops   # source + target forwards
+    K.set_conv_math(K.MATH_F32)
+    try:
+        assert not any(engine.x3_forward_terms(g) for g in want)
+    finally:
+        K.set_conv_math(K.MATH_F32X3)
