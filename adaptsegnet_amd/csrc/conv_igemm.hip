@@ -559,6 +559,16 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.x3g = pl.x3r = true;
       pl.x3r_bm = 128;
     }
+#ifndef ADAPTSEG_X3R_FWD_PERCALL
+#define ADAPTSEG_X3R_FWD_PERCALL 0
+#endif
+    // F32X3 (default) forwards of wide multi-tap convs (Cin >= 256, >= 9 taps: DeeplabVGG
+    // conv3-5, D.conv4) on the term-image kernel with the images made per call (a read of 4 B and
+    // a write of 6 B per input element against K >= 2304 of GEMM per output element); the
+    // Bottleneck conv2 forwards get them from BN1 instead (engine.x3_forward_terms)
+    if (ADAPTSEG_X3R_FWD_PERCALL && pl.x3 && op == ADAPTSEG_CONV_FWD && pl.x3r_ok && d->kh * d->kw >= 9 &&
+        d->c >= 256 && conv_math() == ADAPTSEG_MATH_F32X3)
+      pl.x3g = pl.x3r = true;
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
