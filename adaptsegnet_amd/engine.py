@@ -313,16 +313,12 @@ def block_backward(blk, rec, gout, need_w, ws=None):
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
     # (the saved y is the mask source in eval mode: bf16 like x under bf16 storage)
-    import os
-    tb = not sh and os.environ.get("ADAPTSEG_X3R_DGRAD") == "1" and x3_forward_terms(g2)
     r = bn_backward(blk.bn2, dy2, rec.y2b if sh else rec.y2, rec.c2, rec.s2, relu=True, dx=dy2,
-                    mask_from_x=True, bf16=sh or tb, fp32=f2)
-    dy2b = r[1] if (sh or tb) else None
+                    mask_from_x=True, bf16=sh, fp32=f2)
+    dy2b = r[1] if sh else None
     if not f2:
         dy2 = None   # not written: its consumers read dy2b
     dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b)
-    if tb:
-        dy2b = None
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b

@@ -1,6 +1,7 @@
 #!/bin/bash
 # F32X3 wide multi-tap forwards on the term-image kernel with per-call images
-# (ADAPTSEG_X3R_FWD_PERCALL; libadaptseg_pc.so built with it 1): parity, then c4 / c2 arms.
+# (ADAPTSEG_X3R_FWD_PERCALL; build the arm first: make -C adaptsegnet_amd/csrc BUILD=build_pc
+# OUT=../lib/libadaptseg_pc.so EXTRA=-DADAPTSEG_X3R_FWD_PERCALL=1): parity, then c4 / c2 arms.
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT}" || exit 2
 mkdir -p gpurun_out
