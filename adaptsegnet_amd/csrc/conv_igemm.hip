@@ -337,10 +337,17 @@ int plan_bm(const Plan &pl) {
 // copies: the three bf16 terms, pixel-interleaved [n][h][w][3][c]): the product moves to the x3r
 // kernel, which reads them by LDS-DMA instead of splitting fp32 rows in-kernel (F32X3_PRESPLIT:
 // it is there already; it then skips its per-call copy).  Re-plans the grid.
+static void x3_terms_flags(Plan &pl) {
+  pl.x3g = pl.x3r = pl.x3ext = true;
+  // weight gradients under the default maths run on the side stream beside the main chain's
+  // register-staged blocks: the 128-row tile (96 KB LDS, <= 128 VGPRs) leaves a CU room for one
+  // of them, the 256-row one (144 KB) does not
+  if (pl.mode == MODE_WGRAD && conv_math() == ADAPTSEG_MATH_F32X3) pl.x3r_bm = 128;
+}
 static void x3_terms(Plan &pl) {
   if (!copies_are_terms() || !pl.fast || !pl.x3 || !pl.x3r_ok || !pl.act_ext) return;
   if (pl.mode == MODE_WGRAD && !pl.act_ext2) return;
-  pl.x3g = pl.x3r = pl.x3ext = true;
+  x3_terms_flags(pl);
   set_splits(pl);
 }
 
@@ -821,7 +828,7 @@ int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *
   }
   if (pl.x3r_ok && copies_are_terms()) {   // the plan with the caller's term images
     Plan t = pl;
-    t.x3g = t.x3r = t.x3ext = true;
+    x3_terms_flags(t);
     set_splits(t);
     b = std::max(b, t.slab_bytes);
   }
@@ -901,6 +908,8 @@ int adaptseg_conv2d_wpack(const adaptseg_conv_desc *d, int op, const float *cons
   AS_CHECK_ARG(bytes >= need, "conv2d_wpack: %zu bytes < %zu", bytes, need);
   for (int s = 0; s < d->nseg; ++s) {
     AS_CHECK_ARG(w[s], "conv2d_wpack: null weight %d", s);
+    // the pack kernels read float4 weight rows (a misaligned weight's conv plan reads no pack)
+    AS_CHECK_ARG(aligned16(w[s]), "conv2d_wpack: weight %d must be 16-byte aligned", s);
     pl.p.wt[s] = w[s];
   }
   const hipError_t e = pl.x3 ? prep_x3_wpack(pl, pack, as_stream(stream)) : prep_bf16_wpack(pl, pack, as_stream(stream));

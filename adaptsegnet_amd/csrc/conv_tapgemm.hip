@@ -225,7 +225,9 @@ int tapgemm_fwd(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_b
   st = inner_plan(d, ADAPTSEG_CONV_FWD, pl);
   if (st) return st;
   pl.p.x = x;
-  pl.act_ext = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;   // read by the bf16 kernels only
+  // the operand copy: read by the bf16 LDS-DMA kernels (BF16 maths) and, under F32X3_PRESPLIT,
+  // as the term images of x by the inner x3r kernel (which then skips its per-call split)
+  pl.act_ext = (reinterpret_cast<uintptr_t>(x_bf16) & 15) ? nullptr : x_bf16;
   AS_CHECK_ARG(x || (pl.g16 && pl.act_ext), "conv fwd (tap-GEMM): x is NULL and the inner GEMM needs it");
   pl.p.wt[0] = wp;
   pl.p.out = z;

@@ -191,6 +191,12 @@ def x3_forward_terms(g) -> bool:
     return K.get_conv_math() == K.MATH_F32X3 and g.kh * g.kw > 1 and g.cin >= 256 and g.cin % 32 == 0
 
 
+import os as _os
+# (A/B switch, removed after measurement) 0: conv2 backward on fp32 operands; 1: its weight gradient
+# on term images (y1's from the forward, dY's from BN2's backward); 2: its data gradient too
+X3_BWD_TERMS = int(_os.environ.get("ADAPTSEG_X3_BWD_TERMS", "2"))
+
+
 def block_input_fp32(blk, n, h, w) -> bool:
     """Under bf16 activation storage: does some consumer of this block's INPUT (its conv1 and
     downsample conv: forward and weight gradient) still read fp32?  Then its producer (the
@@ -227,7 +233,12 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     thin2 = sh and bf16_only(g3, n, oh, ow, (0, 2))
     c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=lp)
     terms2 = not sh and x3_forward_terms(g2)   # conv2's forward on y1's term images
-    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2, fp32=not thin1)
+    # ... and its weight gradient: then no consumer reads the fp32 y1 (the BN1 backward's ReLU
+    # mask comes from x in train mode, from the terms' hi image in eval mode)
+    keep1 = terms2 and save and X3_BWD_TERMS >= 1
+    need1 = not terms2 or (save and not keep1)
+    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2,
+                               fp32=not thin1 and need1)
     c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
     y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
     c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
@@ -247,7 +258,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
-        rec.xb, rec.y1b, rec.y2b = xb, y1b if sh else None, y2b   # the weight gradients' bf16 x operands
+        # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
+        rec.xb, rec.y1b, rec.y2b = xb, y1b if (sh or keep1) else None, y2b
         if sh:
             rec.out = outb   # bf16 storage: the BN3 backward's mask source is the bf16 output
     return out, rec, outb
@@ -313,16 +325,22 @@ def block_backward(blk, rec, gout, need_w, ws=None):
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
     # (the saved y is the mask source in eval mode: bf16 like x under bf16 storage)
+    # F32X3 (default maths) with y1's term images saved: BN2's backward also writes dY2's terms,
+    # and conv2's weight gradient (X3_BWD_TERMS 2: its data gradient too) runs on the
+    # term-image kernel (conv_x3r.hpp) instead of splitting both fp32 operands in-kernel
+    t2 = not sh and rec.y1b is not None
+    if t2 and X3_BWD_TERMS >= 2:
+        f2 = False
     r = bn_backward(blk.bn2, dy2, rec.y2b if sh else rec.y2, rec.c2, rec.s2, relu=True, dx=dy2,
-                    mask_from_x=True, bf16=sh, fp32=f2)
-    dy2b = r[1] if sh else None
+                    mask_from_x=True, bf16=sh or t2, fp32=f2)
+    dy2b = r[1] if (sh or t2) else None
     if not f2:
         dy2 = None   # not written: its consumers read dy2b
-    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b)
+    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b if (sh or not f2) else None)
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
-    r = bn_backward(blk.bn1, dy1, rec.y1b if sh else rec.y1, rec.c1, rec.s1, relu=True, dx=dy1,
+    r = bn_backward(blk.bn1, dy1, rec.y1b if (sh or rec.y1 is None) else rec.y1, rec.c1, rec.s1, relu=True, dx=dy1,
                     mask_from_x=True, bf16=sh, fp32=f1)
     dy1b = r[1] if sh else None
     if not f1:

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -26,7 +27,7 @@ __all__ = [
     "bn_fwd_train_tiles", "bn_fwd_infer", "bn_bwd",
     "maxpool_fwd", "maxpool_bwd", "upsample_fwd", "upsample_bwd", "softmax_fwd", "softmax_bwd",
     "ce_fwd", "ce_bwd", "adv_fwd", "adv_bwd", "sgd_step", "adam_step", "zero_", "to_nhwc",
-    "axpy", "add_i64", "weight_pack_scope", "pack_builds", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
+    "axpy", "add_i64", "weight_pack_scope", "pack_builds", "pack_count", "clear_weight_packs", "EPI_ACCUMULATE", "EPI_LEAKY", "EPI_LEAKY_GRAD", "EPI_RELU", "EPI_RELU_GRAD", "EPI_RESIDUAL",
 ]
 
 
@@ -96,13 +97,23 @@ def _desc(g: ConvGeom, n, h, w, strides):
 class _PackCache:
     """Caller-owned weight packs (adaptseg_conv2d_wpack) of the F32X3 / bf16 forward and
     data-gradient kernels.  Active only inside weight_pack_scope(); every pack built inside a
-    scope is stale once the outermost scope exits (the next use rebuilds it in place)."""
+    scope is stale once the outermost scope exits (the next use rebuilds it in place).
+
+    Packs are held per weight TENSOR (keyed by the first weight of the product, dropped by a
+    weakref finalizer on it), so they live exactly as long as the model that owns the weights: dropping a model
+    (a test, an eval loop, a re-created trainer) frees its packs.  Persistent cost while a model
+    lives: F32X3 forward + data-gradient packs are 3 bf16 terms each = 12 B per weight (DeeplabMulti
+    ~0.5 GB), bf16 packs 4 B per weight.  clear_weight_packs() drops every pack at once."""
 
     def __init__(self):
         self.depth = 0       # weight_pack_scope nesting
         self.epoch = 0       # bumped when the outermost scope exits
-        self.entries = {}    # key -> [pack buffer (uint8), epoch it was built in]
-        self.sizes = {}      # (geometry, op, math) -> pack bytes (0: the kernel reads none)
+        # id(first weight) -> {(weight data_ptrs, geometry, op, math): [pack buffer (uint8), epoch
+        # built]}; a weakref.finalize on the weight drops its entry (tensors compare elementwise,
+        # so they cannot key a WeakKeyDictionary)
+        self.entries = {}
+        # (geometry, op, math, NHWC input?) -> pack bytes (0: the kernel reads none)
+        self.sizes = {}
         self.builds = 0      # packs built (tests)
 
 
@@ -132,12 +143,24 @@ def pack_builds() -> int:
     return _PACKS.builds
 
 
+def pack_count() -> int:
+    """Weight packs currently held (tests: they go with their weights)."""
+    return sum(len(v) for v in list(_PACKS.entries.values()))
+
+
+def clear_weight_packs() -> None:
+    """Drop every cached weight pack (their device memory returns to the caching allocator)."""
+    _PACKS.entries.clear()
+
+
 def _wpack(g, n, h, w, strides, weights, op):
     """The cached weight pack for this product inside a weight_pack_scope, else None."""
     if _PACKS.depth == 0:
         return None
+    if not _aligned16(*weights):   # the pack kernels read float4 rows; the conv plan falls back
+        return None
     math = _ops._CONV_MATH[0]
-    skey = (g, op, math)
+    skey = (g, op, math, strides[1] == 1)   # the plan (and its pack) depends on the input layout
     size = _PACKS.sizes.get(skey)
     if size is None:
         d = _desc(g, n, h, w, tuple(strides))[0]
@@ -146,10 +169,15 @@ def _wpack(g, n, h, w, strides, weights, op):
         size = _PACKS.sizes[skey] = b.value
     if size == 0:
         return None
+    wid = id(weights[0])
+    per = _PACKS.entries.get(wid)
+    if per is None:
+        per = _PACKS.entries[wid] = {}
+        weakref.finalize(weights[0], _PACKS.entries.pop, wid, None)
     key = (tuple(t.data_ptr() for t in weights), g, op, math)
-    e = _PACKS.entries.get(key)
+    e = per.get(key)
     if e is None or e[0].numel() < size:
-        e = _PACKS.entries[key] = [torch.empty(size, dtype=torch.uint8, device=weights[0].device), -1]
+        e = per[key] = [torch.empty(size, dtype=torch.uint8, device=weights[0].device), -1]
     if e[1] != _PACKS.epoch:
         _OP.conv2d_wpack(list(weights), e[0], (n, g.cin, h, w), tuple(strides), _wshape(g), g.stride, g.pads,
                          g.dils, op)

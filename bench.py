@@ -123,8 +123,11 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
                     fwd_terms = conv is blk.conv2 and not copies and engine.x3_forward_terms(conv.geom())
                     add(conv.geom(), batch, ch, cw, 0, cp=xcp, terms=fwd_terms)
                     if backward and (li < 4 or "l6" in heads_bwd):
-                        add(conv.geom(), batch, ch, cw, 1, cp=True)
-                        add(conv.geom(), batch, ch, cw, 2, cp=xcp)
+                        # engine.block_backward: conv2's backward on term images (X3_BWD_TERMS)
+                        add(conv.geom(), batch, ch, cw, 1, cp=True,
+                            terms=fwd_terms and engine.X3_BWD_TERMS >= 2)
+                        add(conv.geom(), batch, ch, cw, 2, cp=xcp,
+                            terms=fwd_terms and engine.X3_BWD_TERMS >= 1)
                 h, w = oh, ow
         g6 = engine.aspp_geom(model.layer6)
         add(g6, batch, h, w, 0)

@@ -159,7 +159,8 @@ int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *
    argument of the _x forms takes one (NULL = build per call); it is valid for the weights it
    was built from until they are written — keeping that promise is the caller's side (the
    trainer rebuilds every pack once per step, adaptsegnet_amd.kernels.weight_pack_scope).  A
-   plan that ends on a kernel without a pack (misaligned operands) ignores it. */
+   plan that ends on a kernel without a pack (misaligned operands) ignores it;
+   adaptseg_conv2d_wpack rejects misaligned weights (ADAPTSEG_ERR_ARG). */
 int adaptseg_conv2d_wpack_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
 int adaptseg_conv2d_wpack(const adaptseg_conv_desc *d, int op, const float *const *w, void *pack, size_t bytes,
                           adaptseg_stream_t stream);

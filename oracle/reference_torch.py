@@ -324,7 +324,16 @@ def g_param_multiplicity(key):
 
 
 def make_optimizers(G, D1, D2, cfg):
-    """SGD(optim_parameters) + Adam x2 — train:532-540 (duplicate params, like the reference)."""
+    """SGD(optim_parameters) + Adam x2 — train:532-540 (duplicate params, like the reference).
+    DeeplabVGG (cfg gen "vgg"): optim_parameters is ``self.parameters()`` (deeplab_vgg.py:53-54),
+    one group, so adjust_learning_rate sets only group 0 (train:166-170)."""
+    if cfg.get("gen") == "vgg":
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            opt = torch.optim.SGD([t for t in G.values() if t.requires_grad], lr=cfg["learning_rate"],
+                                  momentum=cfg["momentum"], weight_decay=cfg["weight_decay"], foreach=False)
+        return opt, None, torch.optim.Adam([t for t in D2.values() if t.requires_grad],
+                                           lr=cfg["learning_rate_D"], betas=(0.9, 0.99), foreach=False)
     g0, g1 = [], []
     for k, t in G.items():
         if not (isinstance(t, torch.Tensor) and t.requires_grad):
@@ -371,7 +380,9 @@ def oracle_step(G, D1, D2, opts, cfg, i_iter, batches, bn_train=True):
 
     opt.zero_grad()
     lr = lr_poly(c["learning_rate"], i_iter, c["num_steps"], c["power"])
-    opt.param_groups[0]["lr"], opt.param_groups[1]["lr"] = lr, lr * 10
+    opt.param_groups[0]["lr"] = lr
+    if len(opt.param_groups) > 1:   # train:169-170
+        opt.param_groups[1]["lr"] = lr * 10
     lr_d = lr_poly(c["learning_rate_D"], i_iter, c["num_steps"], c["power"])
     for o in (opt_d1, opt_d2):
         if o is not None:
@@ -383,14 +394,20 @@ def oracle_step(G, D1, D2, opts, cfg, i_iter, batches, bn_train=True):
         tmode = "source" if c["level"] == "single-level" else "target"
     tsize = c["input_size"] if tmode == "source" else c["input_size_target"]
     src_lbl, tgt_lbl = 0, 1
+    if c.get("gen") == "vgg":   # DeeplabVGG returns one map, upsampled by the caller (interp)
+        def fwd(P, x, size, _train):
+            return None, F.interpolate(vgg_forward(P, x), size=(size[1], size[0]), mode="bilinear",
+                                       align_corners=True)
+    else:
+        fwd = g_forward
     for images, labels, images_t in batches:
         if c["level"] == "single-level":
             _set_rg(D2, False)
-            _, pred2 = g_forward(G, images, c["input_size"], bn_train)
+            _, pred2 = fwd(G, images, c["input_size"], bn_train)
             loss_seg2 = F.cross_entropy(pred2, labels, ignore_index=255)
             (loss_seg2 / n_sub).backward()
             acc("loss_seg2", loss_seg2.item() / n_sub)
-            _, pred_t2 = g_forward(G, images_t, tsize, bn_train)
+            _, pred_t2 = fwd(G, images_t, tsize, bn_train)
             l_adv = adv_loss(d_forward(D2, F.softmax(pred_t2, dim=1)), src_lbl, c["gan"])
             (c["lambda_adv_target2"] * l_adv / n_sub).backward()
             acc("loss_adv_target2", l_adv.item() / n_sub)

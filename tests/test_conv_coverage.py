@@ -28,7 +28,8 @@ def _step_products(config):
     tsize = src if level == "single-level" else tgt
     prods = set()
     prev = K.get_conv_math()
-    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32X3 if math == "f32x3" else K.MATH_F32)
+    # bench.CONFIGS "f32": the fp32 configs, which bench.py runs on the default F32X3 maths
+    K.set_conv_math(K.MATH_BF16 if math == "bf16" else K.MATH_F32X3)
     try:
         bench.conv_inventory(model, D, level, batch, src, tgt, tsize, products=prods)
     finally:

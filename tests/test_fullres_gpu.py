@@ -130,6 +130,58 @@ def test_fullres_c5_bf16_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monk
             assert torch.equal(da[k], db[k]), k
 
 
+def test_fullres_c4_vgg_step_vs_oracle():
+    """BASELINE config c4's program at its own geometry: DeeplabVGG (model/deeplab_vgg.py:24-54)
+    single-level Vanilla step (train:385-461, the map upsampled by the caller's interp), source and
+    target 1024x512, batch 1, against the fp32 oracle (R.vgg_forward, the restatement: DeeplabVGG
+    is unimportable here, so the composition is pinned by the restatement and the per-op goldens,
+    SURVEY.md §8c) from identical weights and inputs.  At this size the conv5 / fc6 / fc7 products
+    run unsplit with the in-kernel epilogue.  Losses within 1e-3 relative; the generator's update
+    (one SGD group, optim_parameters = parameters()) and D2's at cosine >= 0.99 (VGG has no BN:
+    the update is well conditioned); the classifier branches the forward never reaches keep no
+    gradient and no update in both."""
+    from adaptsegnet_amd.model import DeeplabVGG, FCDiscriminator
+    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    src = tgt = (1024, 512)
+    xs, lab, xt = _batch(src, tgt)
+    cfg = dict(level="single-level", gan="Vanilla", input_size=src, input_size_target=tgt, gen="vgg")
+    st = R.det_state(R.vgg_specs(), 4244)
+    P = R.to_torch(st, dtype=torch.float32, trainable=lambda k: True)
+    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
+    opts = R.make_optimizers(P, None, D2, R.DEFAULT_CFG | cfg)
+    ref = R.oracle_step(P, None, D2, opts, cfg, 0, [(xs, lab, xt)])
+    m = DeeplabVGG(19)
+    m.load_state_dict({k: torch.from_numpy(v.copy()).float() for k, v in st.items()})
+    m = m.to(DEV)
+    d2 = FCDiscriminator(num_classes=19)
+    d2.load_state_dict(_sd(R.d_specs(), 2002))
+    d2 = d2.to(DEV)
+    tr = AdaptSegTrainer(m, None, d2, StepConfig(level="single-level", input_size=src, input_size_target=tgt))
+    got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()
+    for k, v in ref.items():
+        print(f"c4 {k}: hip={got[k]:.6f} oracle={v:.6f}")
+        assert abs(got[k] - v) <= 1e-3 * abs(v) + 1e-6, (k, got[k], v)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    used = [k for k in P if not k.startswith(("classifier.conv2d_list.2", "classifier.conv2d_list.3"))]
+    for k in P:
+        if k not in used:
+            assert torch.equal(sd[k].double(), torch.from_numpy(st[k]).float().double()), k
+            assert torch.equal(P[k].detach().double(), torch.from_numpy(st[k]).float().double()), k
+    u_ref = torch.cat([(P[k].detach().double() - torch.from_numpy(st[k])).flatten() for k in used])
+    u_hip = torch.cat([(sd[k].double() - torch.from_numpy(st[k])).flatten() for k in used])
+    c = _cos(u_hip, u_ref)
+    print(f"c4 G update cosine {c:.6f}")
+    assert c >= 0.99, c
+    d0 = R.det_state(R.d_specs(), 2002)
+    dsd = d2.state_dict()
+    u_ref = torch.cat([(D2[k].detach().double() - torch.from_numpy(d0[k])).flatten() for k in D2])
+    u_hip = torch.cat([(dsd[k].double().cpu() - torch.from_numpy(d0[k])).flatten() for k in D2])
+    c = _cos(u_hip, u_ref)
+    print(f"c4 D2 update cosine {c:.6f}")
+    assert c >= 0.99, c
+
+
 def test_c1_forward_crossentropy2d_vs_oracle():
     """BASELINE config c1 at its own shape: DeeplabMulti forward (train-mode BN, single head)
     + utils/loss.py CrossEntropy2d on one 1x3x321x321 tensor (model/deeplab_multi.py:174-194,

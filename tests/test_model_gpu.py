@@ -343,6 +343,55 @@ def test_weight_packs_are_built_once_per_step_and_bitwise_neutral(data, math, mo
         K.set_conv_math(K.MATH_F32X3)
 
 
+def test_presplit_program_matches_default_step(data):
+    """The F32X3_PRESPLIT program (bench.py --conv-math f32x3_presplit: every Bottleneck product on
+    the term-image kernel, the BN passes writing / reading term images, the residual stream and
+    the BN3 mask source as terms, the ASPP tap-GEMM reading the last block's terms) against the
+    default F32X3 program: one multi-level train-BN step from identical weights — the same six
+    products per fp32 product, so losses within 1e-5 relative and every parameter group's update
+    within 1e-3 relative Frobenius (what differs is the K-split / summation order)."""
+    from adaptsegnet_amd import kernels as K
+    cfg = dict(level="multi-level", gan="Vanilla", input_size=(57, 41), input_size_target=(49, 33))
+    runs = []
+    for math in (K.MATH_F32X3, K.MATH_F32X3_PRESPLIT):
+        K.set_conv_math(math)
+        try:
+            runs.append(_run_hip("multi-level", "Vanilla", cfg, data, 1, bn_train=True))
+        finally:
+            K.set_conv_math(K.MATH_F32X3)
+    (ma, d1a, d2a, ga), (mb, d1b, d2b, gb) = runs
+    for k, v in ga[0].items():
+        assert abs(gb[0][k] - v) <= 1e-5 * abs(v) + 1e-7, (k, gb[0][k], v)
+    g0 = R.det_state(R.g_specs(), 1338)
+    G = R.to_torch(g0, trainable=R.g_trainable)
+    sa, sb = ma.state_dict(), mb.state_dict()
+    for gname, keys in _groups(G, "multi-level").items():
+        f, c = frob(_updates(None, keys, g0, sb), _updates(None, keys, g0, sa))
+        print(f"presplit vs default G/{gname}: rel {f:.2e} cos {c:.8f}")
+        assert f < 1e-3, (gname, f)
+    for (da, db), seed in (((d1a, d1b), 2001), ((d2a, d2b), 2002)):
+        d0 = R.det_state(R.d_specs(), seed)
+        ua = torch.cat([(da.state_dict()[k].double().cpu() - torch.from_numpy(d0[k])).flatten() for k in d0])
+        ub = torch.cat([(db.state_dict()[k].double().cpu() - torch.from_numpy(d0[k])).flatten() for k in d0])
+        f, _ = frob(ub, ua)
+        assert f < 1e-3, (seed, f)
+
+
+def test_weight_packs_go_with_their_model(data):
+    """The pack cache holds packs per weight tensor (weakly): once a model and its trainer are
+    dropped, its packs are freed (they used to stay allocated for the process)."""
+    import gc
+    from adaptsegnet_amd import kernels as K
+    K.clear_weight_packs()
+    cfg = dict(level="single-level", gan="Vanilla", input_size=(57, 41), input_size_target=(57, 41))
+    m, _d1, d2, _ = _run_hip("single-level", "Vanilla", cfg, data, 1, bn_train=True)
+    held = K.pack_count()
+    assert held > 0
+    del m, d2, _d1, _
+    gc.collect()
+    assert K.pack_count() == 0, K.pack_count()
+
+
 def test_weight_write_between_scopes_invalidates_the_packs(data):
     """A weight write the trainer does not see (through .data, which bypasses autograd's
     version counter) between two pack scopes is picked up: the second scope rebuilds every

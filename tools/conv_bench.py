@@ -19,7 +19,16 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from adaptsegnet_amd import engine  # noqa: E402
 from adaptsegnet_amd import kernels as K  # noqa: E402
+
+
+def _terms(t):
+    """The pixel-interleaved F32X3 term images [..., 3, C] of an fp32 NHWC tensor (bn.hip x3_off)."""
+    hi = t.to(torch.bfloat16)
+    r = t - hi.float()
+    mid = r.to(torch.bfloat16)
+    return torch.stack([hi, mid, (r - mid.float()).to(torch.bfloat16)], dim=-2).contiguous()
 
 
 def shapes(batch, W=1024, H=512):
@@ -106,12 +115,25 @@ def main():
         dbs = [torch.zeros_like(t) for t in bs] if has_bias else None
         pad_wgrad = g.cin % 4 != 0                     # D.conv1 (Cin 20), stem (Cin 4)
         xn = x.permute(0, 3, 1, 2) if x.dim() == 4 and x.shape[-1] == g.cin else x
+        # the products the engine runs on term images under F32X3 (engine.x3_forward_terms /
+        # X3_BWD_TERMS: the layer 3-4 conv2 forward, data and weight gradients), timed so
+        tf = st is None and engine.x3_forward_terms(g)
+        tb = tf and engine.X3_BWD_TERMS >= 2
+        tw = tf and engine.X3_BWD_TERMS >= 1
+        xt = _terms(x) if tf or tw else None
+        dyt = _terms(dy) if tb or tw else None
         for op in ops:
             def run():
-                if op == 0:
+                if op == 0 and tf:
+                    K.conv_fwd(g, None, n, h, w, ws, bs, xb=xt)
+                elif op == 0:
                     K.conv_fwd(g, x, n, h, w, ws, bs, strides=st)
+                elif op == 1 and tb:
+                    K.conv_dgrad(g, None, n, h, w, ws, dyb=dyt)
                 elif op == 1:
                     K.conv_dgrad(g, dy, n, h, w, ws)
+                elif op == 2 and tw:
+                    K.conv_wgrad(g, None, None, n, h, w, dws, dbs, dyb=dyt, xb=xt)
                 elif pad_wgrad:
                     c4 = (g.cin + 3) // 4 * 4
                     xp = K.to_nhwc_pad(xn, c4)
@@ -144,7 +166,7 @@ def main():
                 c4 = (g.cin + 3) // 4 * 4
                 sel, sp = K.conv_kernel_id(dataclasses.replace(g, cin=c4), n, h, w, op, K.nhwc_strides(n, h, w, c4))
             else:
-                sel, sp = K.conv_kernel_id(g, n, h, w, op, st)
+                sel, sp = K.conv_kernel_id(g, n, h, w, op, st, copies=(tf, tb, tw)[op])
             c = count[op] if isinstance(count, dict) else count
             tot_ms += ms * c
             tot_fl += fl * c
