@@ -146,20 +146,14 @@ constexpr int kReduceUnroll = 4;
 // rows in flight per thread of the bf16-storage passes (two quads a row): 2 rows at <= 128
 // VGPRs beat 4 rows at ~200 (c5 40.90 / 40.95 vs 40.57 / 40.63 images/s, one quad x 4 rows
 // 38.06 / 38.21; experiments/ab_bn_bf16.sh)
-#ifndef ADAPTSEG_BN_BF16_ROWS
-#define ADAPTSEG_BN_BF16_ROWS 2
-#endif
-constexpr int kBf16Rows = ADAPTSEG_BN_BF16_ROWS;
+constexpr int kBf16Rows = 2;
 // The BN passes run beside the weight-gradient GEMMs of the side stream.  A term-image F32X3
 // block (conv_x3r.hpp: 8 waves at ~200 VGPRs, one per CU) leaves 96 VGPRs per SIMD free, so
 // under the F32X3_PRESPLIT program the BN blocks fit beside it only at <= 96 VGPRs
-// (ADAPTSEG_BN_MIN_BLOCKS=5 with ADAPTSEG_BN_APPLY_UNROLL=2: 26.79 vs 26.50 images/s there).
-// The default program (register-staged F32X3 convs) runs faster with the x4-unrolled passes at
-// their natural ~126 VGPRs: 27.44 vs 27.18 images/s (profiles/r3/x3_copies_ab.txt).
-#ifndef ADAPTSEG_BN_MIN_BLOCKS
-#define ADAPTSEG_BN_MIN_BLOCKS 1
-#endif
-constexpr int kBnMinBlocks = ADAPTSEG_BN_MIN_BLOCKS;
+// (min 5 blocks with x2 unrolled rows: 26.79 vs 26.50 images/s there).  The default program
+// runs faster with the x4-unrolled passes at their natural ~126 VGPRs: 27.44 vs 27.18 images/s
+// (profiles/r3/x3_copies_ab.txt).
+constexpr int kBnMinBlocks = 1;
 // ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
 // GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
 constexpr int kReduceBlocks = 512, kApplyBlocks = 512;
@@ -173,9 +167,10 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
 
 // Block = 256 threads laid out as TC channel groups (QN quads each) x TR row lanes (TC*TR =
 // 256).  Grid = (ceil(C / (4*QN*TC)), splits).  Partial sums land in ws[2][C][splits] (float).
-template <int MODE, typename TX, typename TY = TX, int QN = 1>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
+// TD: storage of the incoming gradient dy (fp32, or bf16 under bf16 gradient storage)
+template <int MODE, typename TX, typename TY = TX, int QN = 1, typename TD = float>  // MODE 0: stats (shifted by pivot x[0][c]), 1: backward sums
 __global__ void __launch_bounds__(256, kBnMinBlocks)
-bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const float *__restrict__ dy,
+bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const TD *__restrict__ dy,
                  typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
                  int64_t rows_per_split, float *__restrict__ partial) {
@@ -427,13 +422,13 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
 // loads its channels' parameters once and walks rows (no per-element channel modulo); rows
 // are unrolled x4 with all loads issued before any store (dx / dres / y may alias dy / x:
 // every element is still read before it is written, by the same thread).
-#ifndef ADAPTSEG_BN_APPLY_UNROLL
-#define ADAPTSEG_BN_APPLY_UNROLL 4
-#endif
-constexpr int kApplyUnroll = ADAPTSEG_BN_APPLY_UNROLL;
+constexpr int kApplyUnroll = 4;
 
 __device__ __forceinline__ float4 ld4c(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// a gradient quad stored fp32, or bf16 (RNE) under bf16 gradient storage
+__device__ __forceinline__ void stg4(float *p, float4 v) { st4(p, v); }
+__device__ __forceinline__ void stg4(__bf16 *p, float4 v) { *reinterpret_cast<uint2 *>(p) = bf16x4_rne(v); }
 
 template <int QN> __device__ __forceinline__ void stq(float *p, const float4 (&v)[QN]) {
 #pragma unroll
@@ -501,12 +496,12 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
   }
 }
 
-template <typename TX, typename TY = TX, int QN = 1>
+template <typename TX, typename TY = TX, int QN = 1, typename TD = float>
 __global__ void __launch_bounds__(256, kBnMinBlocks)
-bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy, typename Act<TY>::ptr y,
+bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TD *dy, typename Act<TY>::ptr y,
                       const TX *x, const float *__restrict__ w, const float *__restrict__ b,
                       const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,
-                      float *dx, uint2 *dxb, float *dres, int rmode, int train, bool terms = false) {
+                      float *dx, uint2 *dxb, TD *dres, int rmode, int train, bool terms = false) {
   if constexpr (QN == 1) {   // (the grouped body below takes 130 VGPRs here: 3 waves per SIMD)
     const int tr = 256 / tc;
     const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
@@ -527,7 +522,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
       for (int u = 0; u < U; ++u) {
         const int64_t ru = r + (int64_t)u * tr;
         const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
-        g[u] = ld4c(dy + e);
+        g[u] = lda4(dy + e);
         v[u] = train ? lda4(x + e) : z4;
         o4[u] = need_y ? ldm4<TY>(y, row, c0, C) : z4;
       }
@@ -553,7 +548,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
           gg.z = o.z > 0.f ? gg.z : k * gg.z;
           gg.w = o.w > 0.f ? gg.w : k * gg.w;
         }
-        if (dres) st4(dres + e, gg);
+        if (dres) stg4(dres + e, gg);
         float4 out;
         if (train) {
           out.x = ww.x * is.x * (gg.x - mg.x - (v[u].x - m.x) * is.x * mgx.x);
@@ -620,7 +615,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const float *dy,
             gg.z = o.z > 0.f ? gg.z : k * gg.z;
             gg.w = o.w > 0.f ? gg.w : k * gg.w;
           }
-          if (dres) st4(dres + e + 4 * h, gg);
+          if (dres) stg4(dres + e + 4 * h, gg);
           const float4 W = ww[h], I = is[h], M = m[h], G = mg[h], X = mgx[h];
           if (train) {
             out[h].x = W.x * I.x * (gg.x - G.x - (vv.x - M.x) * I.x * X.x);
@@ -710,10 +705,10 @@ static int grid_for(int64_t total4) { return (int)std::min<int64_t>(ceil_div(tot
 
 namespace adaptseg {
 
-template <typename TX, typename TY, int QN>
-static void bn_bwd_kernels(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y, const TX *x,
+template <typename TX, typename TY, int QN, typename TD>
+static void bn_bwd_kernels(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, const TX *x,
                            const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
-                           float *dx, uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight,
+                           float *dx, uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight,
                            float *dbias, float *partial, float *coef, double reduce_bytes, double apply_bytes,
                            bool dterms, hipStream_t s) {
   int slot;
@@ -722,10 +717,10 @@ static void bn_bwd_kernels(int64_t rows, int c, const float *dy, typename Act<TY
     const ReducePlan r = reduce_plan(rows, c, rqn);
     timing_begin(kTBnReduceBwd, s, reduce_bytes, &slot);
     if (rqn == 2)
-      bn_reduce_kernel<1, TX, TY, QN><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
+      bn_reduce_kernel<1, TX, TY, QN, TD><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
           rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
     else
-      bn_reduce_kernel<1, TX, TY, 1><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
+      bn_reduce_kernel<1, TX, TY, 1, TD><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
           rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
     timing_end(slot, s);
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd, coef,
@@ -733,16 +728,16 @@ static void bn_bwd_kernels(int64_t rows, int c, const float *dy, typename Act<TY
   }
   timing_begin(kTBnBwdApply, s, apply_bytes, &slot);
   const ApplyPlan ap = apply_plan(rows, c, QN);
-  bn_bwd_apply2d_kernel<TX, TY, QN><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
+  bn_bwd_apply2d_kernel<TX, TY, QN, TD><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
       rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
       reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms);
   timing_end(slot, s);
 }
 
-template <typename TX, typename TY = TX>
-int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
+template <typename TX, typename TY = TX, typename TD = float>
+int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
                          const float *bias, const float *save_mean, const float *save_invstd, float *dx,
-                         uint16_t *dx_bf16, float *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
+                         uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
                          size_t ws_bytes, hipStream_t s) {
   float *partial = reinterpret_cast<float *>(ws), *coef = nullptr;
   const double eb = sizeof(TX);   // bytes per activation element (x)
@@ -760,20 +755,21 @@ int bn_bwd_launch(int64_t rows, int c, const float *dy, typename Act<TY>::ptr y,
   }
   // reduce: dy, x (+ y for the mask from y) in; apply: dy, x (train), y (mask from y) in; dx,
   // dres out
-  const double reduce_bytes = (4.0 + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
-  const double apply_bytes = (4.0 * (1 + (dx ? 1 : 0) + (dres ? 1 : 0)) + eb * (train ? 1 : 0) +
+  const double db = sizeof(TD);    // bytes per gradient element (dy, dres)
+  const double reduce_bytes = (db + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
+  const double apply_bytes = (db * (1 + (dres ? 1 : 0)) + 4.0 * (dx ? 1 : 0) + eb * (train ? 1 : 0) +
                               ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
                              (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0);
   if constexpr (sizeof(TX) == 2 && !std::is_same<TY, X3>::value) {
     if (qn == 2) {
-      bn_bwd_kernels<TX, TY, 2>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+      bn_bwd_kernels<TX, TY, 2, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
+                                    train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
       AS_CHECK_LAUNCH("bn_bwd");
       return ADAPTSEG_OK;
     }
   }
-  bn_bwd_kernels<TX, TY, 1>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
-                            dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+  bn_bwd_kernels<TX, TY, 1, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
+                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
   AS_CHECK_LAUNCH("bn_bwd");
   return ADAPTSEG_OK;
 }
@@ -839,6 +835,8 @@ static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_
                                                         weight, bias, rb, y, yb, relu, terms);
 }
 
+static constexpr const float *kNoDy = nullptr;   // the statistics pass reads no gradient
+
 int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
                             const float *bias, float *running_mean, float *running_var, float momentum, float eps,
                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
@@ -864,13 +862,13 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
   timing_begin(kTBnReduceStats, s, eb * rows * c, &slot);
   const __bf16 *xb = reinterpret_cast<const __bf16 *>(x_bf16);
   if (x)
-    bn_reduce_kernel<0, float><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, nullptr, nullptr, nullptr,
+    bn_reduce_kernel<0, float><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, x, kNoDy, nullptr, nullptr,
                                                                        nullptr, nullptr, nullptr, 0, r.per, partial);
   else if (r2.splits)
     bn_reduce_kernel<0, __bf16, __bf16, 2><<<dim3(r2.cblocks, r2.splits), 256, 0, s>>>(
-        rows, c, r2.tc, xb, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, r2.per, partial);
+        rows, c, r2.tc, xb, kNoDy, nullptr, nullptr, nullptr, nullptr, nullptr, 0, r2.per, partial);
   else
-    bn_reduce_kernel<0, __bf16><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, xb, nullptr, nullptr, nullptr,
+    bn_reduce_kernel<0, __bf16><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(rows, c, r.tc, xb, kNoDy, nullptr, nullptr,
                                                                         nullptr, nullptr, nullptr, 0, r.per, partial);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_reduce<stats>");
@@ -961,14 +959,20 @@ int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weig
                                  nullptr, relu, stream);
 }
 
-static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, const uint16_t *y_bf16, const float *x,
-                       const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
-                       const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
-                       float *dweight, float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const float *y,
+                       const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
+                       const float *bias, const float *save_mean, const float *save_invstd, float *dx, uint16_t *dx_bf16,
+                       float *dres, uint16_t *dres_bf16, int relu, int train, float *dweight, float *dbias, void *ws,
+                       size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
   const bool xb = x_bf16 != nullptr, terms = copies_are_terms();
-  AS_CHECK_ARG(dy && (dx || dx_bf16) && save_invstd && (!train || ((x || x_bf16) && save_mean)), "bn_bwd: null pointer");
+  AS_CHECK_ARG((dy != nullptr) != (dy_bf16 != nullptr), "bn_bwd: exactly one of dy / dy_bf16");
+  AS_CHECK_ARG((dx || dx_bf16) && save_invstd && (!train || ((x || x_bf16) && save_mean)), "bn_bwd: null pointer");
   AS_CHECK_ARG(!(x && x_bf16) && !(y && y_bf16), "bn_bwd: one pointer each for the saved x and y");
+  // bf16 gradient storage: dres is stored like dy; only with bf16 activation storage
+  AS_CHECK_ARG(dy ? !dres_bf16 : !dres, "bn_bwd: dres is stored like dy (fp32 or bf16)");
+  AS_CHECK_ARG(!dy_bf16 || (!terms && (xb || (!x && y_bf16))),
+               "bn_bwd: a bf16 dy needs bf16 activation storage (BF16 conv maths)");
   if (terms)   // F32X3 maths: x fp32, y fp32 or its three term images
     AS_CHECK_ARG(!xb, "bn_bwd: under the F32X3 conv maths x is fp32 (y may be term images)");
   else
@@ -985,10 +989,16 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
     return bn_bwd_launch<float, X3>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), x, weight, bias,
                                     save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
                                     ws_bytes, s);
-  if (xb || (!x && y_bf16))
-    return bn_bwd_launch<__bf16>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16),
-                                 reinterpret_cast<const __bf16 *>(x_bf16), weight, bias, save_mean, save_invstd, dx,
-                                 dx_bf16, dres, rmode, train, dweight, dbias, ws, ws_bytes, s);
+  if (xb || (!x && y_bf16)) {
+    const __bf16 *yb = reinterpret_cast<const __bf16 *>(y_bf16), *xbb = reinterpret_cast<const __bf16 *>(x_bf16);
+    if (dy_bf16)
+      return bn_bwd_launch<__bf16, __bf16, __bf16>(rows, c, reinterpret_cast<const __bf16 *>(dy_bf16), yb, xbb, weight,
+                                                   bias, save_mean, save_invstd, dx, dx_bf16,
+                                                   reinterpret_cast<__bf16 *>(dres_bf16), rmode, train, dweight, dbias,
+                                                   ws, ws_bytes, s);
+    return bn_bwd_launch<__bf16>(rows, c, dy, yb, xbb, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
+                                 train, dweight, dbias, ws, ws_bytes, s);
+  }
   return bn_bwd_launch<float>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
                               dweight, dbias, ws, ws_bytes, s);
 }
@@ -996,16 +1006,25 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const float *y, con
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, float *dx, float *dres,
                     int relu, int train, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  return bn_bwd_impl(rows, c, dy, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr, dres, relu,
-                     train, nullptr, nullptr, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, nullptr, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr,
+                     dres, nullptr, relu, train, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, const uint16_t *y_bf16, const float *x,
                       const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
                       const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
                       void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
-  return bn_bwd_impl(rows, c, dy, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, relu,
-                     train, nullptr, nullptr, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, nullptr, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres,
+                     nullptr, relu, train, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const float *y,
+                       const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
+                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
+                       uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
+                       size_t ws_bytes, adaptseg_stream_t stream) {
+  return bn_bwd_impl(rows, c, dy, dy_bf16, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16,
+                     dres, dres_bf16, relu, train, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,
@@ -1013,8 +1032,8 @@ int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y,
                            const float *save_invstd, float *dx, float *dres, int act, float *dweight,
                            float *dbias, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   AS_CHECK_ARG(dweight || dbias, "bn_bwd_affine: no affine gradient requested");
-  return bn_bwd_impl(rows, c, dy, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr, dres, act,
-                     1, dweight, dbias, ws, ws_bytes, stream);
+  return bn_bwd_impl(rows, c, dy, nullptr, y, nullptr, x, nullptr, weight, bias, save_mean, save_invstd, dx, nullptr,
+                     dres, nullptr, act, 1, dweight, dbias, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

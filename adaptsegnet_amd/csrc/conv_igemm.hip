@@ -48,14 +48,21 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
           if (bp) v += bp[col];
         }
       }
-      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
-      if (p.flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
+      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) v += epi_prev(p, idx);
+      if (p.flags & ADAPTSEG_EPI_RESIDUAL) v += epi_res(p, idx);
       v = epi_act(v, p.flags);
       if (p.flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], p.flags);
       if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
       if (p.outb) p.outb[idx] = (__bf16)v;
     }
   }
+}
+
+// four bf16 (8-B aligned) as a float4
+__device__ __forceinline__ float4 ldbf4(const __bf16 *p) {
+  const uint2 u = *reinterpret_cast<const uint2 *>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
 }
 
 // Vectorised split-K reduction: 4 consecutive columns per thread (N % 4 == 0 and, for weight
@@ -95,7 +102,8 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
     if (i >= total4) continue;
     const uint32_t row = fdiv(i, fdn4);
     const int col = (int)(i - row * n4) * 4;
-    float *o;
+    float *o = nullptr;
+    size_t idx = 0;
     if (mode == MODE_WGRAD) {
       const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
       float *dst = seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3];
@@ -105,8 +113,8 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
     } else {
-      const size_t idx = (size_t)row * p.N + col;
-      o = p.out + idx;
+      idx = (size_t)row * p.N + col;
+      o = p.out ? p.out + idx : nullptr;   // NULL: bf16 storage, the output is p.outb
       if (mode == MODE_FWD) {
         for (int s = 0; s < p.nseg; ++s) {
           const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
@@ -117,11 +125,11 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
         }
       }
       if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
-        const float4 a = *reinterpret_cast<const float4 *>(o);
+        const float4 a = o ? *reinterpret_cast<const float4 *>(o) : ldbf4(p.outb + idx);
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
       if (p.flags & ADAPTSEG_EPI_RESIDUAL) {
-        const float4 a = *reinterpret_cast<const float4 *>(p.res + idx);
+        const float4 a = p.resb ? ldbf4(p.resb + idx) : *reinterpret_cast<const float4 *>(p.res + idx);
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
       v.x = epi_act(v.x, p.flags); v.y = epi_act(v.y, p.flags);
@@ -132,9 +140,9 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
         v.z = epi_act_grad(v.z, a.z, p.flags); v.w = epi_act_grad(v.w, a.w, p.flags);
       }
     }
-    if (mode == MODE_WGRAD || p.out) *reinterpret_cast<float4 *>(o) = v;   // p.out NULL: bf16 storage
+    if (o) *reinterpret_cast<float4 *>(o) = v;   // (NULL: bf16 storage, only the copy below)
     if (mode != MODE_WGRAD && p.outb) {
-      __bf16 *ob = p.outb + (o - p.out);
+      __bf16 *ob = p.outb + idx;
       ob[0] = (__bf16)v.x; ob[1] = (__bf16)v.y; ob[2] = (__bf16)v.z; ob[3] = (__bf16)v.w;
     }
   }
@@ -385,37 +393,35 @@ void set_splits(Plan &pl) {
   // F32X3 weight gradients (side stream) split to ~384 blocks (1.5 per CU), not 512: a full
   // 2-per-CU grid of 16-wave blocks holds every CU for a whole split, and the main stream's
   // short BN / split-K kernels then wait for CU slots.  384 measured c2 +2.4 %, c3 +2.6 %
-  // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2, tools/dbg/ab_bench_many.sh).
-#ifndef ADAPTSEG_X3_WGRAD_TARGET
-#define ADAPTSEG_X3_WGRAD_TARGET 384
-#endif
-  constexpr int kX3WgradTarget = ADAPTSEG_X3_WGRAD_TARGET;
+  // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2).  Rounding the split count to
+  // nearest instead of down measured -0.2..-0.8 % (profiles/r3/x3_wgrad_split_rounding_ab.txt).
+  constexpr int kX3WgradTarget = 384;
   // The LDS-DMA bf16 weight gradient (side stream) to ~256 blocks: half the split-K slab
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
   constexpr int kG16WgradTarget = 256;
-  // The term-image F32X3 weight gradient (one 8-wave block per CU, side stream): its blocks hold
-  // their CUs against the main stream's term-image convs (neither fits beside the other), so
-  // more, shorter blocks let the main chain in sooner.
-#ifndef ADAPTSEG_X3R_WGRAD_TARGET
-#define ADAPTSEG_X3R_WGRAD_TARGET 256
-#endif
-  constexpr int kX3rWgradTarget = ADAPTSEG_X3R_WGRAD_TARGET;
-  const int target = (pl.mode == MODE_WGRAD && pl.x3r) ? kX3rWgradTarget
-                     : (pl.mode == MODE_WGRAD && pl.g16) ? kG16WgradTarget
+  // (the term-image F32X3 weight gradient picks its own split count below)
+  const int target = (pl.mode == MODE_WGRAD && pl.g16) ? kG16WgradTarget
                      : (pl.mode == MODE_WGRAD && pl.x3)            ? kX3WgradTarget
                                                                    : kSplitTarget;
   // the LDS-DMA bf16 / x3r kernels run one block per CU: split only grids under half the CUs
   const int split_below = pl.mode == MODE_WGRAD ? target : pl.x3r ? 256 : pl.g16 ? 128 : 257;
   int splits = 1;
-  if (pl.tiles < split_below && !pl.s2) {
-#ifndef ADAPTSEG_X3_WGRAD_ROUND_NEAREST
-#define ADAPTSEG_X3_WGRAD_ROUND_NEAREST 0
-#endif
-    if (ADAPTSEG_X3_WGRAD_ROUND_NEAREST && pl.mode == MODE_WGRAD && pl.x3 && !pl.x3r)
-      splits = std::max(1, (target + pl.tiles / 2) / pl.tiles);
-    else
-      splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
+  if (pl.mode == MODE_WGRAD && pl.x3r) {
+    // one 8-wave block per CU: the grid takes ceil(tiles * s / 256) rounds of 1/s of the K range,
+    // so pick the split count s (<= 16, >= 32 K steps each) with the fewest such units — e.g.
+    // layer4.conv2 (144 tiles of 128 rows): s = 1 leaves 112 CUs idle for the whole launch
+    // (MFMA busy 0.315 in isolation), s = 7 runs 4 rounds of 1/7 (0.57 of the s = 1 time)
+    double best = 1e30;
+    for (int s = 1; s <= 16 && (s == 1 || nkt / s >= 32); ++s) {
+      const double t = (double)ceil_div((int64_t)pl.tiles * s, 256) / s;
+      if (t < best * 0.97) {
+        best = t;
+        splits = s;
+      }
+    }
+  } else if (pl.tiles < split_below && !pl.s2) {
+    splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -423,26 +429,10 @@ void set_splits(Plan &pl) {
   splits = (int)ceil_div(nkt, per);
   p.splits = splits;
   p.ktiles_per_split = per;
-  // split-K slabs + one arrival counter per output tile (folded epilogue), 256-B aligned
-  pl.slab_bytes = splits > 1 ? splitk_slab_bytes(pl) + (sizeof(unsigned) * (size_t)pl.tiles + 255) / 256 * 256 : 0;
+  pl.slab_bytes = splits > 1 ? splitk_slab_bytes(pl) : 0;
   if (pl.bf16) pl.slab_bytes += bf16_pre_bytes(pl);
   if (pl.x3) pl.slab_bytes += x3_pre_bytes(pl);
 }
-
-// 256x256 bf16 LDS-DMA tiles (conv_bf16g.hpp), built but off: one 8-wave
-// block per CU hides the DMA ring's latency worse than two 128x256 blocks — per shape slower
-// (l3.conv3 fwd 44.6 -> 57.0 us, l3.ds fwd 60.1 -> 71.0), c5 41.22 / 41.33 images/s off vs
-// 37.27 / 37.25 with both, 40.28 / 40.30 with the weight gradients only, same box
-// (profiles/r3/bf16_wide_tiles_ab.txt).  -DADAPTSEG_G16_WIDE_MIN_TILES=256 /
-// -DADAPTSEG_G16_WIDE_WGRAD=1 build them (tests/test_bf16_gpu.py::test_bf16_wide_tile_products).
-#ifndef ADAPTSEG_G16_WIDE_MIN_TILES
-#define ADAPTSEG_G16_WIDE_MIN_TILES 0
-#endif
-constexpr int64_t kG16WideMinTiles = ADAPTSEG_G16_WIDE_MIN_TILES;   // 0: no 256x256 tiles
-#ifndef ADAPTSEG_G16_WIDE_WGRAD
-#define ADAPTSEG_G16_WIDE_WGRAD 0
-#endif
-constexpr bool kG16WideWgrad = ADAPTSEG_G16_WIDE_WGRAD;   // 256x256 bf16 weight-gradient tiles
 
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
   int st = validate(d);
@@ -549,33 +539,11 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = d->k >= 256 ? 256 : 128;
     }
     // F32X3_PRESPLIT: every such product on the term-image kernel, the images made per call
-    // unless the caller supplies them; F32X3 (default): on it only when the caller does (x3_terms)
+    // unless the caller supplies them; F32X3 (default): on it only when the caller does (x3_terms:
+    // the engine's layer 3-4 conv2 products, whose term images the BN passes write).  Per-call
+    // images under F32X3 measured slower for the multi-tap weight gradients (c2 -1.4 %,
+    // profiles/r3/x3r_wgrad_taps_ab.txt); experiments/r3_rejected.patch keeps that build.
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
-#ifndef ADAPTSEG_X3R_WGRAD_TAPS
-#define ADAPTSEG_X3R_WGRAD_TAPS 0
-#endif
-    // F32X3 (default) multi-tap weight gradients on the 128-row term-image kernel, the images
-    // made per call on the side stream: 9 taps amortise the copies (a 1x1 weight gradient's
-    // copies cost more than the kernel saves), and a 96 KB / <=128-VGPR block leaves room on
-    // its CU for one register-staged main-stream block (the 256-row one does not).  Off: the
-    // step is bound by the main stream's chain, which this leaves as is — same box, c2 26.75 /
-    // 26.74 img/s off vs 26.38 / 26.32 on (target 384: 26.25 / 26.22), c3 17.18 / 17.18 vs
-    // 16.88 / 16.91 (profiles/r3/x3r_wgrad_taps_ab.txt)
-    if (ADAPTSEG_X3R_WGRAD_TAPS && pl.x3 && op == ADAPTSEG_CONV_BWD_WEIGHT && pl.x3r_ok &&
-        d->kh * d->kw > 1 && conv_math() == ADAPTSEG_MATH_F32X3) {
-      pl.x3g = pl.x3r = true;
-      pl.x3r_bm = 128;
-    }
-#ifndef ADAPTSEG_X3R_FWD_PERCALL
-#define ADAPTSEG_X3R_FWD_PERCALL 0
-#endif
-    // F32X3 (default) forwards of wide multi-tap convs (Cin >= 256, >= 9 taps: DeeplabVGG
-    // conv3-5, D.conv4) on the term-image kernel with the images made per call (a read of 4 B and
-    // a write of 6 B per input element against K >= 2304 of GEMM per output element); the
-    // Bottleneck conv2 forwards get them from BN1 instead (engine.x3_forward_terms)
-    if (ADAPTSEG_X3R_FWD_PERCALL && pl.x3 && op == ADAPTSEG_CONV_FWD && pl.x3r_ok && d->kh * d->kw >= 9 &&
-        d->c >= 256 && conv_math() == ADAPTSEG_MATH_F32X3)
-      pl.x3g = pl.x3r = true;
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
@@ -595,20 +563,15 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
-      // 256x256x32 (half the operand bytes per MFMA of 128x256; one block per CU) where such
-      // tiles still give every CU one
-      if (kG16WideMinTiles > 0 && !pl.s2 && p.N >= 256 &&
-          ceil_div(p.M, 256) * ceil_div(p.N, 256) >= kG16WideMinTiles) {
-        pl.g16_bm = pl.g16_bn = 256;
-        pl.g16_bk = 32;
-      }
+      // (256x256x32 tiles, one block per CU, measured slower: c5 -10 % / -2.4 % with the weight
+      // gradients only, profiles/r3/bf16_wide_tiles_ab.txt; experiments/r3_rejected.patch)
     }
     // weight gradients with 16-B channel chunks (Cin % 8 == 0, Cout % 8 == 0) on the LDS-DMA
     // weight-gradient kernel: {128,256}x128 tiles, K steps of 32 output pixels
     if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 8 == 0 && d->k % 8 == 0) {
       pl.g16 = true;
       pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
-      pl.g16_bn = (kG16WideWgrad && d->k >= 256 && p.N >= 256) ? 256 : 128;   // 256x256: x once per row tile
+      pl.g16_bn = 128;
       pl.g16_bk = 32;
     }
   }
@@ -627,9 +590,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 int kernel_id(const Plan &pl, int mode) {
   // 88 / 89: the FAST cfg-8 stride-2 ids, which never occur (cfg 8 has no stride-2 form)
   if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
-  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bn == 256 ? 82 : pl.g16_bm == 256 ? 98 : 99);
+  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
-  if (pl.g16 && pl.g16_bm == 256 && pl.g16_bn == 256) return 100 * mode + 82;   // (a free FAST id: cfg 7 ends at 81)
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
@@ -638,16 +600,12 @@ int kernel_id(const Plan &pl, int mode) {
   return 100 * mode + 10 * pl.cfg + (pl.va ? 2 : 0) + (pl.vb ? 1 : 0);
 }
 
-// Split-K outputs: the operands of the final sum are 16-byte aligned float4 rows (the folded
-// epilogue and splitk_reduce4_kernel both need that; else the scalar splitk_reduce_kernel).
-// ADAPTSEG_SPLITK_FOLD=1 builds the in-kernel fold (splitk_fold, conv_kernels.hpp): the last
-// split to arrive at a tile sums every slab of it.  Measured and rejected (same box, two
-// alternating runs each, profiles/r3/splitk_fold_ab.txt): c2 25.86 vs 26.66 images/s, c5 35.70
-// vs 38.56 — a 128x128 fp32 slab is 64 KB, so one reducer block reads splits x 64 KB (0.6-1 MB)
-// serially at the tail of the launch, where the separate reduce spreads it over the chip.
-#ifndef ADAPTSEG_SPLITK_FOLD
-#define ADAPTSEG_SPLITK_FOLD 0
-#endif
+// Split-K outputs: the operands of the final sum are 16-byte aligned float4 rows for
+// splitk_reduce4_kernel (else the scalar splitk_reduce_kernel).  Folding the sum into the
+// last-arriving split (per-tile arrival counter) measured slower — c2 25.86 vs 26.66 images/s,
+// c5 35.70 vs 38.56 (profiles/r3/splitk_fold_ab.txt): a 128x128 fp32 slab is 64 KB, so one
+// reducer block reads splits x 64 KB serially at the tail of the launch, where the separate
+// reduce spreads it over the chip (experiments/r3_rejected.patch keeps that build).
 
 static bool splitk_vec(const ConvParams &q, const float *slab, const float *final_out, int mode) {
   bool vec = q.N % 4 == 0 && aligned16(slab);
@@ -655,7 +613,8 @@ static bool splitk_vec(const ConvParams &q, const float *slab, const float *fina
     vec = vec && q.kseg % 4 == 0;
     for (int g = 0; g < q.nseg; ++g) vec = vec && aligned16(q.dw[g]);
   } else {
-    vec = vec && aligned16(final_out) && (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res)) &&
+    vec = vec && aligned16(final_out) && aligned16(q.outb) &&
+          (!(q.flags & ADAPTSEG_EPI_RESIDUAL) || aligned16(q.res ? (const void *)q.res : (const void *)q.resb)) &&
           (!(q.flags & kEpiActGrad) || aligned16(q.aux));
     if (mode == MODE_FWD)
       for (int g = 0; g < q.nseg; ++g) vec = vec && (!q.bias[g] || aligned16(q.bias[g]));
@@ -665,8 +624,6 @@ static bool splitk_vec(const ConvParams &q, const float *slab, const float *fina
 
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
-  pl.p.tile_ctr = nullptr;
-  pl.p.fold_out = final_out;
   if (!ws || ws_bytes < pl.slab_bytes) {
     if (pl.slab_bytes) {
       set_error("conv: workspace %zu < required %zu", ws_bytes, pl.slab_bytes);
@@ -676,23 +633,9 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   // workspace: [weight pack / operand copies (F32X3, bf16)][split-K slabs][tile counters]
   const size_t pre = pl.x3 ? x3_pre_bytes(pl) : pl.bf16 ? bf16_pre_bytes(pl) : 0;
   float *slab = nullptr;
-  bool fold = false;
   if (pl.p.splits > 1) {
     slab = reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + pre);
     pl.p.out = slab;
-    // the weight gradients of every kernel with the shared igemm_epilogue (the FAST / bf16 /
-    // F32X3 families) fold the split-K sum into their last-arriving split; the generic kernel
-    // and the (few) split forward / data gradients keep the reduce launch
-    fold = ADAPTSEG_SPLITK_FOLD && mode == MODE_WGRAD && pl.fast && splitk_vec(pl.p, slab, final_out, mode);
-    if (fold) {
-      unsigned *ctr = reinterpret_cast<unsigned *>(reinterpret_cast<char *>(slab) + splitk_slab_bytes(pl));
-      const hipError_t me = hipMemsetAsync(ctr, 0, sizeof(unsigned) * (size_t)pl.tiles, s);
-      if (me != hipSuccess) {
-        set_error("conv: tile-counter memset: %s", hipGetErrorString(me));
-        return ADAPTSEG_ERR_HIP;
-      }
-      pl.p.tile_ctr = ctr;
-    }
   }
   hipError_t e;
   int slot;
@@ -716,7 +659,7 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     set_error("igemm launch: %s", hipGetErrorString(e));
     return ADAPTSEG_ERR_HIP;
   }
-  if (pl.p.splits > 1 && !fold) {
+  if (pl.p.splits > 1) {
     ConvParams q = pl.p;
     q.out = final_out;
     const size_t total = (size_t)q.M * q.N;
@@ -1074,14 +1017,30 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                const float *const *w, const void *w_pack, const float *res, const float *aux,
                                float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
                                adaptseg_stream_t stream) {
+  AS_CHECK_ARG(dx, "conv bwd_data: null dx (bf16-only outputs: adaptseg_conv2d_bwd_data_xg)");
+  return adaptseg_conv2d_bwd_data_xg(d, dy, dy_bf16, w, w_pack, res, nullptr, aux, dx, dx_bf16, flags, ws, ws_bytes,
+                                     stream);
+}
+
+int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
+                                const float *aux, float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
+                                adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
-  AS_CHECK_ARG((dy || dy_bf16) && w && dx, "conv bwd_data: null pointer");
+  AS_CHECK_ARG((dy || dy_bf16) && w && (dx || dx_bf16), "conv bwd_data: null pointer");
+  AS_CHECK_ARG(!(res && res_bf16), "conv bwd_data: one residual pointer");
+  // bf16 gradient storage (BF16 maths): the residual and / or the output as bf16 tensors
+  const bool gb = res_bf16 || !dx;
+  AS_CHECK_ARG(!gb || !copies_are_terms(), "conv bwd_data: bf16 gradient storage needs the BF16 conv maths");
+  AS_CHECK_ARG(!gb || !(use_thin(d, ADAPTSEG_CONV_BWD_DATA) || tapgemm_eligible(d)),
+               "conv bwd_data: the thin / tap-GEMM products take fp32 gradients only");
+  AS_CHECK_ARG(!res_bf16 || aligned16(res_bf16), "conv bwd_data: res_bf16 must be 16-byte aligned");
   AS_CHECK_ARG(dy || copy_only(pl, d, ADAPTSEG_CONV_BWD_DATA),
                "conv bwd_data: this product needs the fp32 dY (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY | ADAPTSEG_EPI_RELU)), "conv bwd_data: LEAKY/RELU not valid");
-  AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res, "conv bwd_data: residual flag without res");
+  AS_CHECK_ARG(!(flags & ADAPTSEG_EPI_RESIDUAL) || res || res_bf16, "conv bwd_data: residual flag without res");
   AS_CHECK_ARG(!(flags & kEpiActGrad) || aux, "conv bwd_data: *_GRAD without aux");
   AS_CHECK_ARG((flags & kEpiActGrad) != kEpiActGrad, "conv bwd_data: LEAKY_GRAD and RELU_GRAD");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv bwd_data: null weight %d", s);
@@ -1111,6 +1070,7 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
   p.out = dx;
   p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(dx_bf16);
   p.res = res;
+  p.resb = reinterpret_cast<const __bf16 *>(res_bf16);
   p.aux = aux;
   p.flags = flags;
   st = attach_wpack(pl, w_pack);

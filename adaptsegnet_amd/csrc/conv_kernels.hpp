@@ -55,6 +55,7 @@ struct ConvParams {
   float *dw[4];                // WGRAD outputs per segment
   const float *bias[4];        // FWD bias per segment (nullable)
   const float *res;            // residual (nullable)
+  const __bf16 *resb;          // ... or the residual stored in bf16 (bf16 gradient storage; then res is NULL)
   const float *aux;            // leaky-grad source (nullable)
   int flags;
   int kw_, kh_;                // kernel width / height (tap -> kh, kw)
@@ -63,12 +64,18 @@ struct ConvParams {
   __bf16 *outb;                // FWD / DGRAD: optional bf16 (RNE) copy of the final output (NULL: none)
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
-  // folded split-K (splits > 1): per-tile arrival counters (zeroed before the launch) and the
-  // final output; the last split of each tile to arrive sums the tile's slabs (igemm_epilogue)
-  unsigned *tile_ctr;
-  float *fold_out;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
+
+// The epilogue's read-modify-write operands under either storage: the accumulate target (the
+// fp32 output, or — bf16 gradient storage, p.out NULL — its bf16 image) and the residual (fp32,
+// or bf16 in p.resb)
+__device__ __forceinline__ float epi_prev(const ConvParams &p, size_t idx) {
+  return p.out ? p.out[idx] : (float)p.outb[idx];
+}
+__device__ __forceinline__ float epi_res(const ConvParams &p, size_t idx) {
+  return p.resb ? (float)p.resb[idx] : p.res[idx];
+}
 
 // ------------------------------------------------------------------------------------
 // Operand gathers.  Each returns 4 consecutive elements along the operand's contiguous
@@ -549,8 +556,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_kernel(const Con
           if (row >= p.M) continue;
           size_t idx = (size_t)row * p.N + col;
           float v = acc[i][j][r] + bsum;
-          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
-          if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
+          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += epi_prev(p, idx);
+          if (flags & ADAPTSEG_EPI_RESIDUAL) v += epi_res(p, idx);
           v = epi_act(v, flags);
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
@@ -652,54 +659,6 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
   dx = kw * dil - pad;
 }
 
-// Folded split-K (weight gradients): the block whose split arrives LAST at its output tile sums
-// the tile's slabs in split order (0, 1, ..., splits-1: deterministic whatever the arrival
-// order) and stores / accumulates the weight-gradient segment, as splitk_reduce4_kernel would.  Hand-off (MI355X_MICROARCH.md, inter-workgroup
-// visibility): every split writes its slab with write-through (sc1) stores, each wave waits for
-// them (vmcnt 0), the block barriers, one lane releases (agent fence) and adds to the tile's
-// counter; the block that sees splits-1 acquires (agent fence, invalidating this CU's L1) before
-// any wave reads a slab.  No block ever waits for another: the last to arrive does the work.
-template <int BN>
-__device__ __forceinline__ void splitk_fold(const ConvParams &p, int tile, int bm, int bn, int BMr, float *lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores are done
-  __syncthreads();
-  int *flag = reinterpret_cast<int *>(lds);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(p.tile_ctr + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = old == (unsigned)(p.splits - 1);
-    if (*flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const uint32_t n4 = (uint32_t)p.N / 4, total4 = (uint32_t)p.M * n4;
-  const float4 *s4 = reinterpret_cast<const float4 *>(p.out);
-  constexpr int Q = BN / 4;   // float4 per tile row
-  for (int r = threadIdx.x; r < BMr * Q; r += blockDim.x) {
-    const int row = bm + r / Q, col = bn + 4 * (r % Q);
-    if (row >= p.M || col >= p.N) continue;
-    const uint32_t i = (uint32_t)row * n4 + (uint32_t)(col >> 2);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-    for (int s = 0; s < p.splits; ++s) {
-      const float4 t = s4[(size_t)s * total4 + i];
-      v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
-    }
-    const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
-    float *dst = seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3];
-    float *o = dst + (size_t)row * p.kseg + (col - seg * p.kseg);
-    if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
-      const float4 a = *reinterpret_cast<const float4 *>(o);
-      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-    }
-    *reinterpret_cast<float4 *>(o) = v;
-  }
-}
-
 // Epilogue shared by the fp32 (igemm_fast_kernel) and bf16 (igemm_bf16_kernel) MFMA paths:
 // both accumulate 32x32 tiles whose C layout is row = (r&3) + 8*(r>>2) + 4*(lane>>5),
 // col = lane&31 (dtype-independent on gfx950).  Split-K slabs, the weight-gradient store
@@ -729,9 +688,6 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
   };
   if (p.splits > 1) {
     float *slab = p.out + (size_t)split * p.M * p.N;
-    // folded sums for the weight gradients only: the forward kernels' SGPR budget (their
-    // epilogue holds the bias / residual / statistics arguments) spills with the fold inlined
-    const bool fold = MODE == MODE_WGRAD && p.tile_ctr != nullptr;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -740,15 +696,9 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = bm + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (full || (row < p.M && col < p.N)) {
-            float *q = slab + (size_t)row * p.N + col;
-            if (fold) __hip_atomic_store(q, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
-            else *q = acc[i][j][r];
-          }
+          if (full || (row < p.M && col < p.N)) slab[(size_t)row * p.N + col] = acc[i][j][r];
         }
       }
-    if constexpr (MODE == MODE_WGRAD)
-      if (fold) splitk_fold<BN>(p, tm * ((p.N + BN - 1) / BN) + tn, bm, bn, BM, lds);
     return;
   }
   if constexpr (MODE == MODE_WGRAD) {
@@ -792,8 +742,8 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
           if (!full && row >= M) continue;
           const size_t idx = out_row(row) * p.N + col;
           float v = acc[i][j][r] + bsum;
-          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += p.out[idx];
-          if (flags & ADAPTSEG_EPI_RESIDUAL) v += p.res[idx];
+          if (flags & ADAPTSEG_EPI_ACCUMULATE) v += epi_prev(p, idx);
+          if (flags & ADAPTSEG_EPI_RESIDUAL) v += epi_res(p, idx);
           v = epi_act(v, flags);
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below

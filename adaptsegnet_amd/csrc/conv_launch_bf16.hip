@@ -193,14 +193,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(
                                              base + al256(g16_act_elems(pl) * sizeof(__bf16)));
-      if (pl.g16_bm == 256 && pl.g16_bn == 256) igemm_bf16g_wgrad_kernel<256, 256><<<grid, block, 0, s>>>(p, act, act2);
-      else if (pl.g16_bm == 256) igemm_bf16g_wgrad_kernel<256><<<grid, block, 0, s>>>(p, act, act2);
+      if (pl.g16_bm == 256) igemm_bf16g_wgrad_kernel<256><<<grid, block, 0, s>>>(p, act, act2);
       else igemm_bf16g_wgrad_kernel<128><<<grid, block, 0, s>>>(p, act, act2);
-      return hipGetLastError();
-    }
-    if (pl.g16_bm == 256 && pl.g16_bn == 256) {   // 256x256x32
-      if (pl.mode == MODE_FWD) igemm_bf16g_kernel<MODE_FWD, 256, 256, 32><<<grid, block, 0, s>>>(p, act, wb);
-      else igemm_bf16g_kernel<MODE_DGRAD, 256, 256, 32><<<grid, block, 0, s>>>(p, act, wb);
       return hipGetLastError();
     }
 #define G16_LAUNCH(MODE_, BK_)                                                                  \

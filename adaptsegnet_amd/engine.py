@@ -21,7 +21,7 @@ Reference semantics followed (file:line in /root/reference):
 from __future__ import annotations
 
 import dataclasses
-
+import os as _os
 
 import torch
 
@@ -97,6 +97,19 @@ def lowp_storage() -> bool:
     residual stream are bf16 tensors; BatchNorm normalises them in fp32 with fp32 statistics
     (from the conv's fp32 accumulators); the gradients stay fp32."""
     return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
+
+
+# (A/B switch) bf16 gradient storage under the BF16 maths
+BF16_GRADS = int(_os.environ.get("ADAPTSEG_BF16_GRADS", "1"))
+
+
+def lowp_grads() -> bool:
+    """bf16 GRADIENT storage (the BF16 maths, config c5, with lowp_storage): a Bottleneck's data
+    gradients (conv dgrad outputs) and its residual gradient are bf16 tensors, as under
+    torch.autocast(bfloat16); BN backward reads them in bf16 and computes in fp32.  Blocks whose
+    input gradient feeds an fp32 consumer (the stem's max-pool backward, layer5's ASPP backward
+    accumulating into layer4.0's input gradient) write that one in fp32."""
+    return lowp_storage() and BF16_GRADS == 1
 
 
 _BF16_SEL: dict = {}
@@ -191,7 +204,6 @@ def x3_forward_terms(g) -> bool:
     return K.get_conv_math() == K.MATH_F32X3 and g.kh * g.kw > 1 and g.cin >= 256 and g.cin % 32 == 0
 
 
-import os as _os
 # (A/B switch, removed after measurement) 0: conv2 backward on fp32 operands; 1: its weight gradient
 # on term images (y1's from the forward, dY's from BN2's backward); 2: its data gradient too
 X3_BWD_TERMS = int(_os.environ.get("ADAPTSEG_X3_BWD_TERMS", "2"))
@@ -308,8 +320,10 @@ def _wgrad_padded(ws, g, dy, x, n, h, w, dw, db=None):
         ws.launch(run, dy, x)
 
 
-def block_backward(blk, rec, gout, need_w, ws=None):
-    """gout: grad of the block output (owned, modified in place).  Returns grad of the input."""
+def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
+    """gout: grad of the block output (owned, modified in place; fp32, or bf16 under bf16
+    gradient storage).  Returns grad of the input — in fp32 when ``dx_fp32``, else (bf16
+    gradient storage) in bf16."""
     n, h, w, oh, ow = rec.n, rec.h, rec.w, rec.oh, rec.ow
     g1, g2, g3 = blk.conv1.geom(), blk.conv2.geom(), blk.conv3.geom()
     # out = relu(bn3(c3) + r): g = gout*[out>0] goes to bn3 and to the residual branch.
@@ -318,9 +332,14 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     f3 = not (sh and bf16_only(g3, n, oh, ow, (1, 2)))
     f2 = not (sh and bf16_only(g2, n, oh, ow, (1, 2)))
     f1 = not (sh and rec.xb is not None and bf16_only(g1, n, h, w, (1, 2)))
+    fd = blk.downsample is None or not (sh and rec.xb is not None and
+                                        bf16_only(blk.downsample[0].geom(), n, h, w, (1, 2)))
+    # bf16 gradient storage: the data gradients are bf16 tensors; a BN backward whose fp32 output
+    # is still wanted (f*: a consumer without a bf16-operand kernel) writes it to its own buffer
+    lg = lowp_grads()
     r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
     dc3, dc3b = r if sh else (r, None)
-    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b)
+    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg)
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
@@ -331,18 +350,21 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     t2 = not sh and rec.y1b is not None
     if t2 and X3_BWD_TERMS >= 2:
         f2 = False
-    r = bn_backward(blk.bn2, dy2, rec.y2b if sh else rec.y2, rec.c2, rec.s2, relu=True, dx=dy2,
+    r = bn_backward(blk.bn2, dy2, rec.y2b if sh else rec.y2, rec.c2, rec.s2, relu=True, dx=None if lg else dy2,
                     mask_from_x=True, bf16=sh or t2, fp32=f2)
-    dy2b = r[1] if (sh or t2) else None
+    # BN2's output: in place over dy2, or (bf16 gradient storage) a new fp32 tensor / None
+    dy2, dy2b = r if (sh or t2) else (r, None)
     if not f2:
         dy2 = None   # not written: its consumers read dy2b
-    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b if (sh or not f2) else None)
+    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b if (sh or not f2) else None,
+                       bf16_only=lg)
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
-    r = bn_backward(blk.bn1, dy1, rec.y1b if (sh or rec.y1 is None) else rec.y1, rec.c1, rec.s1, relu=True, dx=dy1,
+    r = bn_backward(blk.bn1, dy1, rec.y1b if (sh or rec.y1 is None) else rec.y1, rec.c1, rec.s1, relu=True,
+                    dx=None if lg else dy1,
                     mask_from_x=True, bf16=sh, fp32=f1)
-    dy1b = r[1] if sh else None
+    dy1, dy1b = r if sh else (r, None)
     if not f1:
         dy1 = None
     if need_w and blk.conv1.weight.grad is not None:
@@ -350,15 +372,19 @@ def block_backward(blk, rec, gout, need_w, ws=None):
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
-        fd = not (sh and rec.xb is not None and bf16_only(gd, n, h, w, (1, 2)))
-        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=gout, bf16=sh, fp32=fd)
+        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=None if lg else gout, bf16=sh, fp32=fd)
         goutb = r[1] if sh else None
-        gd_in = gout if fd else None   # gout keeps the residual gradient when not rewritten
+        gd_in = (r[0] if sh else r) if fd else None   # (gout keeps the residual gradient when not rewritten)
         if need_w and dconv.weight.grad is not None:
             _wgrad(ws, gd, gd_in, rec.x, n, h, w, [dconv.weight.grad], dyb=goutb, xb=rec.xb)
-        dx = K.conv_dgrad(gd, gd_in, n, h, w, [dconv.weight], dyb=goutb)
+        dx = K.conv_dgrad(gd, gd_in, n, h, w, [dconv.weight], dyb=goutb, bf16_only=lg and not dx_fp32)
         del goutb
         K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, flags=K.EPI_ACCUMULATE, dyb=dy1b)
+    elif lg and dx_fp32 != (gout.dtype == torch.float32):
+        # identity residual, bf16 gradient storage, the input gradient stored unlike gout
+        dx = torch.empty((n, h, w, g1.cin), device=gout.device,
+                         dtype=torch.float32 if dx_fp32 else torch.bfloat16)
+        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, res=gout, dyb=dy1b)
     else:
         # identity residual: dx = dgrad(conv1) + g, written over g in place
         dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout, dyb=dy1b)
@@ -490,7 +516,9 @@ class _DeeplabMultiFn(torch.autograd.Function):
             del gx2
             ctx.q = ctx.qb = None
             for i in reversed(range(n4)):
-                gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w, ws)
+                # layer4.0's input gradient is accumulated into by layer5's backward (fp32)
+                gq = block_backward(model.layer4[i], ctx.recs4[i], gq, need_w, ws,
+                                    dx_fp32=i == 0 and g1_up is not None)
                 done(n4 - i)
                 ctx.recs4[i] = None
             gp3 = gq
@@ -508,7 +536,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
         blocks = [b for layer in (model.layer1, model.layer2, model.layer3) for b in layer]
         g = gp3
         for i in reversed(range(len(blocks))):
-            g = block_backward(blocks[i], ctx.recs[i], g, need_w, ws)
+            g = block_backward(blocks[i], ctx.recs[i], g, need_w, ws, dx_fp32=i == 0)   # (max-pool backward)
             done(n4 + 2 + len(blocks) - 1 - i)
             ctx.recs[i] = None
         c0, y0, s0, am = ctx.stem

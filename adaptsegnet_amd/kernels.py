@@ -260,9 +260,20 @@ def _aligned16(*ts) -> bool:
 
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
-               res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False):
+               res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False, bf16_only: bool = False):
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD).
-    bf16_out: also return a bf16 copy of dx written by the epilogue -> (dx, dxb)."""
+    bf16_out: also return a bf16 copy of dx written by the epilogue -> (dx, dxb).
+    bf16_only (or a bf16 ``out``): dx stored in bf16 only — bf16 gradient storage (BF16 maths);
+    ``res`` may be fp32 or bf16 (adaptseg_conv2d_bwd_data_xg)."""
+    if bf16_only or (out is not None and out.dtype == torch.bfloat16):
+        if out is None:
+            out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.bfloat16)
+        if res is not None:
+            flags |= EPI_RESIDUAL
+        wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
+        _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, aux, None, out, (n, g.cin, h, w), _wshape(g), g.stride,
+                            g.pads, g.dils, flags)
+        return out
     if out is None:
         out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.float32)
     if res is not None:
@@ -353,7 +364,7 @@ def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=
     if not (fp32_out or not bf16_out):
         dx = None
     elif dx is None:
-        dx = torch.empty_like(dy)
+        dx = torch.empty(dy.shape, device=dy.device, dtype=torch.float32)
     dxb = _bf16_like(dy, bf16_out)
     _OP.bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
     return (dx, dxb) if bf16_out else dx

@@ -49,6 +49,35 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _pf(t, n, what):
+    """fp32 operand pointer, checked on the host before any launch: float32 and exactly ``n``
+    elements (a tensor of the wrong dtype or size must raise here, not fault on the GPU)."""
+    if t is None:
+        return None
+    if t.dtype != torch.float32 or t.numel() != n:
+        raise RuntimeError(f"{what}: expected a float32 tensor of {n} elements, got {t.dtype} {tuple(t.shape)}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _pc(t, n, what):
+    """Operand-copy pointer (bf16 image of n elements, or the 3n of F32X3 term images)."""
+    if t is None:
+        return None
+    if t.dtype != torch.bfloat16 or t.numel() not in (n, 3 * n):
+        raise RuntimeError(f"{what}: expected a bf16 copy of {n} (or 3 x {n}) elements, got {t.dtype} "
+                           f"{tuple(t.shape)}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _pfb(t, n, what):
+    """(fp32 pointer, bf16 pointer) of a tensor of n elements stored as either."""
+    if t is None:
+        return None, None
+    if t.dtype == torch.bfloat16:
+        return None, _pc(t, n, what)
+    return _pf(t, n, what), None
+
+
 def _ptrs(ts):
     return _lib.ptr_array([None if t is None else t.data_ptr() for t in ts])
 
@@ -120,6 +149,13 @@ def _wdesc(in_shape, in_stride, w_shape, stride, pad, dil):
     return conv_desc(n, c, h, w, tuple(in_stride), co, kh, kw, stride, tuple(pad), tuple(dil))
 
 
+def _prod(shape):
+    out = 1
+    for v in shape:
+        out *= int(v)
+    return out
+
+
 def _nhwc_strides(n, h, w, c):
     return (h * w * c, 1, w * c, c)
 
@@ -160,11 +196,13 @@ def _conv2d_wpack(weight, pack, in_shape, in_stride, w_shape, stride, pad, dil, 
      "Tensor(a!)? out, Tensor(b!)? outb, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, "
      "int[] dil, int flags) -> ()")
 def _conv2d_fwd(x, xb, weight, wpack, bias, res, out, outb, in_shape, in_stride, w_shape, stride, pad, dil, flags):
-    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_FWD], (out if out is not None else outb).device)
+    nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
     check(_lib.lib().adaptseg_conv2d_fwd_x(
-        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(wpack), _ptrs(bias) if len(bias) else None, _p(res),
-        _p(out), _p(outb), flags, wp, wsz, _stream()), "conv2d_fwd")
+        ctypes.byref(d), _pf(x, nx, "conv2d_fwd x"), _pc(xb, nx, "conv2d_fwd xb"), _ptrs(weight), _p(wpack),
+        _ptrs(bias) if len(bias) else None, _pf(res, ny, "conv2d_fwd res"),
+        _pf(out, ny, "conv2d_fwd out"), _pc(outb, ny, "conv2d_fwd outb"), flags, wp, wsz, _stream()), "conv2d_fwd")
 
 
 @_op("conv2d_fwd_bnstats(Tensor? x, Tensor? xb, Tensor[] weight, Tensor? wpack, Tensor(a!)? out, Tensor(c!)? outb, "
@@ -172,11 +210,13 @@ def _conv2d_fwd(x, xb, weight, wpack, bias, res, out, outb, in_shape, in_stride,
      "int ntiles) -> ()")
 def _conv2d_fwd_bnstats(x, xb, weight, wpack, out, outb, stats, in_shape, in_stride, w_shape, stride, pad, dil,
                         ntiles):
-    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_FWD], stats.device)
     nt = ctypes.c_int(0)
+    nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
     check(_lib.lib().adaptseg_conv2d_fwd_bnstats_x(
-        ctypes.byref(d), _p(x), _p(xb), _ptrs(weight), _p(wpack), _p(out), _p(outb), _p(stats),
+        ctypes.byref(d), _pf(x, nx, "conv2d_fwd_bnstats x"), _pc(xb, nx, "conv2d_fwd_bnstats xb"), _ptrs(weight),
+        _p(wpack), _pf(out, ny, "conv2d_fwd_bnstats out"), _pc(outb, ny, "conv2d_fwd_bnstats outb"), _p(stats),
         ctypes.c_size_t(stats.numel() * 4), ctypes.byref(nt), wp, wsz, _stream()), "conv2d_fwd_bnstats")
     if nt.value != ntiles:
         raise RuntimeError(f"conv2d_fwd_bnstats: planned {ntiles} statistics tiles, the launch produced "
@@ -184,26 +224,32 @@ def _conv2d_fwd_bnstats(x, xb, weight, wpack, out, outb, stats, in_shape, in_str
 
 
 @_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? aux, "
-     "Tensor(a!) dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, "
+     "Tensor(a!)? dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, "
      "int flags) -> ()")
 def _conv2d_bwd_data(dy, dyb, weight, wpack, res, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
+    """res: fp32 or bf16; dx None: the output is stored in bf16 only (dxb) — bf16 gradient storage
+    (adaptseg_conv2d_bwd_data_xg)."""
     n, c, h, w = in_shape
-    d, ws, _, _ = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_BWD_DATA], dx.device)
-    check(_lib.lib().adaptseg_conv2d_bwd_data_x(
-        ctypes.byref(d), _p(dy), _p(dyb), _ptrs(weight), _p(wpack), _p(res), _p(aux), _p(dx), _p(dxb), flags, wp,
-        wsz, _stream()),
+    d, ws, oh, ow = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], (dx if dx is not None else dxb).device)
+    nx, ny = n * h * w * c, n * oh * ow * w_shape[0]
+    check(_lib.lib().adaptseg_conv2d_bwd_data_xg(
+        ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_data dy"), _pc(dyb, ny, "conv2d_bwd_data dyb"), _ptrs(weight),
+        _p(wpack), *_pfb(res, nx, "conv2d_bwd_data res"), _pf(aux, nx, "conv2d_bwd_data aux"),
+        _pf(dx, nx, "conv2d_bwd_data dx"), _pc(dxb, nx, "conv2d_bwd_data dxb"), flags, wp, wsz, _stream()),
         "conv2d_bwd_data")
 
 
 @_op("conv2d_bwd_weight(Tensor? dy, Tensor? dyb, Tensor? x, Tensor? xb, Tensor(a!)[] dw, Tensor(b!)[] db, "
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_bwd_weight(dy, dyb, x, xb, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
-    d, ws, _, _ = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dw[0].device)
+    nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
     check(_lib.lib().adaptseg_conv2d_bwd_weight_x(
-        ctypes.byref(d), _p(dy), _p(dyb), _p(x), _p(xb), _ptrs(dw), _ptrs(db) if len(db) else None, flags, wp,
-        wsz, _stream()), "conv2d_bwd_weight")
+        ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_weight dy"), _pc(dyb, ny, "conv2d_bwd_weight dyb"),
+        _pf(x, nx, "conv2d_bwd_weight x"), _pc(xb, nx, "conv2d_bwd_weight xb"), _ptrs(dw),
+        _ptrs(db) if len(db) else None, flags, wp, wsz, _stream()), "conv2d_bwd_weight")
 
 
 # ---- batch norm (x as [rows, C]: the NHWC buffer) ------------------------------------------
@@ -267,12 +313,15 @@ def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, a
 @_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
      "Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
 def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
-    """y / x (the saved activations): fp32 or bf16; dy, dx, dres fp32."""
+    """y / x (the saved activations): fp32 or bf16; dy and dres fp32, or both bf16 (bf16 gradient
+    storage, adaptseg_bn_bwd_xg); dx fp32."""
     rows, c = _rc(dy)
+    n = rows * c
     wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)
-    check(_lib.lib().adaptseg_bn_bwd_x(
-        rows, c, _p(dy), *_fb(y), *_fb(x), _p(weight), _p(bias), _p(mean), _p(invstd), _p(dx), _p(dxb), _p(dres),
-        int(act), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+    check(_lib.lib().adaptseg_bn_bwd_xg(
+        rows, c, *_pfb(dy, n, "bn_bwd dy"), *_pfb(y, n, "bn_bwd y"), *_pfb(x, n, "bn_bwd x"), _p(weight),
+        _p(bias), _p(mean), _p(invstd), _pf(dx, n, "bn_bwd dx"), _pc(dxb, n, "bn_bwd dxb"),
+        *_pfb(dres, n, "bn_bwd dres"), int(act), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
 
 
 @_op("bn_bwd_affine(Tensor dy, Tensor? y, Tensor x, Tensor? weight, Tensor? bias, Tensor mean, "

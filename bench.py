@@ -173,7 +173,7 @@ def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
     if sel % 100 in (88, 89, 95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
-    if sel % 100 >= 90 or sel % 100 == 82:
+    if sel % 100 >= 90:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
     return FP32_MFMA_PEAK_TFLOPS, "fp32-input MFMA"
 
@@ -189,8 +189,6 @@ def selector_symbol(sel):
     if sel % 100 in (92, 93) and op == 1:   # bf16 LDS-DMA stride-2 data gradient (parity classes)
         bm, bn = (128, 256) if var == 2 else (256, 128)
         return f"igemm_bf16g_kernel<1, {bm}, {bn}, 32, true>"
-    if sel % 100 == 82:   # bf16 LDS-DMA 256x256x32 tile
-        return "igemm_bf16g_wgrad_kernel<256, 256>" if op == 2 else f"igemm_bf16g_kernel<{op}, 256, 256, 32>"
     if sel % 100 in (94, 97, 98, 99):   # the bf16 LDS-DMA kernels (conv_bf16g.hpp)
         if op == 2:
             return f"igemm_bf16g_wgrad_kernel<{256 if var == 8 else 128}>"

@@ -176,6 +176,18 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                const float *const *w, const void *w_pack, const float *res, const float *aux,
                                float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
                                adaptseg_stream_t stream);
+/* adaptseg_conv2d_bwd_data_x with bf16 GRADIENT storage (BF16 conv maths, config c5: under
+   torch.autocast(bfloat16) the data gradients of the convs and the residual gradient of a
+   Bottleneck, model/deeplab_multi.py:83-103, are bf16 tensors).  The residual read by
+   ADAPTSEG_EPI_RESIDUAL is fp32 (res) or bf16 (res_bf16, 16-byte aligned; at most one of them);
+   dx == NULL stores the output in bf16 only (dx_bf16: RNE of the fp32 epilogue value), and then
+   ADAPTSEG_EPI_ACCUMULATE adds to dx_bf16.  The thin (Cout <= 4) and tap-GEMM products keep fp32
+   gradients (ADAPTSEG_ERR_ARG for res_bf16 / dx == NULL there, and under the F32X3 maths).
+   adaptseg_conv2d_bwd_data_x is this with res_bf16 = NULL and dx != NULL. */
+int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
+                                const float *aux, float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
+                                adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
    (Cin and Cout multiples of 8) reads them; other kernels ignore them.  Exception: the
@@ -266,6 +278,16 @@ int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, cons
                       const uint16_t *x_bf16, const float *weight, const float *bias, const float *save_mean,
                       const float *save_invstd, float *dx, uint16_t *dx_bf16, float *dres, int relu, int train,
                       void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+
+/* adaptseg_bn_bwd_x with bf16 GRADIENT storage (BF16 conv maths with bf16 activation storage,
+   config c5): the incoming gradient is dy (fp32) or dy_bf16 (exactly one), and the residual
+   gradient dres is written like it (dres / dres_bf16; it may alias dy of the same storage).  dx
+   is fp32 and / or its bf16 copy, as in adaptseg_bn_bwd_x (for bf16 storage: dx_bf16 only). */
+int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const float *y,
+                       const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
+                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
+                       uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
+                       size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's
    NaiveConvolution norms, model/custom_layers.py:25-33): additionally dbias[c] += sum(g),

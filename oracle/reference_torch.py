@@ -200,43 +200,54 @@ def _bn(x, P, key, train):
 
 
 class _StoreBF16(torch.autograd.Function):
-    """Round to bf16 (RNE) in the forward, identity in the backward: an activation STORED in
-    bf16 whose gradient stays in full precision (the engine's bf16 activation storage)."""
+    """Round to bf16 (RNE) in the forward: an activation STORED in bf16 (the engine's bf16
+    activation storage).  In the backward the gradient w.r.t. it is rounded to bf16 too when
+    ``round_grad`` (bf16 gradient storage, engine.lowp_grads: the data / residual gradients of a
+    Bottleneck are bf16 tensors), else passed through in full precision."""
 
     @staticmethod
-    def forward(ctx, t):
+    def forward(ctx, t, round_grad):
+        ctx.round_grad = round_grad
         return t.to(torch.bfloat16).to(t.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        return g
+        return (g.to(torch.bfloat16).to(g.dtype) if ctx.round_grad else g), None
 
 
-_ACT_BF16 = [False]
+_ACT_BF16 = [False, False]   # activations stored bf16, gradients stored bf16
 
 
 class bf16_activation_storage:
     """Context manager: inside it, every Bottleneck conv output, BN output and block output is
     rounded to bf16 as it is stored (torch.autocast(bfloat16)'s storage; the engine's config c5
-    program, engine.bf16_operands).  The stem, the classifiers and the discriminators are
-    unaffected, as in the engine."""
+    program, engine.bf16_operands), and with ``grads`` (default) so is the gradient w.r.t. each of
+    them (engine.lowp_grads) — except where the engine keeps that gradient in fp32: the output of
+    layer4's last block (it comes from the ASPP head's backward) and, when both heads are trained
+    (multi-level), the output of layer3's last block (layer4.0's input gradient, which layer5's
+    backward accumulates into).  The stem, the classifiers and the discriminators are unaffected,
+    as in the engine."""
+
+    def __init__(self, grads=True):
+        self.grads = grads
 
     def __enter__(self):
-        self._prev = _ACT_BF16[0]
-        _ACT_BF16[0] = True
+        self._prev = list(_ACT_BF16)
+        _ACT_BF16[0], _ACT_BF16[1] = True, self.grads
         return self
 
     def __exit__(self, *exc):
-        _ACT_BF16[0] = self._prev
+        _ACT_BF16[:] = self._prev
 
 
-def _st(t):
-    return _StoreBF16.apply(t) if _ACT_BF16[0] else t
+def _st(t, grad=True):
+    return _StoreBF16.apply(t, grad and _ACT_BF16[1]) if _ACT_BF16[0] else t
 
 
-def _bottleneck(y, P, pre, stride, dil, has_ds, train):
+def _bottleneck(y, P, pre, stride, dil, has_ds, train, out_grad_bf16=True):
     """deeplab_multi.py:83-103 — the stride sits on the first 1x1 conv (:64).  _st: bf16
-    storage of each stored activation (identity unless bf16_activation_storage is on)."""
+    storage of each stored activation (identity unless bf16_activation_storage is on);
+    out_grad_bf16: the gradient w.r.t. the block output is stored in bf16 too."""
     t = _st(F.conv2d(y, P[pre + "conv1.weight"], None, stride))
     t = _st(F.relu(_bn(t, P, pre + "bn1", train)))
     t = _st(F.conv2d(t, P[pre + "conv2.weight"], None, 1, dil, dil))
@@ -247,7 +258,7 @@ def _bottleneck(y, P, pre, stride, dil, has_ds, train):
                      pre + "downsample.1", train))
     else:
         sc = y
-    return _st(F.relu(t + sc))
+    return _st(F.relu(t + sc), out_grad_bf16)
 
 
 def _aspp(y, P, pre, rates=ASPP_RATES):
@@ -260,8 +271,10 @@ def _aspp(y, P, pre, rates=ASPP_RATES):
     return out
 
 
-def g_forward(P, x, input_size, train=True, layout=RESNET101):
-    """ResNetMulti.forward(x, input_size) — deeplab_multi.py:174-194. input_size = (W, H)."""
+def g_forward(P, x, input_size, train=True, layout=RESNET101, grad_heads=2):
+    """ResNetMulti.forward(x, input_size) — deeplab_multi.py:174-194. input_size = (W, H).
+    grad_heads: how many heads the caller's loss reaches (1: single-level, pred1 unused) — only
+    bf16 gradient storage depends on it (see bf16_activation_storage)."""
     y = F.conv2d(x, P["conv1.weight"], None, 2, 3)
     y = F.relu(_bn(y, P, "bn1", train))
     y = F.max_pool2d(y, 3, 2, 1, ceil_mode=False)
@@ -270,7 +283,9 @@ def g_forward(P, x, input_size, train=True, layout=RESNET101):
         if li == 4:
             x1 = _aspp(y, P, "layer5")
         for b in range(nblk):
-            y = _bottleneck(y, P, f"layer{li}.{b}.", stride if b == 0 else 1, dil, b == 0, train)
+            last = b == nblk - 1
+            ogb = not (last and (li == 4 or (li == 3 and grad_heads == 2)))
+            y = _bottleneck(y, P, f"layer{li}.{b}.", stride if b == 0 else 1, dil, b == 0, train, ogb)
     x2 = _aspp(y, P, "layer6")
     size = (int(input_size[1]), int(input_size[0]))
     up = lambda t: F.interpolate(t, size=size, mode="bilinear", align_corners=True)  # noqa: E731
@@ -399,7 +414,8 @@ def oracle_step(G, D1, D2, opts, cfg, i_iter, batches, bn_train=True):
             return None, F.interpolate(vgg_forward(P, x), size=(size[1], size[0]), mode="bilinear",
                                        align_corners=True)
     else:
-        fwd = g_forward
+        def fwd(P, x, size, train):
+            return g_forward(P, x, size, train, grad_heads=1 if c["level"] == "single-level" else 2)
     for images, labels, images_t in batches:
         if c["level"] == "single-level":
             _set_rg(D2, False)

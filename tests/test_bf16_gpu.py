@@ -87,7 +87,7 @@ def test_bf16_conv_products(case, bf16_any):
     # the bf16 kernel must be the one selected (kernel id 100*op + 90 + s2 + 2*(tile width 256))
     for op in (0, 1, 2):
         kid, _ = k.conv_kernel_id(geom, n, h, w, op)
-        assert kid // 10 % 10 == 9 or kid % 100 == 82, (op, kid)   # 82: the 256x256 LDS-DMA tile
+        assert kid // 10 % 10 == 9, (op, kid)
         if k.get_conv_math() == k.MATH_BF16_WIDE and op < 2 and (cout if op == 0 else cin) >= 256:
             assert kid % 10 >= 2, (op, kid)   # the 256-wide tile
 
@@ -194,7 +194,7 @@ def test_bf16_operand_copies_are_bitwise_neutral(bf16_math):
     assert torch.equal(ybi, yi.to(torch.bfloat16))
     wt = [(torch.randn(cout, 3, 3, c, generator=g) * 0.05).to(DEV)]
     kid, sp = k.conv_kernel_id(geom, n, h, w, 0)
-    assert kid % 100 in (82, 94, 97, 98, 99), kid   # the LDS-DMA kernel
+    assert kid % 100 in (94, 97, 98, 99), kid   # the LDS-DMA kernel
     assert torch.equal(k.conv_fwd(geom, y, n, h, w, wt, xb=yb), k.conv_fwd(geom, y, n, h, w, wt))
     gy = torch.randn(n, h, w, cout, generator=g).to(DEV)
     dx, dxb = k.bn_bwd(gy, None, x if cout == c else torch.randn(n, h, w, cout, generator=g).to(DEV),
@@ -203,7 +203,7 @@ def test_bf16_operand_copies_are_bitwise_neutral(bf16_math):
     assert torch.equal(dxb, dx.to(torch.bfloat16))
     assert torch.equal(k.conv_dgrad(geom, dx, n, h, w, wt, dyb=dxb), k.conv_dgrad(geom, dx, n, h, w, wt))
     # weight gradient on bf16 copies of both operands: bitwise the plain call's result
-    assert k.conv_kernel_id(geom, n, h, w, 2)[0] % 100 in (82, 98)   # the LDS-DMA weight-gradient kernel, BM 256
+    assert k.conv_kernel_id(geom, n, h, w, 2)[0] % 100 == 98   # the LDS-DMA weight-gradient kernel, BM 256
     dw0 = [torch.zeros_like(wt[0])]
     dw1 = [torch.zeros_like(wt[0])]
     k.conv_wgrad(geom, gy, y, n, h, w, dw0, accumulate=False)
@@ -316,7 +316,7 @@ def test_aspp_tap_gemm_reads_the_bf16_copy_bitwise(bf16_math):
     xb = x.to(torch.bfloat16)
     wt = [(torch.randn(cout, 3, 3, c, generator=g) * 0.02).to(DEV) for _ in range(4)]
     bs = [torch.randn(cout, generator=g).to(DEV) for _ in range(4)]
-    assert k.conv_kernel_id(geom, n, h, w, 0)[0] % 100 in (82, 94, 97, 98, 99)   # inner GEMM on the LDS-DMA kernel
+    assert k.conv_kernel_id(geom, n, h, w, 0)[0] % 100 in (94, 97, 98, 99)   # inner GEMM on the LDS-DMA kernel
     assert torch.equal(k.conv_fwd(geom, x, n, h, w, wt, bs, xb=xb), k.conv_fwd(geom, x, n, h, w, wt, bs))
     gy = torch.randn(n, h, w, cout, generator=g).to(DEV)
     dw0 = [torch.zeros_like(t) for t in wt]
@@ -325,50 +325,3 @@ def test_aspp_tap_gemm_reads_the_bf16_copy_bitwise(bf16_math):
     k.conv_wgrad(geom, gy, x, n, h, w, dw1, accumulate=False, xb=xb)
     for a, b in zip(dw0, dw1):
         assert torch.equal(a, b)
-
-
-# (n, cin, h, w, cout, ks, dil, ops on the 256x256 tile): products whose M x N gives >= 256 tiles
-WIDE_CASES = [
-    (1, 512, 128, 128, 1024, 1, 1, (0, 2)),   # 1x1 expansion (layer4 conv3 class), forward, weight gradient
-    (1, 1024, 128, 128, 512, 1, 1, (1, 2)),   # its data gradient class (N = Cin = 1024)
-    (2, 256, 128, 128, 512, 3, 2, (0, 2)),    # dilated 3x3, forward (N = 512)
-    (2, 512, 128, 128, 256, 3, 2, (1, 2)),    # dilated 3x3, data gradient (N = Cin = 512)
-    (1, 64, 90, 100, 256, 3, 1, (2,)),        # Cin 64: a 256-column tile spans four taps
-]
-
-
-@pytest.mark.parametrize("case", WIDE_CASES, ids=[f"w{i}" for i in range(len(WIDE_CASES))])
-def test_bf16_wide_tile_products(case, bf16_math):
-    """The 256x256x32 LDS-DMA tiles (selector 100*op + 82, conv_bf16g.hpp; the weight gradient's
-    igemm_bf16g_wgrad_kernel<256, 256>): bf16 operands, fp32
-    accumulation.  Reference: torch's fp32 conv of the same bf16-rounded operands on the GPU
-    (the bf16 products are exact in fp32, so only the accumulation order differs; these shapes
-    are too large for a CPU fp64 conv inside the test budget): max|err| <= 2e-5 * max|ref|."""
-    k = bf16_math
-    n, cin, h, w, cout, ks, dil, ops = case
-    pad = (ks // 2) * dil
-    geom = k.ConvGeom(cin, cout, ks, ks, 1, (pad,), (dil,))
-    sel = [k.conv_kernel_id(geom, n, h, w, op)[0] for op in ops]
-    if all(s % 100 != 82 for s in sel):
-        pytest.skip("library built without the 256x256 tiles (ADAPTSEG_G16_WIDE_*; off by default, DESIGN §3.8)")
-    assert sel == [100 * op + 82 for op in ops], sel
-    g = torch.Generator(device=DEV).manual_seed(hash(case) % 1000)
-    x = torch.randn(n, cin, h, w, generator=g, device=DEV)
-    wt = torch.randn(cout, cin, ks, ks, generator=g, device=DEV) / (cin * ks * ks) ** 0.5
-    gy = torch.randn(n, cout, h, w, generator=g, device=DEV)
-    xb, wb, gb = (t.to(torch.bfloat16).float() for t in (x, wt, gy))
-    wd = [wt.permute(0, 2, 3, 1).contiguous()]
-    if 0 in ops:
-        ref = F.conv2d(xb, wb, None, 1, pad, dil)
-        y = k.conv_fwd(geom, x.permute(0, 2, 3, 1).contiguous(), n, h, w, wd)
-        assert rel(y.permute(0, 3, 1, 2), ref) < 2e-5
-    if 1 in ops:
-        ref = torch.nn.grad.conv2d_input(x.shape, wb, gb, 1, pad, dil)
-        dx = k.conv_dgrad(geom, gy.permute(0, 2, 3, 1).contiguous(), n, h, w, wd)
-        assert rel(dx.permute(0, 3, 1, 2), ref) < 2e-5
-    if 2 in ops:   # weight gradient: k = output pixel, both operands bf16 copies
-        ref = torch.nn.grad.conv2d_weight(xb, wt.shape, gb, 1, pad, dil)
-        dw = torch.zeros_like(wd[0])
-        k.conv_wgrad(geom, gy.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous(), n, h, w, [dw],
-                     accumulate=False)
-        assert rel(dw.permute(0, 3, 1, 2), ref) < 2e-5

@@ -106,3 +106,80 @@ def test_bn_backward_on_bf16_storage(K, rows, c, mask_from_y):
         scale = float(dref.abs().max())
         assert float((dxb.double() - dref).abs().max()) < 2 ** -8 * scale + 1e-6, (rows, c)
     assert float((outs[0][0].double() - outs[1][0].double()).abs().max()) <= 2 ** -7 * float(dref.abs().max())
+
+
+@pytest.mark.parametrize("rows,c,mask_from_y,train", [(4 * 37 * 53, 256, True, True), (3 * 41 * 29 + 7, 64, False, True),
+                                                      (2 * 33 * 17, 1024, True, True), (1999, 12, False, True),
+                                                      (2 * 33 * 17, 1024, True, False)])
+def test_bn_backward_on_bf16_gradient_storage(K, rows, c, mask_from_y, train):
+    """bf16 GRADIENT storage (engine.lowp_grads, adaptseg_bn_bwd_xg): dy is a bf16 tensor, the
+    residual gradient dres is written over it in bf16 (in place, as block_backward does with the
+    residual stream), dx as its bf16 copy only.  Against the fp64 restatement on the same bf16
+    values: dres exactly dy*mask (masking is exact in bf16), dx within one bf16 ulp of the scale;
+    both thread layouts (the 16-B one and, misaligned, one quad a thread); eval mode too."""
+    g = torch.Generator().manual_seed(11 * rows + c)
+    x = (torch.randn(rows, c, generator=g) * 2 + 0.5).to(DEV).to(torch.bfloat16)
+    res = torch.randn(rows, c, generator=g).to(DEV).to(torch.bfloat16) if mask_from_y else None
+    w, b = torch.rand(c, generator=g).to(DEV) + 0.5, torch.randn(c, generator=g).to(DEV) * 0.1
+    rm, rv = torch.randn(c, generator=g).to(DEV) * 0.1, torch.rand(c, generator=g).to(DEV) + 0.5
+    _, mean, invstd, yb = K.bn_fwd_train(x, w, b, None, None, 0.1, 1e-5, res=res, relu=True, bf16_out=True,
+                                         fp32_out=False)
+    if not train:
+        mean, invstd = rm, torch.rsqrt(rv + 1e-5)
+    dy = torch.randn(rows, c, generator=g).to(DEV).to(torch.bfloat16)
+    xd, md, idd = x.double(), mean.double(), invstd.double()
+    xhat = (xd - md) * idd
+    o = yb.double() if mask_from_y else xhat * w.double() + b.double()
+    gg = dy.double() * (o > 0)
+    if train:
+        dref = w.double() * idd * (gg - gg.mean(0) - xhat * (gg * xhat).mean(0))
+    else:
+        dref = gg * w.double() * idd
+    scale = float(dref.abs().max())
+    for aligned in (True, False):
+        dd = dy.clone() if aligned else misaligned(dy)
+        yy, xx = (yb, x) if aligned else (misaligned(yb), misaligned(x))
+        _, dxb = K.bn_bwd(dd, yy if (mask_from_y or not train) else None, xx, w, mean, invstd, relu=True,
+                          dres=dd if mask_from_y else None, bias=b, bf16_out=True, fp32_out=False, train=train)
+        assert dxb.dtype == torch.bfloat16
+        if mask_from_y:
+            assert dd.dtype == torch.bfloat16 and torch.equal(dd.double(), dy.double() * (o > 0))
+        assert float((dxb.double() - dref).abs().max()) < 2 ** -8 * scale + 1e-6, (rows, c, aligned)
+
+
+def test_conv_dgrad_bf16_gradient_storage(K):
+    """bf16 gradient storage in the conv data gradient (adaptseg_conv2d_bwd_data_xg): the identity
+    residual read in bf16 and the output stored bf16-only (block_backward's dx = dgrad(conv1) + g),
+    fp32 residual into a bf16 output and bf16 residual into an fp32 output (the blocks whose input
+    gradient changes storage), and EPI_ACCUMULATE into a bf16 output (the downsample block).
+    Against fp64 on the same bf16 operands, the result rounded to bf16: within one bf16 ulp (RNE
+    of an fp32 value that is itself within 1e-5 of the exact sum).  Shapes with and without split-K."""
+    for n, cin, h, w, cout in ((2, 1024, 16, 24, 256), (2, 512, 64, 96, 128)):
+        geom = K.ConvGeom(cin, cout, 1, 1, 1, (0,), (1,))
+        g = torch.Generator().manual_seed(cin + h)
+        wt = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+        dy = torch.randn(n, h, w, cout, generator=g)
+        res = torch.randn(n, h, w, cin, generator=g)
+        wb, dyb, resb = (t.to(torch.bfloat16).double() for t in (wt, dy, res))
+        ref = torch.einsum("nhwo,oi->nhwi", dyb, wb[:, :, 0, 0])
+        wd = [wt.permute(0, 2, 3, 1).contiguous().to(DEV)]
+        dyd = dy.to(DEV).to(torch.bfloat16)
+        tol = lambda r: 2.0 ** -8 * r.abs() + 1e-5 * float(r.abs().max())   # noqa: E731
+
+        def ok(got, r):
+            return bool(((got.double().cpu() - r).abs() <= tol(r)).all())
+
+        # bf16 residual, bf16-only output, in place (the identity block)
+        gb = res.to(DEV).to(torch.bfloat16)
+        out = K.conv_dgrad(geom, None, n, h, w, wd, out=gb, res=gb, dyb=dyd)
+        assert out is gb and out.dtype == torch.bfloat16 and ok(out, ref + resb)
+        # fp32 residual -> bf16 output; bf16 residual -> fp32 output
+        ob = K.conv_dgrad(geom, None, n, h, w, wd, res=res.to(DEV), dyb=dyd, bf16_only=True)
+        assert ob.dtype == torch.bfloat16 and ok(ob, ref + res.double())
+        of = torch.empty(n, h, w, cin, device=DEV)
+        K.conv_dgrad(geom, None, n, h, w, wd, out=of, res=res.to(DEV).to(torch.bfloat16), dyb=dyd)
+        assert float((of.double().cpu() - (ref + resb)).abs().max()) < 1e-5 * float((ref + resb).abs().max())
+        # accumulate into a bf16 output
+        acc = res.to(DEV).to(torch.bfloat16)
+        K.conv_dgrad(geom, None, n, h, w, wd, out=acc, flags=K.EPI_ACCUMULATE, dyb=dyd)
+        assert ok(acc, ref + resb)

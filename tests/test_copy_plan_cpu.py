@@ -74,7 +74,7 @@ def test_skip_decisions_match_across_geometries_but_the_kernel_variants_do_not()
 
 def test_copy_operand_only_matches_the_lds_dma_selectors():
     """adaptseg_conv2d_copy_operand_only (what engine.bf16_only asks) is exactly the set of
-    products the planner puts on the LDS-DMA kernels (selectors 100*op + 82 / 94 / 97-99, 192 / 193)
+    products the planner puts on the LDS-DMA kernels (selectors 100*op + 94 / 97-99, 192 / 193)
     or the register-staged bf16 forward (90-93), for every conv geometry of the c5 step; under
     F32X3 it is exactly the set the term-image kernel takes when the copies are passed
     (selectors 100*op + 88 / 89, conv_x3r.hpp); under the fp32-input MFMA math never."""
@@ -101,7 +101,7 @@ def test_copy_operand_only_matches_the_lds_dma_selectors():
         seen = set()
         for g, n, h, w, op, st in geoms:
             kid, _ = K.conv_kernel_id(g, n, h, w, op, st)
-            lds_dma = kid % 100 in (82, 94, 97, 98, 99) or (op == 1 and kid % 100 in (92, 93))
+            lds_dma = kid % 100 in (94, 97, 98, 99) or (op == 1 and kid % 100 in (92, 93))
             # the register-staged bf16 forward (90-93) reads the contiguous bf16 copy too
             lds_dma = lds_dma or (op == 0 and kid % 100 in (90, 91, 92, 93))
             if g.cout <= 32:   # tap-GEMM (ASPP heads): the selector is the inner GEMM's, whose

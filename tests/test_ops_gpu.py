@@ -607,8 +607,7 @@ def test_f32x3_accuracy_matches_fp32_mfma(op):
     1024) its max error vs fp64 stays within 1.5x that of the exact fp32-MFMA kernel (the dropped
     split terms are below one fp32 rounding per product), for both F32X3 kernels (the
     register-staged one, selector 100*op + 95, and the pre-split LDS-DMA 256x128x32 one under
-    F32X3_PRESPLIT, + 88; a -DADAPTSEG_X3R_FWD_PERCALL=1 build takes the latter for the wide 3x3
-    forward under the default maths too, images made per call)."""
+    F32X3_PRESPLIT, + 88)."""
     k = K()
     g = torch.Generator().manual_seed(77)
     errs = {}
@@ -627,7 +626,7 @@ def test_f32x3_accuracy_matches_fp32_mfma(op):
             k.set_conv_math({"f32": k.MATH_F32, "f32x3": k.MATH_F32X3, "f32x3_presplit": k.MATH_F32X3_PRESPLIT}[math])
             try:
                 sel, _ = k.conv_kernel_id(geom, n, h, w, op)
-                assert sel % 100 == {"f32": -1 if sel % 100 in (86, 87, 88, 89) or sel % 100 >= 90 else sel % 100, "f32x3": sel % 100 if op == 0 and ks > 1 and sel % 100 == 88 else 95,
+                assert sel % 100 == {"f32": -1 if sel % 100 in (86, 87, 88, 89) or sel % 100 >= 90 else sel % 100, "f32x3": 95,
                                       "f32x3_presplit": 88}[math], (math, sel)
                 if op == 0:
                     out = nchw(k.conv_fwd(geom, nhwc(x), n, h, w, [w_cl(wt)]))

@@ -155,10 +155,11 @@ def test_reference_trajectory_fixture_and_oracle_iteration0():
         assert abs(got[k] - tr[0, j]) <= 1e-5 * abs(tr[0, j]), (k, got[k], tr[0, j])
 
 
-def test_bf16_activation_storage_rounds_block_outputs_and_passes_gradients_straight():
-    """R.bf16_activation_storage (the oracle side of config c5's bf16 activation storage): inside
-    it every Bottleneck output is exactly bf16-representable, the rounding is a straight-through
-    identity in the backward, and outside it the oracle is unchanged."""
+def test_bf16_activation_storage_rounds_block_outputs_and_their_gradients():
+    """R.bf16_activation_storage (the oracle side of config c5's bf16 activation and gradient
+    storage): inside it every Bottleneck output is exactly bf16-representable, the gradient
+    w.r.t. a stored tensor is rounded to bf16 (RNE) in the backward — or passed straight through
+    with grads=False / where the engine keeps it fp32 — and outside it the oracle is unchanged."""
     P = R.to_torch(R.det_state(R.g_specs(), 7), dtype=torch.float64)
     y = torch.randn(1, 256, 9, 11, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
     y = y.to(torch.bfloat16).double().requires_grad_()   # block inputs are stored bf16 as well
@@ -172,5 +173,15 @@ def test_bf16_activation_storage_rounds_block_outputs_and_passes_gradients_strai
     rel = float((out - plain).abs().max() / plain.abs().max())
     assert 0 < rel < 2e-2, rel
     g = torch.randn_like(out)
-    (gi,) = torch.autograd.grad(R._StoreBF16.apply(out), out, g)
+    (gi,) = torch.autograd.grad(R._StoreBF16.apply(out, False), out, g)
     assert torch.equal(gi, g)
+    (gi,) = torch.autograd.grad(R._StoreBF16.apply(out, True), out, g)
+    assert torch.equal(gi, g.to(torch.bfloat16).double()) and not torch.equal(gi, g)
+    with R.bf16_activation_storage(grads=False):
+        (gi,) = torch.autograd.grad(R._st(out), out, g)
+    assert torch.equal(gi, g)
+    with R.bf16_activation_storage():
+        (gi,) = torch.autograd.grad(R._st(out, grad=False), out, g)
+        assert torch.equal(gi, g)
+        (gi,) = torch.autograd.grad(R._st(out), out, g)
+        assert torch.equal(gi, g.to(torch.bfloat16).double())

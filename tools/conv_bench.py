@@ -117,7 +117,7 @@ def main():
         xn = x.permute(0, 3, 1, 2) if x.dim() == 4 and x.shape[-1] == g.cin else x
         # the products the engine runs on term images under F32X3 (engine.x3_forward_terms /
         # X3_BWD_TERMS: the layer 3-4 conv2 forward, data and weight gradients), timed so
-        tf = st is None and engine.x3_forward_terms(g)
+        tf = st is None and name.endswith("conv2") and engine.x3_forward_terms(g)
         tb = tf and engine.X3_BWD_TERMS >= 2
         tw = tf and engine.X3_BWD_TERMS >= 1
         xt = _terms(x) if tf or tw else None
