@@ -68,14 +68,19 @@ _SIGS = {
     "adaptseg_conv2d_fwd_bnstats_x": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _SZ, ctypes.POINTER(ctypes.c_int), _P,
                                       _SZ, _P],
     "adaptseg_conv2d_bwd_data_x": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
-    "adaptseg_conv2d_bwd_data_xg": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
+    "adaptseg_conv2d_bwd_data_xg": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight_x": [_DESC, _P, _P, _P, _P, _PP, _PP, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_train_x": [_L, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_train_tiles_x": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I,
                                       _P],
     "adaptseg_bn_fwd_infer_x": [_L, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I, _P],
+    "adaptseg_bn_fwd_train_xm": [_L, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P, _SZ,
+                                 _P],
+    "adaptseg_bn_fwd_train_tiles_xm": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P,
+                                       _I, _P],
+    "adaptseg_bn_fwd_infer_xm": [_L, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _P],
     "adaptseg_bn_bwd_x": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
-    "adaptseg_bn_bwd_xg": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
+    "adaptseg_bn_bwd_xg": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
     "adaptseg_bn_workspace_size": [_L, _I, ctypes.POINTER(_SZ)],
     "adaptseg_bn_fwd_train": [_L, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_upsample_argmax": [_I, _I, _I, _I, _I, _I, _P, _P, _P],
@@ -116,6 +121,7 @@ _SIGS = {
     "adaptseg_grid_warp_bwd_workspace_size": [_I, _I, _I, _I, ctypes.POINTER(_SZ)],
     "adaptseg_grid_warp_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
+    "adaptseg_set_wgrad_reduce_priority": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_enable_mem": [_I],

@@ -165,6 +165,37 @@ __device__ __forceinline__ float fwd_act(float v, int act) {
   return v;
 }
 
+// ReLU mask bitmaps [rows][C / 32] (C % 32 == 0): bit c % 32 of word (row, c / 32) is set when a
+// BN+ReLU output is > 0.  The forward apply writes it beside y, and the backward reads 1 bit per
+// element for the mask instead of the stored y (4 B fp32 / 2 B bf16): the Bottleneck's BN3,
+// whose mask gates the residual gradient as well (model/deeplab_multi.py:96-103).  The lanes of an
+// aligned 32-channel group — 8 lanes of one quad (QN 1) or 4 lanes of two quads (QN 2), always
+// consecutive lanes of one row in these kernels — merge their bits with xor-shuffles, and the
+// group's first lane stores the word.
+template <int QN>
+__device__ __forceinline__ void store_mask_bits(uint32_t *bits, int64_t row, int c, int C, const float4 (&o)[QN]) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int h = 0; h < QN; ++h)
+    v |= ((o[h].x > 0.f ? 1u : 0u) | (o[h].y > 0.f ? 2u : 0u) | (o[h].z > 0.f ? 4u : 0u) | (o[h].w > 0.f ? 8u : 0u))
+         << (4 * h);
+  v <<= (c & 31);
+#pragma unroll
+  for (int m = 1; m < 8 / QN; m <<= 1) v |= __shfl_xor(v, m);
+  if ((c & 31) == 0) bits[row * (C >> 5) + (c >> 5)] = v;
+}
+// this thread's 4*QN mask bits of (row, c..): the word shifted so bit 0 is channel c
+__device__ __forceinline__ uint32_t load_mask_bits(const uint32_t *bits, int64_t row, int c, int C) {
+  return bits[row * (C >> 5) + (c >> 5)] >> (c & 31);
+}
+__device__ __forceinline__ float4 mask_quad(float4 g, uint32_t w) {
+  g.x = (w & 1u) ? g.x : 0.f;
+  g.y = (w & 2u) ? g.y : 0.f;
+  g.z = (w & 4u) ? g.z : 0.f;
+  g.w = (w & 8u) ? g.w : 0.f;
+  return g;
+}
+
 // Block = 256 threads laid out as TC channel groups (QN quads each) x TR row lanes (TC*TR =
 // 256).  Grid = (ceil(C / (4*QN*TC)), splits).  Partial sums land in ws[2][C][splits] (float).
 // TD: storage of the incoming gradient dy (fp32, or bf16 under bf16 gradient storage)
@@ -173,7 +204,7 @@ __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const TD *__restrict__ dy,
                  typename Act<TY>::ptr __restrict__ y, const float *__restrict__ mean, const float *__restrict__ invstd,
                  const float *__restrict__ w, const float *__restrict__ b, int relu,
-                 int64_t rows_per_split, float *__restrict__ partial) {
+                 int64_t rows_per_split, float *__restrict__ partial, const uint32_t *__restrict__ dbits = nullptr) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc;   // channel group within block
   const int rl = threadIdx.x / tc;   // row lane
@@ -201,6 +232,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const TD
     constexpr int U = QN == 2 ? kBf16Rows : kReduceUnroll;
     for (int64_t r = r0 + rl; r < r1; r += U * tr) {
       float4 v[U][QN], g[U][QN], o[U][QN];
+      uint32_t mb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t ru = r + (int64_t)u * tr;
@@ -209,6 +241,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const TD
         if (MODE == 1) {
           ldq<QN>(dy + e, g[u]);
           if (relu == 1 || relu == 3) ldmq<TY, QN>(y, row, c0, C, o[u]);
+          mb[u] = dbits ? load_mask_bits(dbits, row, c0, C) : ~0u;
         }
       }
 #pragma unroll
@@ -224,6 +257,7 @@ bn_reduce_kernel(int64_t rows, int C, int tc, const TX *__restrict__ x, const TD
             a2.x += d.x * d.x; a2.y += d.y * d.y; a2.z += d.z * d.z; a2.w += d.w * d.w;
           } else {
             float4 gg = g[u][h];
+            if (dbits) gg = mask_quad(gg, mb[u] >> (4 * h));
             if (relu == 2) gg = relu_mask_from_x(gg, vv, pv, is[h], ww[h], bb[h]);
             else if (relu) gg = act_mask_o(gg, relu, o[u][h], vv, pv, is[h], ww[h], bb[h]);
             a1.x += gg.x; a1.y += gg.y; a1.z += gg.z; a1.w += gg.w;
@@ -395,7 +429,7 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
                                       const float *__restrict__ rm, const float *__restrict__ rv, float eps,
                                       const float *__restrict__ w, const float *__restrict__ b,
                                       typename Act<TR>::ptr __restrict__ res, float *__restrict__ y, uint2 *yb, int relu,
-                                      bool terms = false) {
+                                      bool terms = false, uint32_t *mbits = nullptr) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = (int)((i * 4) % C);
@@ -415,6 +449,10 @@ __global__ void bn_infer_apply_kernel(int64_t total4, int C, const TX *__restric
     }
     if (y) reinterpret_cast<float4 *>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
     if (yb) store_copy(yb, row, c, C, make_float4(o[0], o[1], o[2], o[3]), terms);
+    if (mbits) {   // (C % 32 == 0: the 8 quads of a word are 8 consecutive lanes of this loop)
+      const float4 oq[1] = {make_float4(o[0], o[1], o[2], o[3])};
+      store_mask_bits<1>(mbits, row, c, C, oq);
+    }
   }
 }
 
@@ -455,7 +493,8 @@ template <typename TX, typename TR = TX, int QN = 1>
 __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const float *__restrict__ mean,
                   const float *__restrict__ invstd, const float *__restrict__ w, const float *__restrict__ b,
-                  typename Act<TR>::ptr res, float *y, uint2 *yb, int act, bool terms = false) {
+                  typename Act<TR>::ptr res, float *y, uint2 *yb, int act, bool terms = false,
+                  uint32_t *mbits = nullptr) {
   const int tr = 256 / tc;
   const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
   const int c0 = (blockIdx.x * tc + cq) * 4 * QN;
@@ -492,6 +531,7 @@ bn_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TX *x, const f
       }
       if (y) stq<QN>(y + ru * C + c0, o);
       if (yb) store_copyq<QN>(yb, ru, c0, C, o, terms);
+      if (mbits) store_mask_bits<QN>(mbits, ru, c0, C, o);
     }
   }
 }
@@ -501,7 +541,8 @@ __global__ void __launch_bounds__(256, kBnMinBlocks)
 bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TD *dy, typename Act<TY>::ptr y,
                       const TX *x, const float *__restrict__ w, const float *__restrict__ b,
                       const float *__restrict__ mean, const float *__restrict__ invstd, const float *__restrict__ coef,
-                      float *dx, uint2 *dxb, TD *dres, int rmode, int train, bool terms = false) {
+                      float *dx, uint2 *dxb, TD *dres, int rmode, int train, bool terms = false,
+                      const uint32_t *__restrict__ dbits = nullptr) {
   if constexpr (QN == 1) {   // (the grouped body below takes 130 VGPRs here: 3 waves per SIMD)
     const int tr = 256 / tc;
     const int cq = threadIdx.x % tc, rl = threadIdx.x / tc;
@@ -525,6 +566,7 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TD *dy, ty
         g[u] = lda4(dy + e);
         v[u] = train ? lda4(x + e) : z4;
         o4[u] = need_y ? ldm4<TY>(y, row, c0, C) : z4;
+        if (dbits) g[u] = mask_quad(g[u], load_mask_bits(dbits, row, c0, C));
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -584,6 +626,11 @@ bn_bwd_apply2d_kernel(int64_t rows, int C, int tc, int64_t per, const TD *dy, ty
         const int64_t ru = r + (int64_t)u * tr;
         const int64_t row = ru < r1 ? ru : r, e = row * C + c0;
         ldq<QN>(dy + e, g[u]);
+        if (dbits) {
+          const uint32_t mw = load_mask_bits(dbits, row, c0, C);
+#pragma unroll
+          for (int h = 0; h < QN; ++h) g[u][h] = mask_quad(g[u][h], mw >> (4 * h));
+        }
         if (train) ldq<QN>(x + e, v[u]);
         else zq<QN>(v[u]);
         if (need_y) ldmq<TY, QN>(y, row, c0, C, o4[u]);
@@ -710,7 +757,7 @@ static void bn_bwd_kernels(int64_t rows, int c, const TD *dy, typename Act<TY>::
                            const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
                            float *dx, uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight,
                            float *dbias, float *partial, float *coef, double reduce_bytes, double apply_bytes,
-                           bool dterms, hipStream_t s) {
+                           bool dterms, const uint32_t *dbits, hipStream_t s) {
   int slot;
   if (train) {
     const int rqn = reduce_qn(QN, c);
@@ -718,10 +765,10 @@ static void bn_bwd_kernels(int64_t rows, int c, const TD *dy, typename Act<TY>::
     timing_begin(kTBnReduceBwd, s, reduce_bytes, &slot);
     if (rqn == 2)
       bn_reduce_kernel<1, TX, TY, QN, TD><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
-          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
+          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial, dbits);
     else
       bn_reduce_kernel<1, TX, TY, 1, TD><<<dim3(r.cblocks, r.splits), 256, 0, s>>>(
-          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial);
+          rows, c, r.tc, x, dy, y, save_mean, save_invstd, weight, bias, rmode, r.per, partial, dbits);
     timing_end(slot, s);
     bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, r.splits, partial, save_invstd, coef,
                                                                    dweight, dbias);
@@ -730,7 +777,7 @@ static void bn_bwd_kernels(int64_t rows, int c, const TD *dy, typename Act<TY>::
   const ApplyPlan ap = apply_plan(rows, c, QN);
   bn_bwd_apply2d_kernel<TX, TY, QN, TD><<<dim3(ap.cblocks, ap.rsplits), 256, 0, s>>>(
       rows, c, ap.tc, ap.per, dy, y, x, weight, bias, save_mean, save_invstd, coef, dx,
-      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms);
+      reinterpret_cast<uint2 *>(dx_bf16), dres, rmode, train, dterms, dbits);
   timing_end(slot, s);
 }
 
@@ -738,7 +785,7 @@ template <typename TX, typename TY = TX, typename TD = float>
 int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
                          const float *bias, const float *save_mean, const float *save_invstd, float *dx,
                          uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
-                         size_t ws_bytes, hipStream_t s) {
+                         size_t ws_bytes, hipStream_t s, const uint32_t *dbits = nullptr) {
   float *partial = reinterpret_cast<float *>(ws), *coef = nullptr;
   const double eb = sizeof(TX);   // bytes per activation element (x)
   const bool terms = std::is_same<TY, X3>::value;   // y stored as F32X3 term images
@@ -756,20 +803,22 @@ int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, co
   // reduce: dy, x (+ y for the mask from y) in; apply: dy, x (train), y (mask from y) in; dx,
   // dres out
   const double db = sizeof(TD);    // bytes per gradient element (dy, dres)
-  const double reduce_bytes = (db + eb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
-  const double apply_bytes = (db * (1 + (dres ? 1 : 0)) + 4.0 * (dx ? 1 : 0) + eb * (train ? 1 : 0) +
+  const double mb = dbits ? 0.125 : 0.0;   // bytes per element of a mask bitmap
+  const double reduce_bytes = (db + eb + mb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
+  const double apply_bytes = (db * (1 + (dres ? 1 : 0)) + 4.0 * (dx ? 1 : 0) + eb * (train ? 1 : 0) + mb +
                               ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
                              (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0);
   if constexpr (sizeof(TX) == 2 && !std::is_same<TY, X3>::value) {
     if (qn == 2) {
       bn_bwd_kernels<TX, TY, 2, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                    train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+                                    train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, dbits,
+                                    s);
       AS_CHECK_LAUNCH("bn_bwd");
       return ADAPTSEG_OK;
     }
   }
   bn_bwd_kernels<TX, TY, 1, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, s);
+                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, dbits, s);
   AS_CHECK_LAUNCH("bn_bwd");
   return ADAPTSEG_OK;
 }
@@ -812,7 +861,8 @@ static double fwd_apply_bytes(int64_t rows, int c, const float *x, const float *
 
 static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *mean,
                          const float *invstd, const float *weight, const float *bias, const float *res,
-                         const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu, hipStream_t s) {
+                         const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu, hipStream_t s,
+                         uint32_t *mbits = nullptr) {
   const bool terms = copies_are_terms() && y_bf16;
   uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
@@ -821,27 +871,28 @@ static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_
   const dim3 g(ap.cblocks, ap.rsplits);
   if (x && rb)
     bn_apply2d_kernel<float, X3><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, rb, y, yb,
-                                                   relu, terms);
+                                                   relu, terms, mbits);
   else if (x)
     bn_apply2d_kernel<float, float><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, res, y,
-                                                      yb, relu, terms);
+                                                      yb, relu, terms, mbits);
   else if (qn == 2)
     bn_apply2d_kernel<__bf16, __bf16, 2><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
                                                            reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
-                                                           weight, bias, rb, y, yb, relu, terms);
+                                                           weight, bias, rb, y, yb, relu, terms, mbits);
   else
     bn_apply2d_kernel<__bf16, __bf16><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per,
                                                         reinterpret_cast<const __bf16 *>(x_bf16), mean, invstd,
-                                                        weight, bias, rb, y, yb, relu, terms);
+                                                        weight, bias, rb, y, yb, relu, terms, mbits);
 }
 
 static constexpr const float *kNoDy = nullptr;   // the statistics pass reads no gradient
 
-int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
-                            const float *bias, float *running_mean, float *running_var, float momentum, float eps,
-                            float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
-                            float *y, uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes,
-                            adaptseg_stream_t stream) {
+static int bn_fwd_train_impl(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                             const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                             float *y, uint16_t *y_bf16, uint32_t *relu_bits, int relu, void *ws, size_t ws_bytes,
+                             adaptseg_stream_t stream) {
+  AS_CHECK_ARG(!relu_bits || c % 32 == 0, "bn_fwd_train: a mask bitmap needs C %% 32 == 0 (C=%d)", c);
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_train: rows>0, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(rows > 1, "bn_fwd_train: expected more than 1 value per channel when training");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
@@ -880,10 +931,29 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
                                                                    save_invstd, running_mean, running_var, momentum, eps);
   AS_CHECK_LAUNCH("bn_stats_final");
   timing_begin(kTBnApply, s, fwd_apply_bytes(rows, c, x, res, res_bf16, y, y_bf16), &slot);
-  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s);
+  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s,
+               relu_bits);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                            float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                            float *y, uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes,
+                            adaptseg_stream_t stream) {
+  return bn_fwd_train_impl(rows, c, x, x_bf16, weight, bias, running_mean, running_var, momentum, eps, save_mean,
+                           save_invstd, res, res_bf16, y, y_bf16, nullptr, relu, ws, ws_bytes, stream);
+}
+
+int adaptseg_bn_fwd_train_xm(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                             const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                             float *y, uint16_t *y_bf16, uint32_t *relu_bits, int relu, void *ws, size_t ws_bytes,
+                             adaptseg_stream_t stream) {
+  return bn_fwd_train_impl(rows, c, x, x_bf16, weight, bias, running_mean, running_var, momentum, eps, save_mean,
+                           save_invstd, res, res_bf16, y, y_bf16, relu_bits, relu, ws, ws_bytes, stream);
 }
 
 int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weight, const float *bias,
@@ -894,11 +964,12 @@ int adaptseg_bn_fwd_train(int64_t rows, int c, const float *x, const float *weig
                                  save_mean, save_invstd, res, nullptr, y, nullptr, relu, ws, ws_bytes, stream);
 }
 
-int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
-                                  const uint16_t *x_bf16, const float *weight, const float *bias,
-                                  float *running_mean, float *running_var, float momentum, float eps,
-                                  float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
-                                  float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
+int adaptseg_bn_fwd_train_tiles_xm(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                   const uint16_t *x_bf16, const float *weight, const float *bias,
+                                   float *running_mean, float *running_var, float momentum, float eps,
+                                   float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                                   float *y, uint16_t *y_bf16, uint32_t *relu_bits, int relu, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(!relu_bits || c % 32 == 0, "bn_fwd_train_tiles: a mask bitmap needs C %% 32 == 0 (C=%d)", c);
   AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles: rows>1, C%%4==0 required (C=%d)", c);
   AS_CHECK_ARG(stats && ntiles > 0 && save_mean && save_invstd, "bn_fwd_train_tiles: null pointer");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_train_tiles: activation %d", relu);
@@ -910,10 +981,21 @@ int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int n
   AS_CHECK_LAUNCH("bn_tiles_final");
   int slot;  // x (+res) in, y out
   timing_begin(kTBnApply, s, fwd_apply_bytes(rows, c, x, res, res_bf16, y, y_bf16), &slot);
-  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s);
+  launch_apply(rows, c, x, x_bf16, save_mean, save_invstd, weight, bias, res, res_bf16, y, y_bf16, relu, s,
+               relu_bits);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
   return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                  const uint16_t *x_bf16, const float *weight, const float *bias,
+                                  float *running_mean, float *running_var, float momentum, float eps,
+                                  float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                                  float *y, uint16_t *y_bf16, int relu, adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_train_tiles_xm(rows, c, stats, ntiles, x, x_bf16, weight, bias, running_mean, running_var,
+                                        momentum, eps, save_mean, save_invstd, res, res_bf16, y, y_bf16, nullptr, relu,
+                                        stream);
 }
 
 int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int ntiles, const float *x,
@@ -924,10 +1006,11 @@ int adaptseg_bn_fwd_train_tiles(int64_t rows, int c, const float *stats, int nti
                                        momentum, eps, save_mean, save_invstd, res, nullptr, y, nullptr, relu, stream);
 }
 
-int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
-                            const float *bias, const float *running_mean, const float *running_var, float eps,
-                            const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
-                            adaptseg_stream_t stream) {
+int adaptseg_bn_fwd_infer_xm(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                             const float *bias, const float *running_mean, const float *running_var, float eps,
+                             const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16,
+                             uint32_t *relu_bits, int relu, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(!relu_bits || c % 32 == 0, "bn_fwd_infer: a mask bitmap needs C %% 32 == 0 (C=%d)", c);
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_fwd_infer: C%%4==0 required");
   AS_CHECK_ARG(running_mean && running_var, "bn_fwd_infer: null running statistics");
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_fwd_infer: activation %d", relu);
@@ -940,16 +1023,24 @@ int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t 
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
   if (x && rb)
     bn_infer_apply_kernel<float, X3><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
-                                                                      weight, bias, rb, y, yb, relu, terms);
+                                                                      weight, bias, rb, y, yb, relu, terms, relu_bits);
   else if (x)
     bn_infer_apply_kernel<float, float><<<grid_for(total4), 256, 0, s>>>(total4, c, x, running_mean, running_var, eps,
-                                                                         weight, bias, res, y, yb, relu, terms);
+                                                                         weight, bias, res, y, yb, relu, terms, relu_bits);
   else
     bn_infer_apply_kernel<__bf16, __bf16><<<grid_for(total4), 256, 0, s>>>(
         total4, c, reinterpret_cast<const __bf16 *>(x_bf16), running_mean, running_var, eps, weight, bias, rb, y, yb,
-        relu, terms);
+        relu, terms, relu_bits);
   AS_CHECK_LAUNCH("bn_infer_apply");
   return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                            const float *bias, const float *running_mean, const float *running_var, float eps,
+                            const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
+                            adaptseg_stream_t stream) {
+  return adaptseg_bn_fwd_infer_xm(rows, c, x, x_bf16, weight, bias, running_mean, running_var, eps, res, res_bf16, y,
+                                  y_bf16, nullptr, relu, stream);
 }
 
 int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight, const float *bias,
@@ -963,7 +1054,7 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_
                        const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
                        const float *bias, const float *save_mean, const float *save_invstd, float *dx, uint16_t *dx_bf16,
                        float *dres, uint16_t *dres_bf16, int relu, int train, float *dweight, float *dbias, void *ws,
-                       size_t ws_bytes, adaptseg_stream_t stream) {
+                       size_t ws_bytes, adaptseg_stream_t stream, const uint32_t *dy_bits = nullptr) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
   const bool xb = x_bf16 != nullptr, terms = copies_are_terms();
   AS_CHECK_ARG((dy != nullptr) != (dy_bf16 != nullptr), "bn_bwd: exactly one of dy / dy_bf16");
@@ -980,6 +1071,7 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_
   AS_CHECK_ARG(relu >= 0 && relu <= 2, "bn_bwd: activation %d (0 none, 1 ReLU, 2 LeakyReLU)", relu);
   AS_CHECK_ARG(!relu || y || y_bf16 || train, "bn_bwd: activation without y needs train mode (mask from x)");
   AS_CHECK_ARG(train || (!dweight && !dbias), "bn_bwd: affine gradients need train mode");
+  AS_CHECK_ARG(!dy_bits || c % 32 == 0, "bn_bwd: a mask bitmap needs C %% 32 == 0 (C=%d)", c);
   // mask mode: ReLU 1 (from the saved output y) / 2 (recomputed from x, y == NULL);
   // LeakyReLU 3 (from y) / 4 (from x)
   const bool has_y = y || y_bf16;
@@ -988,19 +1080,19 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_
   if (terms && y_bf16)
     return bn_bwd_launch<float, X3>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), x, weight, bias,
                                     save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
-                                    ws_bytes, s);
+                                    ws_bytes, s, dy_bits);
   if (xb || (!x && y_bf16)) {
     const __bf16 *yb = reinterpret_cast<const __bf16 *>(y_bf16), *xbb = reinterpret_cast<const __bf16 *>(x_bf16);
     if (dy_bf16)
       return bn_bwd_launch<__bf16, __bf16, __bf16>(rows, c, reinterpret_cast<const __bf16 *>(dy_bf16), yb, xbb, weight,
                                                    bias, save_mean, save_invstd, dx, dx_bf16,
                                                    reinterpret_cast<__bf16 *>(dres_bf16), rmode, train, dweight, dbias,
-                                                   ws, ws_bytes, s);
+                                                   ws, ws_bytes, s, dy_bits);
     return bn_bwd_launch<__bf16>(rows, c, dy, yb, xbb, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                 train, dweight, dbias, ws, ws_bytes, s);
+                                 train, dweight, dbias, ws, ws_bytes, s, dy_bits);
   }
   return bn_bwd_launch<float>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
-                              dweight, dbias, ws, ws_bytes, s);
+                              dweight, dbias, ws, ws_bytes, s, dy_bits);
 }
 
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
@@ -1018,13 +1110,13 @@ int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, cons
                      nullptr, relu, train, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
-int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const float *y,
-                       const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
-                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
-                       uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
+int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const uint32_t *dy_bits,
+                       const float *y, const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16,
+                       const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                       float *dx, uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
                        size_t ws_bytes, adaptseg_stream_t stream) {
   return bn_bwd_impl(rows, c, dy, dy_bf16, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16,
-                     dres, dres_bf16, relu, train, nullptr, nullptr, ws, ws_bytes, stream);
+                     dres, dres_bf16, relu, train, nullptr, nullptr, ws, ws_bytes, stream, dy_bits);
 }
 
 int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,

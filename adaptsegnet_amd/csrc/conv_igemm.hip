@@ -129,7 +129,11 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
       if (p.flags & ADAPTSEG_EPI_RESIDUAL) {
-        const float4 a = p.resb ? ldbf4(p.resb + idx) : *reinterpret_cast<const float4 *>(p.res + idx);
+        float4 a = p.resb ? ldbf4(p.resb + idx) : *reinterpret_cast<const float4 *>(p.res + idx);
+        if (p.resbits) {   // masked residual (4 consecutive channels: 4 bits of one word)
+          const uint32_t w = p.resbits[idx >> 5] >> (idx & 31);
+          a.x = (w & 1u) ? a.x : 0.f; a.y = (w & 2u) ? a.y : 0.f; a.z = (w & 4u) ? a.z : 0.f; a.w = (w & 8u) ? a.w : 0.f;
+        }
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
       v.x = epi_act(v.x, p.flags); v.y = epi_act(v.y, p.flags);
@@ -622,6 +626,47 @@ static bool splitk_vec(const ConvParams &q, const float *slab, const float *fina
   return vec;
 }
 
+// Split-K sums of the weight gradients on a high-priority companion stream
+// (adaptseg_set_wgrad_reduce_priority): the weight-gradient GEMMs run on a low-priority side
+// stream beside the main chain, and their short, HBM-bound sums then wait behind the main chain's
+// blocks for CU slots (in the c2 trace ~70 us per launch for ~26 MB) while the side stream's next
+// GEMM waits for them.  The companion stream is ordered after the GEMM and the caller's stream
+// after the sum (events), so the results keep the caller's stream order.
+struct HiReduce {
+  std::mutex mu;
+  bool enabled = false;
+  hipStream_t stream[16] = {};
+  std::vector<hipEvent_t> ring[16];
+  size_t next[16] = {};
+};
+static HiReduce g_hr;
+
+// (stream, event ring slot) of the calling thread's device, created on first use; nullptr: off
+static hipStream_t hr_stream(int &dev) {
+  if (!g_hr.enabled || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  if (!g_hr.stream[dev]) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&g_hr.stream[dev], hipStreamNonBlocking, hi) != hipSuccess) {
+      g_hr.stream[dev] = nullptr;
+      return nullptr;
+    }
+  }
+  return g_hr.stream[dev];
+}
+static hipEvent_t hr_event(int dev) {
+  // a ring of events: a wait captures the event's latest record when it is enqueued, so an event
+  // may be re-recorded once its waits are enqueued (both happen inside one run_plan call)
+  std::vector<hipEvent_t> &r = g_hr.ring[dev];
+  if (r.size() < 64) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    r.push_back(e);
+    return e;
+  }
+  return r[g_hr.next[dev]++ % r.size()];
+}
+
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
   if (!ws || ws_bytes < pl.slab_bytes) {
@@ -660,6 +705,16 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     return ADAPTSEG_ERR_HIP;
   }
   if (pl.p.splits > 1) {
+    hipStream_t caller = s;
+    std::unique_lock<std::mutex> hr_lock(g_hr.mu, std::defer_lock);
+    int dev = 0;
+    if (mode == MODE_WGRAD && g_hr.enabled) {
+      hr_lock.lock();
+      hipStream_t hs = hr_stream(dev);
+      hipEvent_t ea = hs ? hr_event(dev) : nullptr;
+      if (hs && ea && hipEventRecord(ea, caller) == hipSuccess && hipStreamWaitEvent(hs, ea, 0) == hipSuccess)
+        s = hs;
+    }
     ConvParams q = pl.p;
     q.out = final_out;
     const size_t total = (size_t)q.M * q.N;
@@ -683,6 +738,16 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     }
     timing_end(slot, s);
     AS_CHECK_LAUNCH("splitk_reduce");
+    if (s != caller) {   // the caller's stream resumes after the sum
+      hipEvent_t eb = hr_event(dev);
+      if (!eb || hipEventRecord(eb, s) != hipSuccess || hipStreamWaitEvent(caller, eb, 0) != hipSuccess) {
+        // fall back to a full sync of the companion stream: ordering must hold
+        if (hipStreamSynchronize(s) != hipSuccess) {
+          set_error("splitk_reduce: companion-stream ordering failed");
+          return ADAPTSEG_ERR_HIP;
+        }
+      }
+    }
   }
   return ADAPTSEG_OK;
 }
@@ -1018,14 +1083,14 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
                                adaptseg_stream_t stream) {
   AS_CHECK_ARG(dx, "conv bwd_data: null dx (bf16-only outputs: adaptseg_conv2d_bwd_data_xg)");
-  return adaptseg_conv2d_bwd_data_xg(d, dy, dy_bf16, w, w_pack, res, nullptr, aux, dx, dx_bf16, flags, ws, ws_bytes,
-                                     stream);
+  return adaptseg_conv2d_bwd_data_xg(d, dy, dy_bf16, w, w_pack, res, nullptr, nullptr, aux, dx, dx_bf16, flags, ws,
+                                     ws_bytes, stream);
 }
 
 int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                 const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
-                                const float *aux, float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
-                                adaptseg_stream_t stream) {
+                                const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags,
+                                void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
@@ -1037,6 +1102,8 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
   AS_CHECK_ARG(!gb || !(use_thin(d, ADAPTSEG_CONV_BWD_DATA) || tapgemm_eligible(d)),
                "conv bwd_data: the thin / tap-GEMM products take fp32 gradients only");
   AS_CHECK_ARG(!res_bf16 || aligned16(res_bf16), "conv bwd_data: res_bf16 must be 16-byte aligned");
+  AS_CHECK_ARG(!res_bits || (d->c % 32 == 0 && !(use_thin(d, ADAPTSEG_CONV_BWD_DATA) || tapgemm_eligible(d))),
+               "conv bwd_data: a residual mask bitmap needs Cin %% 32 == 0 and the implicit-GEMM path");
   AS_CHECK_ARG(dy || copy_only(pl, d, ADAPTSEG_CONV_BWD_DATA),
                "conv bwd_data: this product needs the fp32 dY (no bf16-operand kernel for it)");
   AS_CHECK_ARG(!(flags & (ADAPTSEG_EPI_LEAKY | ADAPTSEG_EPI_RELU)), "conv bwd_data: LEAKY/RELU not valid");
@@ -1071,6 +1138,7 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
   p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(dx_bf16);
   p.res = res;
   p.resb = reinterpret_cast<const __bf16 *>(res_bf16);
+  p.resbits = res_bits;
   p.aux = aux;
   p.flags = flags;
   st = attach_wpack(pl, w_pack);
@@ -1155,6 +1223,12 @@ int adaptseg_conv_set_math(int math) {
                    math == ADAPTSEG_MATH_F32X3 || math == ADAPTSEG_MATH_F32X3_PRESPLIT,
                "conv_set_math: bad math %d", math);
   g_conv_math.store(math);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_set_wgrad_reduce_priority(int enable) {
+  std::lock_guard<std::mutex> lk(g_hr.mu);
+  g_hr.enabled = enable != 0;
   return ADAPTSEG_OK;
 }
 

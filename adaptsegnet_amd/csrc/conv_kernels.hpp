@@ -56,6 +56,7 @@ struct ConvParams {
   const float *bias[4];        // FWD bias per segment (nullable)
   const float *res;            // residual (nullable)
   const __bf16 *resb;          // ... or the residual stored in bf16 (bf16 gradient storage; then res is NULL)
+  const uint32_t *resbits;     // optional mask bitmap of the residual [rows][N / 32]: res counts where the bit is set
   const float *aux;            // leaky-grad source (nullable)
   int flags;
   int kw_, kh_;                // kernel width / height (tap -> kh, kw)
@@ -74,7 +75,9 @@ __device__ __forceinline__ float epi_prev(const ConvParams &p, size_t idx) {
   return p.out ? p.out[idx] : (float)p.outb[idx];
 }
 __device__ __forceinline__ float epi_res(const ConvParams &p, size_t idx) {
-  return p.resb ? (float)p.resb[idx] : p.res[idx];
+  const float r = p.resb ? (float)p.resb[idx] : p.res[idx];
+  // (N % 32 == 0: element idx = row * N + col has bit col % 32 of word row * N / 32 + col / 32)
+  return (!p.resbits || ((p.resbits[idx >> 5] >> (idx & 31)) & 1u)) ? r : 0.f;
 }
 
 // ------------------------------------------------------------------------------------

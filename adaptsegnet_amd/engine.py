@@ -51,6 +51,8 @@ class WgradStream:
         side = WgradStream._streams.get(device.index)
         if side is None:
             side = WgradStream._streams[device.index] = torch.cuda.Stream(device)
+            # the weight gradients' split-K sums on a high-priority companion stream (A/B switch)
+            K.set_wgrad_reduce_priority(HI_REDUCE == 1)
         self.side = side
         self.used = False
 
@@ -112,6 +114,9 @@ def lowp_grads() -> bool:
     return lowp_storage() and BF16_GRADS == 1
 
 
+# (A/B switch) weight-gradient split-K sums on a high-priority companion stream
+HI_REDUCE = int(_os.environ.get("ADAPTSEG_HI_REDUCE", "1"))
+
 _BF16_SEL: dict = {}
 
 
@@ -135,21 +140,23 @@ def _copy_pays(g, n, h, w, ops) -> bool:
     return any(bf16_only(g, n, h, w, (op,)) for op in ops)
 
 
-def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False, fp32=True):
+def bn_forward_b(bn, x, res, relu, training, tiles=None, bf16=False, fp32=True, ybits=None):
     """bn_forward that also returns the bf16 copy of y (None unless ``bf16``); fp32=False skips
-    the fp32 y (returned as None) when every consumer reads the copy."""
+    the fp32 y (returned as None) when every consumer reads the copy.  ybits: a mask_bits_like
+    bitmap the pass fills with y's ReLU mask."""
     fp32 = fp32 or not bf16
     if training:
         if tiles is not None:
             r = K.bn_fwd_train_tiles(x, tiles, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                     bn.momentum, bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32)
+                                     bn.momentum, bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32,
+                                     ybits=ybits)
         else:
             r = K.bn_fwd_train(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
-                               bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32)
+                               bn.eps, res=res, relu=relu, bf16_out=bf16, fp32_out=fp32, ybits=ybits)
         y, mean, invstd = r[:3]
         return y, (mean, invstd, True), (r[3] if bf16 else None)
     r = K.bn_fwd_infer(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, res=res,
-                       relu=relu, bf16_out=bf16, fp32_out=fp32)
+                       relu=relu, bf16_out=bf16, fp32_out=fp32, ybits=ybits)
     y, yb = r if bf16 else (r, None)
     return y, (bn.running_mean, None, False), yb
 
@@ -161,17 +168,19 @@ def bn_forward(bn, x, res, relu, training, tiles=None):
     return y, st
 
 
-def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False, fp32=True):
+def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False, fp32=True,
+                dybits=None):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
     mode instead of reading the saved output y (one activation read less per pass).
-    bf16: return (dx, bf16 copy of dx) for the bf16-math data gradient that consumes dx."""
+    bf16: return (dx, bf16 copy of dx) for the bf16-math data gradient that consumes dx.
+    dybits: a mask bitmap applied to dy first (the Bottleneck's BN3 / downsample BN)."""
     mean, invstd, train = st
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
     elif mask_from_x and relu:
         y = None
     return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train,
-                    bias=bn.bias, bf16_out=bf16, fp32_out=fp32 or not bf16)
+                    bias=bn.bias, bf16_out=bf16, fp32_out=fp32 or not bf16, dybits=dybits)
 
 
 # ---------------------------------------------------------------------------------------
@@ -181,7 +190,12 @@ def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, b
 
 class BlockRec:
     __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
-                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b")
+                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3")
+
+
+# (A/B switch) the Bottleneck's output ReLU mask as a bitmap (1 bit per element) instead of the
+# stored block output: BN3's backward and the residual gradient read it
+MASK_BITS = int(_os.environ.get("ADAPTSEG_MASK_BITS", "1"))
 
 
 def _conv_bn(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
@@ -263,16 +277,21 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
             r = rb   # the residual stream is bf16
     else:
         r = xb if sh else x
-    out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh, fp32=not sh or out_fp32)
+    # the output's ReLU mask, out > 0, as a bitmap for the backward (BN3's mask and the residual
+    # gradient's): 1 bit per element instead of re-reading the stored output (4 B / 2 B) twice
+    bits3 = K.mask_bits_like(c3) if (save and MASK_BITS and g3.cout % 32 == 0) else None
+    out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh, fp32=not sh or out_fp32,
+                                 ybits=bits3)
     rec = None
     if save:
         rec = BlockRec()
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
-        rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, out, cd, sd
+        rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, (None if bits3 is not None else out), cd, sd
+        rec.bits3 = bits3
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
         rec.xb, rec.y1b, rec.y2b = xb, y1b if (sh or keep1) else None, y2b
-        if sh:
+        if sh and bits3 is None:
             rec.out = outb   # bf16 storage: the BN3 backward's mask source is the bf16 output
     return out, rec, outb
 
@@ -337,7 +356,11 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     # bf16 gradient storage: the data gradients are bf16 tensors; a BN backward whose fp32 output
     # is still wanted (f*: a consumer without a bf16-operand kernel) writes it to its own buffer
     lg = lowp_grads()
-    r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
+    bits = rec.bits3
+    if bits is not None:   # g = gout * bit: BN3's input gradient; the residual gradient stays implicit
+        r = bn_backward(blk.bn3, gout, None, rec.c3, rec.s3, relu=False, dybits=bits, bf16=sh, fp32=f3)
+    else:
+        r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
     dc3, dc3b = r if sh else (r, None)
     dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg)
     if need_w and blk.conv3.weight.grad is not None:
@@ -372,7 +395,8 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
         gd = dconv.geom()
-        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=None if lg else gout, bf16=sh, fp32=fd)
+        r = bn_backward(dbn, gout, None, rec.cd, rec.sd, relu=False, dx=None if lg else gout, bf16=sh, fp32=fd,
+                        dybits=bits)
         goutb = r[1] if sh else None
         gd_in = (r[0] if sh else r) if fd else None   # (gout keeps the residual gradient when not rewritten)
         if need_w and dconv.weight.grad is not None:
@@ -384,10 +408,11 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
         # identity residual, bf16 gradient storage, the input gradient stored unlike gout
         dx = torch.empty((n, h, w, g1.cin), device=gout.device,
                          dtype=torch.float32 if dx_fp32 else torch.bfloat16)
-        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, res=gout, dyb=dy1b)
+        K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=dx, res=gout, dyb=dy1b, resbits=bits)
     else:
-        # identity residual: dx = dgrad(conv1) + g, written over g in place
-        dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout, dyb=dy1b)
+        # identity residual: dx = dgrad(conv1) + g, written over g in place (g = gout * bit when
+        # the mask is a bitmap)
+        dx = K.conv_dgrad(g1, dy1, n, h, w, [blk.conv1.weight], out=gout, res=gout, dyb=dy1b, resbits=bits)
     return dx
 
 

@@ -260,19 +260,21 @@ def _aligned16(*ts) -> bool:
 
 
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
-               res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False, bf16_only: bool = False):
+               res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False, bf16_only: bool = False,
+               resbits=None):
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD).
     bf16_out: also return a bf16 copy of dx written by the epilogue -> (dx, dxb).
     bf16_only (or a bf16 ``out``): dx stored in bf16 only — bf16 gradient storage (BF16 maths);
-    ``res`` may be fp32 or bf16 (adaptseg_conv2d_bwd_data_xg)."""
+    ``res`` may be fp32 or bf16 (adaptseg_conv2d_bwd_data_xg).  resbits: a mask bitmap
+    (mask_bits_like) gating res element-wise."""
     if bf16_only or (out is not None and out.dtype == torch.bfloat16):
         if out is None:
             out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.bfloat16)
         if res is not None:
             flags |= EPI_RESIDUAL
         wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
-        _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, aux, None, out, (n, g.cin, h, w), _wshape(g), g.stride,
-                            g.pads, g.dils, flags)
+        _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, None, out, (n, g.cin, h, w), _wshape(g),
+                            g.stride, g.pads, g.dils, flags)
         return out
     if out is None:
         out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.float32)
@@ -282,8 +284,8 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
         flags |= EPI_LEAKY_GRAD
     outb = _bf16_like(out, bf16_out)
     wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
-    _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, aux, out, outb, (n, g.cin, h, w), _wshape(g), g.stride,
-                        g.pads, g.dils, flags)
+    _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, out, outb, (n, g.cin, h, w), _wshape(g),
+                        g.stride, g.pads, g.dils, flags)
     return (out, outb) if bf16_out else out
 
 
@@ -318,8 +320,17 @@ def _f32_like(t):
     return torch.empty(t.shape, device=t.device, dtype=torch.float32)
 
 
+def mask_bits_like(t):
+    """A ReLU mask bitmap for a [..., C] activation (C % 32 == 0): int32 [rows, C / 32], bit c % 32
+    of word (row, c / 32) = element (row, c) > 0 (written by the bn_fwd_* ``ybits`` argument)."""
+    c = t.shape[-1]
+    if c % 32:
+        raise RuntimeError(f"mask_bits_like: C must be a multiple of 32, got {c}")
+    return torch.empty((t.numel() // c, c // 32), device=t.device, dtype=torch.int32)
+
+
 def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                 relu=True, out=None, bf16_out=False, fp32_out=True):
+                 relu=True, out=None, bf16_out=False, fp32_out=True, ybits=None):
     """bf16_out: also return a bf16 (RNE) copy of y, the operand of a bf16-math conv: (y, mean,
     invstd, yb).  fp32_out=False (with bf16_out): only the copy is written, y is None.
     x / res may be bf16 tensors (bf16 activation storage), both or neither."""
@@ -328,37 +339,39 @@ def bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, res=
     yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
-    _OP.bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, float(momentum),
+    _OP.bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, ybits, mean, invstd, float(momentum),
                      float(eps), int(relu))
     return (y, mean, invstd, yb) if bf16_out else (y, mean, invstd)
 
 
 def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, momentum, eps, res=None,
-                       relu=True, out=None, bf16_out=False, fp32_out=True):
-    """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles."""
+                       relu=True, out=None, bf16_out=False, fp32_out=True, ybits=None):
+    """bn_fwd_train whose statistics come from conv_fwd_bnstats's row tiles.  ybits: the caller's
+    mask_bits_like(x) bitmap to fill with y's ReLU mask (or None)."""
     stats, ntiles = tiles
     c = x.shape[-1]
     y = (_f32_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
     yb = _bf16_like(x, bf16_out)
     mean = torch.empty(c, device=x.device, dtype=torch.float32)
     invstd = torch.empty(c, device=x.device, dtype=torch.float32)
-    _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, yb, mean,
+    _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, yb, ybits, mean,
                            invstd, float(momentum), float(eps), int(relu))
     return (y, mean, invstd, yb) if bf16_out else (y, mean, invstd)
 
 
 def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None,
-                 bf16_out=False, fp32_out=True):
+                 bf16_out=False, fp32_out=True, ybits=None):
     y = (_f32_like(x) if out is None else out) if (fp32_out or not bf16_out) else None
     yb = _bf16_like(x, bf16_out)
-    _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, float(eps), int(relu))
+    _OP.bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, ybits, float(eps), int(relu))
     return (y, yb) if bf16_out else y
 
 
 def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None,
-           bf16_out=False, fp32_out=True):
+           bf16_out=False, fp32_out=True, dybits=None):
     """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy.
     y=None with relu (train mode): the mask is recomputed from x, weight and bias.
+    dybits: a mask bitmap (mask_bits_like) applied to dy first, g = dy * bit.
     bf16_out: return (dx, dxb) with a bf16 (RNE) copy of dx (a bf16-math data-gradient operand);
     fp32_out=False (with bf16_out): only the copy is written, dx is None."""
     if not (fp32_out or not bf16_out):
@@ -366,7 +379,7 @@ def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=
     elif dx is None:
         dx = torch.empty(dy.shape, device=dy.device, dtype=torch.float32)
     dxb = _bf16_like(dy, bf16_out)
-    _OP.bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
+    _OP.bn_bwd(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
     return (dx, dxb) if bf16_out else dx
 
 
@@ -586,6 +599,12 @@ def conv_copy_operand_only(g: ConvGeom, n, h, w, op, strides=None) -> bool:
     check(_lib.lib().adaptseg_conv2d_copy_operand_only(ctypes.byref(d), op, ctypes.byref(only)),
           "conv2d_copy_operand_only")
     return bool(only.value)
+
+
+def set_wgrad_reduce_priority(enable: bool = True) -> None:
+    """Weight-gradient split-K sums on a high-priority companion stream (adaptseg.h
+    adaptseg_set_wgrad_reduce_priority; process-wide)."""
+    check(_lib.lib().adaptseg_set_wgrad_reduce_priority(1 if enable else 0), "set_wgrad_reduce_priority")
 
 
 def timing_enable(selector: int = -1, enable: bool = True):

@@ -78,6 +78,15 @@ def _pfb(t, n, what):
     return _pf(t, n, what), None
 
 
+def _pbits(t, n, what):
+    """Mask-bitmap pointer: int32 words, one bit per element of an n-element tensor."""
+    if t is None:
+        return None
+    if t.dtype != torch.int32 or t.numel() * 32 != n:
+        raise RuntimeError(f"{what}: expected an int32 bitmap of {n // 32} words, got {t.dtype} {tuple(t.shape)}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
 def _ptrs(ts):
     return _lib.ptr_array([None if t is None else t.data_ptr() for t in ts])
 
@@ -223,19 +232,20 @@ def _conv2d_fwd_bnstats(x, xb, weight, wpack, out, outb, stats, in_shape, in_str
                            f"{nt.value} (unaligned operand?)")
 
 
-@_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? aux, "
-     "Tensor(a!)? dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, "
-     "int flags) -> ()")
-def _conv2d_bwd_data(dy, dyb, weight, wpack, res, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
-    """res: fp32 or bf16; dx None: the output is stored in bf16 only (dxb) — bf16 gradient storage
-    (adaptseg_conv2d_bwd_data_xg)."""
+@_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? resbits, "
+     "Tensor? aux, Tensor(a!)? dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, "
+     "int[] dil, int flags) -> ()")
+def _conv2d_bwd_data(dy, dyb, weight, wpack, res, resbits, aux, dx, dxb, in_shape, w_shape, stride, pad, dil, flags):
+    """res: fp32 or bf16, masked by the bitmap resbits (int32 [rows, Cin / 32]) when given; dx None:
+    the output is stored in bf16 only (dxb) — bf16 gradient storage (adaptseg_conv2d_bwd_data_xg)."""
     n, c, h, w = in_shape
     d, ws, oh, ow = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
     wp, wsz = _ws_args(ws[CONV_BWD_DATA], (dx if dx is not None else dxb).device)
     nx, ny = n * h * w * c, n * oh * ow * w_shape[0]
     check(_lib.lib().adaptseg_conv2d_bwd_data_xg(
         ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_data dy"), _pc(dyb, ny, "conv2d_bwd_data dyb"), _ptrs(weight),
-        _p(wpack), *_pfb(res, nx, "conv2d_bwd_data res"), _pf(aux, nx, "conv2d_bwd_data aux"),
+        _p(wpack), *_pfb(res, nx, "conv2d_bwd_data res"), _pbits(resbits, nx, "conv2d_bwd_data resbits"),
+        _pf(aux, nx, "conv2d_bwd_data aux"),
         _pf(dx, nx, "conv2d_bwd_data dx"), _pc(dxb, nx, "conv2d_bwd_data dxb"), flags, wp, wsz, _stream()),
         "conv2d_bwd_data")
 
@@ -278,50 +288,60 @@ def _fb(t):
 
 
 @_op("bn_fwd_train(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-     "Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, "
-     "int act) -> ()")
-def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, mean, invstd, momentum, eps, act):
-    """x / res: fp32 or bf16 (bf16 activation storage, config c5)."""
+     "Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, Tensor(g!)? ybits, Tensor(d!) mean, Tensor(e!) invstd, "
+     "float momentum, float eps, int act) -> ()")
+def _bn_fwd_train(x, weight, bias, running_mean, running_var, res, y, yb, ybits, mean, invstd, momentum, eps, act):
+    """x / res: fp32 or bf16 (bf16 activation storage, config c5); ybits: the ReLU mask bitmap of y
+    (int32 [rows, C / 32]) or None."""
     rows, c = _rc(x)
+    n = rows * c
     wp, wsz = _ws_args(bn_ws_bytes(rows, c), x.device)
-    check(_lib.lib().adaptseg_bn_fwd_train_x(
-        rows, c, *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(momentum), float(eps),
-        _p(mean), _p(invstd), *_fb(res), _p(y), _p(yb), int(act), wp, wsz, _stream()), "bn_fwd_train")
+    check(_lib.lib().adaptseg_bn_fwd_train_xm(
+        rows, c, *_pfb(x, n, "bn_fwd_train x"), _p(weight), _p(bias), _p(running_mean), _p(running_var),
+        float(momentum), float(eps), _p(mean), _p(invstd), *_pfb(res, n, "bn_fwd_train res"),
+        _pf(y, n, "bn_fwd_train y"), _pc(yb, n, "bn_fwd_train yb"), _pbits(ybits, n, "bn_fwd_train ybits"),
+        int(act), wp, wsz, _stream()), "bn_fwd_train")
 
 
 @_op("bn_fwd_train_tiles(Tensor x, Tensor stats, int ntiles, Tensor? weight, Tensor? bias, "
      "Tensor(a!)? running_mean, Tensor(b!)? running_var, Tensor? res, Tensor(c!)? y, Tensor(f!)? yb, "
-     "Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
-def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, yb, mean, invstd,
+     "Tensor(g!)? ybits, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps, int act) -> ()")
+def _bn_fwd_train_tiles(x, stats, ntiles, weight, bias, running_mean, running_var, res, y, yb, ybits, mean, invstd,
                         momentum, eps, act):
     rows, c = _rc(x)
-    check(_lib.lib().adaptseg_bn_fwd_train_tiles_x(
-        rows, c, _p(stats), int(ntiles), *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var),
-        float(momentum), float(eps), _p(mean), _p(invstd), *_fb(res), _p(y), _p(yb), int(act), _stream()),
+    n = rows * c
+    check(_lib.lib().adaptseg_bn_fwd_train_tiles_xm(
+        rows, c, _p(stats), int(ntiles), *_pfb(x, n, "bn_fwd_train_tiles x"), _p(weight), _p(bias),
+        _p(running_mean), _p(running_var), float(momentum), float(eps), _p(mean), _p(invstd),
+        *_pfb(res, n, "bn_fwd_train_tiles res"), _pf(y, n, "bn_fwd_train_tiles y"),
+        _pc(yb, n, "bn_fwd_train_tiles yb"), _pbits(ybits, n, "bn_fwd_train_tiles ybits"), int(act), _stream()),
         "bn_fwd_train_tiles")
 
 
 @_op("bn_fwd_infer(Tensor x, Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
-     "Tensor? res, Tensor(a!)? y, Tensor(b!)? yb, float eps, int act) -> ()")
-def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, eps, act):
+     "Tensor? res, Tensor(a!)? y, Tensor(b!)? yb, Tensor(c!)? ybits, float eps, int act) -> ()")
+def _bn_fwd_infer(x, weight, bias, running_mean, running_var, res, y, yb, ybits, eps, act):
     rows, c = _rc(x)
-    check(_lib.lib().adaptseg_bn_fwd_infer_x(
-        rows, c, *_fb(x), _p(weight), _p(bias), _p(running_mean), _p(running_var), float(eps), *_fb(res), _p(y),
-        _p(yb), int(act), _stream()), "bn_fwd_infer")
+    n = rows * c
+    check(_lib.lib().adaptseg_bn_fwd_infer_xm(
+        rows, c, *_pfb(x, n, "bn_fwd_infer x"), _p(weight), _p(bias), _p(running_mean), _p(running_var),
+        float(eps), *_pfb(res, n, "bn_fwd_infer res"), _pf(y, n, "bn_fwd_infer y"), _pc(yb, n, "bn_fwd_infer yb"),
+        _pbits(ybits, n, "bn_fwd_infer ybits"), int(act), _stream()), "bn_fwd_infer")
 
 
-@_op("bn_bwd(Tensor dy, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, Tensor invstd, "
-     "Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
-def _bn_bwd(dy, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
+@_op("bn_bwd(Tensor dy, Tensor? dybits, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor? mean, "
+     "Tensor invstd, Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, bool train) -> ()")
+def _bn_bwd(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, train):
     """y / x (the saved activations): fp32 or bf16; dy and dres fp32, or both bf16 (bf16 gradient
-    storage, adaptseg_bn_bwd_xg); dx fp32."""
+    storage, adaptseg_bn_bwd_xg); dx fp32; dybits: a mask bitmap applied to dy (or None)."""
     rows, c = _rc(dy)
     n = rows * c
     wp, wsz = _ws_args(bn_ws_bytes(rows, c) if train else 0, dy.device)
     check(_lib.lib().adaptseg_bn_bwd_xg(
-        rows, c, *_pfb(dy, n, "bn_bwd dy"), *_pfb(y, n, "bn_bwd y"), *_pfb(x, n, "bn_bwd x"), _p(weight),
-        _p(bias), _p(mean), _p(invstd), _pf(dx, n, "bn_bwd dx"), _pc(dxb, n, "bn_bwd dxb"),
-        *_pfb(dres, n, "bn_bwd dres"), int(act), 1 if train else 0, wp, wsz, _stream()), "bn_bwd")
+        rows, c, *_pfb(dy, n, "bn_bwd dy"), _pbits(dybits, n, "bn_bwd dybits"), *_pfb(y, n, "bn_bwd y"),
+        *_pfb(x, n, "bn_bwd x"), _p(weight), _p(bias), _p(mean), _p(invstd), _pf(dx, n, "bn_bwd dx"),
+        _pc(dxb, n, "bn_bwd dxb"), *_pfb(dres, n, "bn_bwd dres"), int(act), 1 if train else 0, wp, wsz, _stream()),
+        "bn_bwd")
 
 
 @_op("bn_bwd_affine(Tensor dy, Tensor? y, Tensor x, Tensor? weight, Tensor? bias, Tensor mean, "

@@ -183,11 +183,15 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
    dx == NULL stores the output in bf16 only (dx_bf16: RNE of the fp32 epilogue value), and then
    ADAPTSEG_EPI_ACCUMULATE adds to dx_bf16.  The thin (Cout <= 4) and tap-GEMM products keep fp32
    gradients (ADAPTSEG_ERR_ARG for res_bf16 / dx == NULL there, and under the F32X3 maths).
-   adaptseg_conv2d_bwd_data_x is this with res_bf16 = NULL and dx != NULL. */
+   res_bits (any conv maths; Cin % 32 == 0; NULL = none): a ReLU mask bitmap [rows][Cin / 32] of
+   the residual (written by adaptseg_bn_fwd_*_xm) — the epilogue adds res only where the bit is
+   set, i.e. the masked residual gradient g = gout * [out > 0] of a Bottleneck (deeplab_multi.py:
+   96-103) read straight from gout, so the BN backward need not write g out.
+   adaptseg_conv2d_bwd_data_x is this with res_bf16 = res_bits = NULL and dx != NULL. */
 int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                 const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
-                                const float *aux, float *dx, uint16_t *dx_bf16, int flags, void *ws, size_t ws_bytes,
-                                adaptseg_stream_t stream);
+                                const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags,
+                                void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
    (Cin and Cout multiples of 8) reads them; other kernels ignore them.  Exception: the
@@ -208,6 +212,14 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
                                float *const *dw, float *const *db, int flags, void *ws,
                                size_t ws_bytes, adaptseg_stream_t stream);
+
+/* Process-wide: run the split-K sums of the weight gradients on a high-priority companion stream
+   of the calling thread's device (enable != 0), ordered after the GEMM by an event and followed
+   by an event the caller's stream waits on — results keep the caller's stream order.  For a
+   caller that issues weight gradients on a low-priority stream beside a high-priority one (the
+   step's side stream), so their short HBM-bound sums do not queue behind the other stream's
+   blocks.  Default off. */
+int adaptseg_set_wgrad_reduce_priority(int enable);
 
 /* ------------------------------------------------------------------------------------ */
 /* BatchNorm2d, train mode (batch statistics) with fused residual add and ReLU.          */
@@ -253,6 +265,24 @@ int adaptseg_bn_fwd_infer_x(int64_t rows, int c, const float *x, const uint16_t 
                             const float *bias, const float *running_mean, const float *running_var, float eps,
                             const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16, int relu,
                             adaptseg_stream_t stream);
+/* The _x forward passes that also write the ReLU mask bitmap of y (relu_bits, [rows][c / 32]
+   uint32, c % 32 == 0; bit c % 32 of word (row, c / 32) = y > 0): the backward then reads 1 bit
+   per element instead of the stored y (adaptseg_bn_bwd_xg dy_bits, adaptseg_conv2d_bwd_data_xg
+   res_bits). */
+int adaptseg_bn_fwd_train_xm(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                             const float *bias, float *running_mean, float *running_var, float momentum, float eps,
+                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                             float *y, uint16_t *y_bf16, uint32_t *relu_bits, int relu, void *ws, size_t ws_bytes,
+                             adaptseg_stream_t stream);
+int adaptseg_bn_fwd_train_tiles_xm(int64_t rows, int c, const float *stats, int ntiles, const float *x,
+                                   const uint16_t *x_bf16, const float *weight, const float *bias,
+                                   float *running_mean, float *running_var, float momentum, float eps,
+                                   float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
+                                   float *y, uint16_t *y_bf16, uint32_t *relu_bits, int relu, adaptseg_stream_t stream);
+int adaptseg_bn_fwd_infer_xm(int64_t rows, int c, const float *x, const uint16_t *x_bf16, const float *weight,
+                             const float *bias, const float *running_mean, const float *running_var, float eps,
+                             const float *res, const uint16_t *res_bf16, float *y, uint16_t *y_bf16,
+                             uint32_t *relu_bits, int relu, adaptseg_stream_t stream);
 
 /* Eval-mode BN (running statistics): y = (x-rm)/sqrt(rv+eps)*w + b (+res), ReLU if relu. */
 int adaptseg_bn_fwd_infer(int64_t rows, int c, const float *x, const float *weight,
@@ -282,11 +312,15 @@ int adaptseg_bn_bwd_x(int64_t rows, int c, const float *dy, const float *y, cons
 /* adaptseg_bn_bwd_x with bf16 GRADIENT storage (BF16 conv maths with bf16 activation storage,
    config c5): the incoming gradient is dy (fp32) or dy_bf16 (exactly one), and the residual
    gradient dres is written like it (dres / dres_bf16; it may alias dy of the same storage).  dx
-   is fp32 and / or its bf16 copy, as in adaptseg_bn_bwd_x (for bf16 storage: dx_bf16 only). */
-int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const float *y,
-                       const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
-                       const float *bias, const float *save_mean, const float *save_invstd, float *dx,
-                       uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
+   is fp32 and / or its bf16 copy, as in adaptseg_bn_bwd_x (for bf16 storage: dx_bf16 only).
+   dy_bits (any maths; C % 32 == 0; NULL = none): a mask bitmap [rows][c / 32] applied to dy
+   first, g = dy * bit (then the `relu` mask as usual) — the Bottleneck's BN3 backward with its
+   ReLU mask from the forward's bitmap (relu = 0), and the downsample BN's, whose incoming
+   gradient is that same masked g. */
+int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const uint32_t *dy_bits,
+                       const float *y, const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16,
+                       const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                       float *dx, uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
                        size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's

@@ -561,13 +561,14 @@ def test_custom_ops_opcheck():
     cases = [
         (ops.conv2d_fwd.default, (x, None, [wt], None, [None], None, y, None, [n, cin, h, w], [h * w * cin, 1, w * cin, cin],
                                   [cout, cin, 3, 3], 1, [1], [1], 0)),
-        (ops.conv2d_bwd_data.default, (r(n, h, w, cout), None, [wt], None, None, None, torch.empty_like(x), None, [n, cin, h, w],
+        (ops.conv2d_bwd_data.default, (r(n, h, w, cout), None, [wt], None, None, None, None, torch.empty_like(x), None, [n, cin, h, w],
                                        [cout, cin, 3, 3], 1, [1], [1], 0)),
         (ops.conv2d_bwd_weight.default, (r(n, h, w, cout), None, x, None, [torch.zeros_like(wt)], [], [n, cin, h, w],
                                          [h * w * cin, 1, w * cin, cin], [cout, cin, 3, 3], 1, [1], [1], 2)),
         (ops.bn_fwd_train.default, (r(n, h, w, cout), r(cout), r(cout), torch.zeros(cout, device=DEV),
                                     torch.ones(cout, device=DEV), None, torch.empty(n, h, w, cout, device=DEV),
-                                    None, torch.empty(cout, device=DEV), torch.empty(cout, device=DEV), 0.1, 1e-5, 1)),
+                                    None, torch.empty(n * h * w, 1, device=DEV, dtype=torch.int32),
+                                    torch.empty(cout, device=DEV), torch.empty(cout, device=DEV), 0.1, 1e-5, 1)),
         (ops.upsample_bilinear_fwd.default, (r(n, 4, 5, 19), torch.empty(n, 13, 17, 19, device=DEV))),
         (ops.softmax_fwd.default, (r(n, h, w, 19), torch.empty(n, h, w, 19, device=DEV))),
         (ops.softmax_ce_fwd.default, (r(n, h, w, 19), torch.randint(0, 19, (n, h, w), generator=g).to(DEV), 255,

@@ -9,7 +9,8 @@ CrossEntropy2d — with /root/reference/model/deeplab_multi.py + utils/loss.py a
 oracle/reference_torch.py, and (2) one single-level adversarial step at batch 1, 1024x512 (the
 c2 shape bench.py's ``cpu_baseline`` times) with the reference modules composed as
 train_gta2cityscapes_multi.py:379-464 and with ``oracle_step``.  SURVEY §8(d) asks the
-restatement to match the reference within +-10 %.  Writes profiles/r1/cpu_calibration.json.
+restatement to match the reference within +-10 %.  Writes profiles/r4/cpu_calibration.json
+(round 1's run: profiles/r1/).
 """
 from __future__ import annotations
 
@@ -30,14 +31,19 @@ sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 from oracle import reference_torch as R  # noqa: E402
 
 
-def best_of(fn, reps):
-    fn()  # warm-up
-    ts = []
+def best_of_pair(fa, fb, reps):
+    """min time of fa and of fb over ``reps`` interleaved repetitions (after one warm-up each):
+    alternating keeps allocator / oneDNN-cache / thermal drift from favouring either side (run
+    back to back, the same pair measured anywhere from -12 % to +16 % apart)."""
+    fa()
+    fb()
+    ta, tb = [], []
     for _ in range(reps):
-        t0 = time.perf_counter()
-        fn()
-        ts.append(time.perf_counter() - t0)
-    return min(ts), ts
+        for f, ts in ((fa, ta), (fb, tb)):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+    return min(ta), min(tb)
 
 
 def main():
@@ -71,8 +77,7 @@ def main():
             _, p2 = R.g_forward(G, x1, (321, 321), train=True)
             R.cross_entropy2d(p2, l1)
 
-    out["c1_reference_s"], _ = best_of(ref_c1, args.reps)
-    out["c1_port_s"], _ = best_of(port_c1, args.reps)
+    out["c1_reference_s"], out["c1_port_s"] = best_of_pair(ref_c1, port_c1, args.reps)
 
     # ---- c2 shape, batch 1: one single-level step ------------------------------------------
     xs = torch.from_numpy(R.det_images((1, 3, 512, 1024), 1)).float()
@@ -116,11 +121,11 @@ def main():
     def port_step():
         R.oracle_step(Gp, None, D2p, opts, cfg, 0, [(xs, lab, xt)])
 
-    out["c2b1_step_reference_s"], _ = best_of(ref_step, args.reps)
-    out["c2b1_step_port_s"], _ = best_of(port_step, args.reps)
+    out["c2b1_step_reference_s"], out["c2b1_step_port_s"] = best_of_pair(ref_step, port_step, args.reps)
     out["c1_port_over_reference"] = out["c1_port_s"] / out["c1_reference_s"]
     out["c2b1_port_over_reference"] = out["c2b1_step_port_s"] / out["c2b1_step_reference_s"]
-    path = os.path.join(REPO, "profiles", "r1", "cpu_calibration.json")
+    out["reps"] = args.reps
+    path = os.path.join(REPO, "profiles", "r4", "cpu_calibration.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))
 
