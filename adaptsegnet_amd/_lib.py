@@ -121,7 +121,6 @@ _SIGS = {
     "adaptseg_grid_warp_bwd_workspace_size": [_I, _I, _I, _I, ctypes.POINTER(_SZ)],
     "adaptseg_grid_warp_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
-    "adaptseg_set_wgrad_reduce_priority": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_enable_mem": [_I],

@@ -626,47 +626,6 @@ static bool splitk_vec(const ConvParams &q, const float *slab, const float *fina
   return vec;
 }
 
-// Split-K sums of the weight gradients on a high-priority companion stream
-// (adaptseg_set_wgrad_reduce_priority): the weight-gradient GEMMs run on a low-priority side
-// stream beside the main chain, and their short, HBM-bound sums then wait behind the main chain's
-// blocks for CU slots (in the c2 trace ~70 us per launch for ~26 MB) while the side stream's next
-// GEMM waits for them.  The companion stream is ordered after the GEMM and the caller's stream
-// after the sum (events), so the results keep the caller's stream order.
-struct HiReduce {
-  std::mutex mu;
-  bool enabled = false;
-  hipStream_t stream[16] = {};
-  std::vector<hipEvent_t> ring[16];
-  size_t next[16] = {};
-};
-static HiReduce g_hr;
-
-// (stream, event ring slot) of the calling thread's device, created on first use; nullptr: off
-static hipStream_t hr_stream(int &dev) {
-  if (!g_hr.enabled || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  if (!g_hr.stream[dev]) {
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&g_hr.stream[dev], hipStreamNonBlocking, hi) != hipSuccess) {
-      g_hr.stream[dev] = nullptr;
-      return nullptr;
-    }
-  }
-  return g_hr.stream[dev];
-}
-static hipEvent_t hr_event(int dev) {
-  // a ring of events: a wait captures the event's latest record when it is enqueued, so an event
-  // may be re-recorded once its waits are enqueued (both happen inside one run_plan call)
-  std::vector<hipEvent_t> &r = g_hr.ring[dev];
-  if (r.size() < 64) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    r.push_back(e);
-    return e;
-  }
-  return r[g_hr.next[dev]++ % r.size()];
-}
-
 int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   float *final_out = pl.p.out;
   if (!ws || ws_bytes < pl.slab_bytes) {
@@ -705,16 +664,6 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     return ADAPTSEG_ERR_HIP;
   }
   if (pl.p.splits > 1) {
-    hipStream_t caller = s;
-    std::unique_lock<std::mutex> hr_lock(g_hr.mu, std::defer_lock);
-    int dev = 0;
-    if (mode == MODE_WGRAD && g_hr.enabled) {
-      hr_lock.lock();
-      hipStream_t hs = hr_stream(dev);
-      hipEvent_t ea = hs ? hr_event(dev) : nullptr;
-      if (hs && ea && hipEventRecord(ea, caller) == hipSuccess && hipStreamWaitEvent(hs, ea, 0) == hipSuccess)
-        s = hs;
-    }
     ConvParams q = pl.p;
     q.out = final_out;
     const size_t total = (size_t)q.M * q.N;
@@ -738,16 +687,6 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     }
     timing_end(slot, s);
     AS_CHECK_LAUNCH("splitk_reduce");
-    if (s != caller) {   // the caller's stream resumes after the sum
-      hipEvent_t eb = hr_event(dev);
-      if (!eb || hipEventRecord(eb, s) != hipSuccess || hipStreamWaitEvent(caller, eb, 0) != hipSuccess) {
-        // fall back to a full sync of the companion stream: ordering must hold
-        if (hipStreamSynchronize(s) != hipSuccess) {
-          set_error("splitk_reduce: companion-stream ordering failed");
-          return ADAPTSEG_ERR_HIP;
-        }
-      }
-    }
   }
   return ADAPTSEG_OK;
 }
@@ -1223,12 +1162,6 @@ int adaptseg_conv_set_math(int math) {
                    math == ADAPTSEG_MATH_F32X3 || math == ADAPTSEG_MATH_F32X3_PRESPLIT,
                "conv_set_math: bad math %d", math);
   g_conv_math.store(math);
-  return ADAPTSEG_OK;
-}
-
-int adaptseg_set_wgrad_reduce_priority(int enable) {
-  std::lock_guard<std::mutex> lk(g_hr.mu);
-  g_hr.enabled = enable != 0;
   return ADAPTSEG_OK;
 }
 

@@ -51,8 +51,6 @@ class WgradStream:
         side = WgradStream._streams.get(device.index)
         if side is None:
             side = WgradStream._streams[device.index] = torch.cuda.Stream(device)
-            # the weight gradients' split-K sums on a high-priority companion stream (A/B switch)
-            K.set_wgrad_reduce_priority(HI_REDUCE == 1)
         self.side = side
         self.used = False
 
@@ -113,9 +111,6 @@ def lowp_grads() -> bool:
     accumulating into layer4.0's input gradient) write that one in fp32."""
     return lowp_storage() and BF16_GRADS == 1
 
-
-# (A/B switch) weight-gradient split-K sums on a high-priority companion stream
-HI_REDUCE = int(_os.environ.get("ADAPTSEG_HI_REDUCE", "1"))
 
 _BF16_SEL: dict = {}
 
@@ -279,7 +274,9 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         r = xb if sh else x
     # the output's ReLU mask, out > 0, as a bitmap for the backward (BN3's mask and the residual
     # gradient's): 1 bit per element instead of re-reading the stored output (4 B / 2 B) twice
-    bits3 = K.mask_bits_like(c3) if (save and MASK_BITS and g3.cout % 32 == 0) else None
+    # (fp32 storage only: with bf16 storage the output re-read costs 2 B, and the masked residual
+    # in the bf16 data-gradient epilogue measured c5 -1.2 %, profiles/r4/mask_bits_ab.txt)
+    bits3 = K.mask_bits_like(c3) if (save and MASK_BITS and not lp and g3.cout % 32 == 0) else None
     out, s3, outb = bn_forward_b(blk.bn3, c3, r, True, training, t3, bf16=sh, fp32=not sh or out_fp32,
                                  ybits=bits3)
     rec = None

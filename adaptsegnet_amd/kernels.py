@@ -601,12 +601,6 @@ def conv_copy_operand_only(g: ConvGeom, n, h, w, op, strides=None) -> bool:
     return bool(only.value)
 
 
-def set_wgrad_reduce_priority(enable: bool = True) -> None:
-    """Weight-gradient split-K sums on a high-priority companion stream (adaptseg.h
-    adaptseg_set_wgrad_reduce_priority; process-wide)."""
-    check(_lib.lib().adaptseg_set_wgrad_reduce_priority(1 if enable else 0), "set_wgrad_reduce_priority")
-
-
 def timing_enable(selector: int = -1, enable: bool = True):
     check(_lib.lib().adaptseg_timing_enable(1 if enable else 0, int(selector)), "timing_enable")
 

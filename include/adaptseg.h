@@ -213,14 +213,6 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
                                float *const *dw, float *const *db, int flags, void *ws,
                                size_t ws_bytes, adaptseg_stream_t stream);
 
-/* Process-wide: run the split-K sums of the weight gradients on a high-priority companion stream
-   of the calling thread's device (enable != 0), ordered after the GEMM by an event and followed
-   by an event the caller's stream waits on — results keep the caller's stream order.  For a
-   caller that issues weight gradients on a low-priority stream beside a high-priority one (the
-   step's side stream), so their short HBM-bound sums do not queue behind the other stream's
-   blocks.  Default off. */
-int adaptseg_set_wgrad_reduce_priority(int enable);
-
 /* ------------------------------------------------------------------------------------ */
 /* BatchNorm2d, train mode (batch statistics) with fused residual add and ReLU.          */
 /* Replaces nn.BatchNorm2d + ReLU + "out += residual" in model/deeplab_multi.py:65-101, */
