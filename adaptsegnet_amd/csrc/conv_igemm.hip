@@ -58,9 +58,8 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
   }
 }
 
-// four bf16 (8-B aligned) as a float4
-__device__ __forceinline__ float4 ldbf4(const __bf16 *p) {
-  const uint2 u = *reinterpret_cast<const uint2 *>(p);
+
+__device__ __forceinline__ float4 bf4_of(uint2 u) {
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                      __uint_as_float(u.y & 0xffff0000u));
 }
@@ -68,7 +67,10 @@ __device__ __forceinline__ float4 ldbf4(const __bf16 *p) {
 // Vectorised split-K reduction: 4 consecutive columns per thread (N % 4 == 0 and, for weight
 // gradients, segments of kseg % 4 == 0), 32-bit indexing.  G split-groups per block: thread
 // (g, lane) sums slabs g, g+G, ... of float4 `lane`, then the G partials are added in fixed
-// order through LDS — deterministic, and a 256-split reduce is 16 loads deep, not 256.
+// order through LDS — deterministic, and a 256-split reduce is 16 loads deep, not 256.  The
+// read-back operands (accumulate target, residual and its bitmap) are loaded raw BEFORE the slab
+// loads, so their latency overlaps the slabs' instead of following it (round 4; bf16 images as
+// raw words, converted at the use).
 template <int G>
 __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p, const float *__restrict__ slab,
                                                              int mode, FastDiv fdn4) {
@@ -77,9 +79,40 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
   const uint32_t total4 = (uint32_t)p.M * n4;
   const float4 *s4 = reinterpret_cast<const float4 *>(slab);
   const int lane = threadIdx.x % L, g = threadIdx.x / L;
+  const int flags = p.flags;
+  const bool acc_f = flags & ADAPTSEG_EPI_ACCUMULATE;
+  const bool res_f = mode != MODE_WGRAD && (flags & ADAPTSEG_EPI_RESIDUAL);
   __shared__ float4 red[G > 1 ? 256 : 1];
   for (uint32_t base = blockIdx.x * L; base < total4; base += gridDim.x * L) {  // block-uniform trip count
     const uint32_t i = base + lane;
+    const bool fin = i < total4 && (G == 1 || g == 0);   // this thread finishes float4 i
+    const uint32_t row = fin ? fdiv(i, fdn4) : 0;
+    const int col = fin ? (int)(i - row * n4) * 4 : 0;
+    float *o = nullptr;
+    size_t idx = 0;
+    float4 prev = make_float4(0.f, 0.f, 0.f, 0.f), resv = prev;
+    uint2 prevb = make_uint2(0, 0), resb = prevb;
+    uint32_t rw = ~0u;
+    if (fin) {
+      if (mode == MODE_WGRAD) {
+        const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
+        float *dst = seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3];
+        o = dst + (size_t)row * p.kseg + (col - seg * p.kseg);
+        if (acc_f) prev = *reinterpret_cast<const float4 *>(o);
+      } else {
+        idx = (size_t)row * p.N + col;
+        o = p.out ? p.out + idx : nullptr;   // NULL: bf16 storage, the output is p.outb
+        if (acc_f) {
+          if (o) prev = *reinterpret_cast<const float4 *>(o);
+          else prevb = *reinterpret_cast<const uint2 *>(p.outb + idx);
+        }
+        if (res_f) {
+          if (p.resb) resb = *reinterpret_cast<const uint2 *>(p.resb + idx);
+          else resv = *reinterpret_cast<const float4 *>(p.res + idx);
+          if (p.resbits) rw = p.resbits[idx >> 5] >> (idx & 31);   // 4 consecutive channels: 4 bits
+        }
+      }
+    }
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < total4) {
 #pragma unroll 8
@@ -97,24 +130,13 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
           v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
         }
       __syncthreads();
-      if (g != 0) continue;
     }
-    if (i >= total4) continue;
-    const uint32_t row = fdiv(i, fdn4);
-    const int col = (int)(i - row * n4) * 4;
-    float *o = nullptr;
-    size_t idx = 0;
+    if (!fin) continue;
     if (mode == MODE_WGRAD) {
-      const int seg = (int)fdiv((uint32_t)col, p.fd_nseg_k);
-      float *dst = seg == 0 ? p.dw[0] : seg == 1 ? p.dw[1] : seg == 2 ? p.dw[2] : p.dw[3];
-      o = dst + (size_t)row * p.kseg + (col - seg * p.kseg);
-      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
-        const float4 a = *reinterpret_cast<const float4 *>(o);
-        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      if (acc_f) {
+        v.x += prev.x; v.y += prev.y; v.z += prev.z; v.w += prev.w;
       }
     } else {
-      idx = (size_t)row * p.N + col;
-      o = p.out ? p.out + idx : nullptr;   // NULL: bf16 storage, the output is p.outb
       if (mode == MODE_FWD) {
         for (int s = 0; s < p.nseg; ++s) {
           const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
@@ -124,24 +146,21 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
           }
         }
       }
-      if (p.flags & ADAPTSEG_EPI_ACCUMULATE) {
-        const float4 a = o ? *reinterpret_cast<const float4 *>(o) : ldbf4(p.outb + idx);
+      if (acc_f) {
+        const float4 a = o ? prev : bf4_of(prevb);
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
-      if (p.flags & ADAPTSEG_EPI_RESIDUAL) {
-        float4 a = p.resb ? ldbf4(p.resb + idx) : *reinterpret_cast<const float4 *>(p.res + idx);
-        if (p.resbits) {   // masked residual (4 consecutive channels: 4 bits of one word)
-          const uint32_t w = p.resbits[idx >> 5] >> (idx & 31);
-          a.x = (w & 1u) ? a.x : 0.f; a.y = (w & 2u) ? a.y : 0.f; a.z = (w & 4u) ? a.z : 0.f; a.w = (w & 8u) ? a.w : 0.f;
-        }
+      if (res_f) {
+        float4 a = p.resb ? bf4_of(resb) : resv;
+        a.x = (rw & 1u) ? a.x : 0.f; a.y = (rw & 2u) ? a.y : 0.f; a.z = (rw & 4u) ? a.z : 0.f; a.w = (rw & 8u) ? a.w : 0.f;
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
-      v.x = epi_act(v.x, p.flags); v.y = epi_act(v.y, p.flags);
-      v.z = epi_act(v.z, p.flags); v.w = epi_act(v.w, p.flags);
-      if (p.flags & kEpiActGrad) {
+      v.x = epi_act(v.x, flags); v.y = epi_act(v.y, flags);
+      v.z = epi_act(v.z, flags); v.w = epi_act(v.w, flags);
+      if (flags & kEpiActGrad) {
         const float4 a = *reinterpret_cast<const float4 *>(p.aux + idx);
-        v.x = epi_act_grad(v.x, a.x, p.flags); v.y = epi_act_grad(v.y, a.y, p.flags);
-        v.z = epi_act_grad(v.z, a.z, p.flags); v.w = epi_act_grad(v.w, a.w, p.flags);
+        v.x = epi_act_grad(v.x, a.x, flags); v.y = epi_act_grad(v.y, a.y, flags);
+        v.z = epi_act_grad(v.z, a.z, flags); v.w = epi_act_grad(v.w, a.w, flags);
       }
     }
     if (o) *reinterpret_cast<float4 *>(o) = v;   // (NULL: bf16 storage, only the copy below)

@@ -211,7 +211,7 @@ def selector_symbol(sel):
 def pmc_traffic(config, sel):
     """Per-launch HBM-side bytes of the dominant kernel from the committed PMC passes
     (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command)."""
-    for rnd in ("r3", "r2", "r1"):   # newest committed pass first
+    for rnd in ("r4", "r3", "r2", "r1"):   # newest committed pass first
         path = os.path.join(REPO, "profiles", rnd, "pmc", f"traffic_{config}.json")
         try:
             d = json.load(open(path))
