@@ -59,7 +59,7 @@ __device__ __forceinline__ int g16_off(int r, int ch) {
 // CU — half the operand bytes per MFMA of the 128x256 tile, for products whose M x N fills the
 // chip with such tiles.
 template <int MODE, int BM, int BN, int BK, bool S2 = false>
-__global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 2 : 1) igemm_bf16g_kernel(const ConvParams p,
+__global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) igemm_bf16g_kernel(const ConvParams p,
                                                                               const __bf16 *__restrict__ ab,
                                                                               const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
@@ -262,7 +262,8 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 2 : 1) ig
     __syncthreads();  // the epilogue reuses the LDS
   }
 
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+  static_assert(kG16Stages * STAGE >= WAVES_M * WAVES_N * 32 * 33 * 4, "LDS for the bf16x8 epilogue");
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 8, true>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }
 

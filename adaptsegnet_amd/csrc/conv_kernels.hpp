@@ -742,6 +742,71 @@ __device__ __forceinline__ void epi_store_rows(const ConvParams &p, const floatx
   }
 }
 
+__device__ __forceinline__ bool has_bias(const ConvParams &p) {
+  return p.bias[0] || (p.nseg > 1 && (p.bias[1] || (p.nseg > 2 && (p.bias[2] || (p.nseg > 3 && p.bias[3])))));
+}
+
+// bf16-only outputs (bf16 activation / gradient storage, config c5; no bias) of a full tile: each wave
+// stages one 32x32 accumulator block at a time through its own 4.2 KB of LDS and writes rows of
+// eight bf16 per lane (16 B), reading the bf16 residual / accumulate target the same way —
+// instead of a 2-B store and a 2-B read-back per element, which left the memory-bound bf16
+// layer-1/2 data gradients at 1.6-3 TB/s alone (profiles/r4/c5_dgrad_pmc.txt).  No block barrier:
+// the LDS region is the wave's own (LDS operations of a wave complete in order).
+template <int EK, int MODE, int TM, int TN>
+__device__ __forceinline__ void epi_store_bf16x8(const ConvParams &p, const floatx16 (&acc)[TM][TN], int bm, int bn,
+                                                 int wm, int wn, int wtm, int wtn, int lane, int wave, float *lds) {
+  constexpr int LS = 33;                       // padded row stride (floats) of the staging block
+  float *w = lds + wave * (32 * LS);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int c8 = (lane & 3) * 8;               // this lane's 8-column chunk ...
+  const int rr = lane >> 2;                    // ... of rows rr and rr + 16
+  const uint32_t N = (uint32_t)p.N;
+  const int flags = p.flags;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int gcol = bn + wn * wtn + j * 32 + c8;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_barrier(0);   // one block's operands live at a time
+      const int grow = bm + wm * wtm + i * 32 + rr;
+      uint4 rd[2];
+      if constexpr (EK != EK_PLAIN) {   // the read-backs first (16 B per lane and row)
+        const __bf16 *src = EK == EK_RES_BF16 ? p.resb : p.outb;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          rd[h] = *reinterpret_cast<const uint4 *>(src + (size_t)((uint32_t)(grow + 16 * h) * N + gcol));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w[((r & 3) + 8 * (r >> 2) + 4 * hh) * LS + l32] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's stores land before its reads
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = w[(rr + 16 * h) * LS + c8 + q];
+        if constexpr (EK != EK_PLAIN) {
+          const uint32_t u[4] = {rd[h].x, rd[h].y, rd[h].z, rd[h].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] += __uint_as_float(u[q] << 16);
+            v[2 * q + 1] += __uint_as_float(u[q] & 0xffff0000u);
+          }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a = epi_act(v[2 * q], flags), b = epi_act(v[2 * q + 1], flags);
+          o[q] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) |
+                 ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+        }
+        *reinterpret_cast<uint4 *>(p.outb + (size_t)((uint32_t)(grow + 16 * h) * N + gcol)) =
+            make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's staging
+    }
+  }
+}
+
 // The general store (stride-2 parity scatter, activation gradients, accumulate + residual, or
 // outputs of >= 2^30 elements): per-element read-backs.
 template <int MODE, int TM, int TN, typename ROWF>
@@ -785,8 +850,9 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
 // residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
 // `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
 // RB: rows per read-back batch (8), or 0: the per-element path only (the kernel built for three
-// blocks per CU, whose 168-VGPR budget the batched variants overflow).
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int RB = 8>
+// blocks per CU, whose 168-VGPR budget the batched variants overflow).  V8: the kernel's LDS
+// holds WAVES_M * WAVES_N * 4.2 KB for epi_store_bf16x8 (the bf16-output LDS-DMA kernels).
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int RB = 8, bool V8 = false>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
                                                int bm, int bn, int tm, int tn, int split, int M, int Hc,
                                                int Wc, int py, int px, float *lds) {
@@ -854,7 +920,21 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
     }
 #define AS_EPI(EK_) \
   if constexpr (RB > 0) epi_store_rows<EK_, MODE, TM, TN, RB>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M)
-    switch (ek) {
+    bool v8 = false;
+    if constexpr (V8 && !S2) {
+      v8 = full && !p.out && p.outb && !p.resbits && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
+           (ek == EK_PLAIN || ek == EK_RES_BF16 || ek == EK_ACC_BF16) &&
+           !(reinterpret_cast<uintptr_t>(p.outb) & 15) && (ek != EK_RES_BF16 || !(reinterpret_cast<uintptr_t>(p.resb) & 15));
+      if (v8) {
+        if (ek == EK_PLAIN) epi_store_bf16x8<EK_PLAIN, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+        else if (ek == EK_RES_BF16)
+          epi_store_bf16x8<EK_RES_BF16, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+        else epi_store_bf16x8<EK_ACC_BF16, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+      }
+    }
+    if (V8 && !v8) {   // (the bf16-output kernels: the batched kinds do not fit their 128 VGPRs)
+      epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);
+    } else if (!v8) switch (ek) {
       case EK_PLAIN: AS_EPI(EK_PLAIN); break;
       case EK_RES_F32: AS_EPI(EK_RES_F32); break;
       case EK_RES_BF16: AS_EPI(EK_RES_BF16); break;
