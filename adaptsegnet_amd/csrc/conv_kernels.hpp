@@ -807,6 +807,64 @@ __device__ __forceinline__ void epi_store_bf16x8(const ConvParams &p, const floa
   }
 }
 
+// fp32 outputs of a full tile (F32X3 / fp32 kernels; no bias, no bf16 copy): each wave stages one
+// 32x32 accumulator block at a time through its own 4.6 KB of LDS and writes rows of four fp32
+// per lane (16 B), reading the residual (+ its bitmap word) / accumulate target the same way —
+// a quarter of the per-element path's memory instructions.
+template <int EK, int MODE, int TM, int TN>
+__device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const floatx16 (&acc)[TM][TN], int bm, int bn,
+                                                int wm, int wn, int wtm, int wtn, int lane, int wave, float *lds) {
+  constexpr int LS = 36;                       // padded row stride: 16-B aligned rows for ds_read_b128
+  float *w = lds + wave * (32 * LS);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int c4 = (lane & 7) * 4;               // this lane's 4-column chunk ...
+  const int rr = lane >> 3;                    // ... of rows rr + 8 h, h = 0..3
+  const uint32_t N = (uint32_t)p.N;
+  const int flags = p.flags;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int gcol = bn + wn * wtn + j * 32 + c4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_barrier(0);   // one block's operands live at a time
+      const int grow = bm + wm * wtm + i * 32 + rr;
+      float4 rd[4];
+      uint32_t rb[4];
+      if constexpr (EK != EK_PLAIN) {   // the read-backs first (16 B per lane and row)
+        const float *src = EK == EK_RES_F32 ? p.res : p.out;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t e = (uint32_t)(grow + 8 * h) * N + gcol;
+          rd[h] = ld_e<float4>(src, e >> 2);
+          rb[h] = (EK == EK_RES_F32 && p.resbits) ? ld_word(p.resbits, e) : ~0u;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w[((r & 3) + 8 * (r >> 2) + 4 * hh) * LS + l32] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's stores land before its reads
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t e = (uint32_t)(grow + 8 * h) * N + gcol;
+        float4 v = *reinterpret_cast<const float4 *>(w + (rr + 8 * h) * LS + c4);
+        if constexpr (EK == EK_ACC_F32) {
+          v.x += rd[h].x; v.y += rd[h].y; v.z += rd[h].z; v.w += rd[h].w;
+        }
+        if constexpr (EK == EK_RES_F32) {
+          const uint32_t m = rb[h] >> (e & 31);
+          v.x += (m & 1u) ? rd[h].x : 0.f;
+          v.y += (m & 2u) ? rd[h].y : 0.f;
+          v.z += (m & 4u) ? rd[h].z : 0.f;
+          v.w += (m & 8u) ? rd[h].w : 0.f;
+        }
+        v.x = epi_act(v.x, flags); v.y = epi_act(v.y, flags);
+        v.z = epi_act(v.z, flags); v.w = epi_act(v.w, flags);
+        st_e<float4>(p.out, e >> 2, v);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's staging
+    }
+  }
+}
+
 // The general store (stride-2 parity scatter, activation gradients, accumulate + residual, or
 // outputs of >= 2^30 elements): per-element read-backs.
 template <int MODE, int TM, int TN, typename ROWF>
@@ -850,9 +908,11 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
 // residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
 // `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
 // RB: rows per read-back batch (8), or 0: the per-element path only (the kernel built for three
-// blocks per CU, whose 168-VGPR budget the batched variants overflow).  V8: the kernel's LDS
-// holds WAVES_M * WAVES_N * 4.2 KB for epi_store_bf16x8 (the bf16-output LDS-DMA kernels).
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int RB = 8, bool V8 = false>
+// blocks per CU, whose 168-VGPR budget the batched variants overflow).  VEC: the LDS-transposed
+// 16-B stores of full tiles — 1: bf16 outputs (epi_store_bf16x8, the bf16-output LDS-DMA kernels),
+// 2: fp32 outputs (epi_store_f32x4, the F32X3 kernels); the kernel's LDS holds WAVES_M * WAVES_N *
+// 4.6 KB; its other tiles take the per-element path (the batched kinds do not fit beside them).
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int RB = 8, int VEC = 0>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
                                                int bm, int bn, int tm, int tn, int split, int M, int Hc,
                                                int Wc, int py, int px, float *lds) {
@@ -920,21 +980,32 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
     }
 #define AS_EPI(EK_) \
   if constexpr (RB > 0) epi_store_rows<EK_, MODE, TM, TN, RB>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M)
-    bool v8 = false;
-    if constexpr (V8 && !S2) {
-      v8 = full && !p.out && p.outb && !p.resbits && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
-           (ek == EK_PLAIN || ek == EK_RES_BF16 || ek == EK_ACC_BF16) &&
-           !(reinterpret_cast<uintptr_t>(p.outb) & 15) && (ek != EK_RES_BF16 || !(reinterpret_cast<uintptr_t>(p.resb) & 15));
-      if (v8) {
+    bool vec = false;
+    if constexpr (VEC == 1 && !S2) {
+      vec = full && !p.out && p.outb && !p.resbits && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
+            (ek == EK_PLAIN || ek == EK_RES_BF16 || ek == EK_ACC_BF16) &&
+            !(reinterpret_cast<uintptr_t>(p.outb) & 15) && (ek != EK_RES_BF16 || !(reinterpret_cast<uintptr_t>(p.resb) & 15));
+      if (vec) {
         if (ek == EK_PLAIN) epi_store_bf16x8<EK_PLAIN, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
         else if (ek == EK_RES_BF16)
           epi_store_bf16x8<EK_RES_BF16, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
         else epi_store_bf16x8<EK_ACC_BF16, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
       }
     }
-    if (V8 && !v8) {   // (the bf16-output kernels: the batched kinds do not fit their 128 VGPRs)
+    if constexpr (VEC == 2 && !S2) {
+      vec = full && p.out && !p.outb && (p.N & 3) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
+            (ek == EK_PLAIN || ek == EK_RES_F32 || ek == EK_ACC_F32) && !(reinterpret_cast<uintptr_t>(p.out) & 15) &&
+            (ek != EK_RES_F32 || !(reinterpret_cast<uintptr_t>(p.res) & 15));
+      if (vec) {
+        if (ek == EK_PLAIN) epi_store_f32x4<EK_PLAIN, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+        else if (ek == EK_RES_F32)
+          epi_store_f32x4<EK_RES_F32, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+        else epi_store_f32x4<EK_ACC_F32, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+      }
+    }
+    if (VEC && !vec) {
       epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);
-    } else if (!v8) switch (ek) {
+    } else if (!vec) switch (ek) {
       case EK_PLAIN: AS_EPI(EK_PLAIN); break;
       case EK_RES_F32: AS_EPI(EK_RES_F32); break;
       case EK_RES_BF16: AS_EPI(EK_RES_BF16); break;

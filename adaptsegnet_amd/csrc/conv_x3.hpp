@@ -398,7 +398,8 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] += accs[i][j];
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+  static_assert(sizeof(lds) >= WAVES_M * WAVES_N * 32 * 36 * 4, "LDS for the f32x4 epilogue");
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 8, 2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }
 
