@@ -157,6 +157,10 @@ constexpr int kBnMinBlocks = 1;
 // ~2 blocks per CU for the reduce and apply passes: they share the chip with the weight-gradient
 // GEMMs of the side stream (2048 blocks measured -0.3 % at c2 with the F32X3 kernels)
 constexpr int kReduceBlocks = 512, kApplyBlocks = 512;
+// the forward apply passes run without the weight-gradient stream beside them: 1024 blocks
+// (c5 +2.0 %, c2 +0.5 %; 2048: +1.9 / +0.2 %; the backward passes at 1024: c5 -1.2 %,
+// profiles/r4/bn_grids_ab.txt)
+constexpr int kApplyBlocksFwd = 1024;
 
 // Forward activation: 0 none, 1 ReLU, 2 LeakyReLU(0.2) (model/custom_layers.py:83-96).
 __device__ __forceinline__ float fwd_act(float v, int act) {
@@ -685,7 +689,7 @@ struct ApplyPlan {
   int64_t per;
 };
 
-static ApplyPlan apply_plan(int64_t rows, int C, int qn = 1) {
+static ApplyPlan apply_plan(int64_t rows, int C, int qn = 1, int blocks = kApplyBlocks) {
   ApplyPlan a;
   const int groups = C / (4 * qn);   // channel groups of qn quads
   a.tc = std::min(groups, 64);
@@ -695,7 +699,7 @@ static ApplyPlan apply_plan(int64_t rows, int C, int qn = 1) {
   const int tr = 256 / a.tc;
   // ~2 blocks per CU: the apply passes run beside the weight-gradient GEMMs; 512 blocks measured
   // +0.8 % at c2 over 2048 (c3 equal), 256 -0.6 % (two runs each)
-  const int want = std::max(1, kApplyBlocks / a.cblocks);
+  const int want = std::max(1, blocks / a.cblocks);
   const int64_t maxs = std::max<int64_t>(1, ceil_div(rows, (int64_t)tr * (qn == 2 ? kBf16Rows : kApplyUnroll)));
   a.rsplits = (int)std::min<int64_t>(want, maxs);
   a.per = ceil_div(rows, a.rsplits);
@@ -867,7 +871,7 @@ static void launch_apply(int64_t rows, int c, const float *x, const uint16_t *x_
   uint2 *yb = reinterpret_cast<uint2 *>(y_bf16);
   const __bf16 *rb = reinterpret_cast<const __bf16 *>(res_bf16);
   const int qn = (!x && !terms) ? bf16_qn(c, {x_bf16, res_bf16, y, y_bf16}) : 1;
-  const ApplyPlan ap = apply_plan(rows, c, qn);
+  const ApplyPlan ap = apply_plan(rows, c, qn, kApplyBlocksFwd);
   const dim3 g(ap.cblocks, ap.rsplits);
   if (x && rb)
     bn_apply2d_kernel<float, X3><<<g, 256, 0, s>>>(rows, c, ap.tc, ap.per, x, mean, invstd, weight, bias, rb, y, yb,
