@@ -55,10 +55,12 @@ CONFIGS = {
 }
 
 
-def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None):
+def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None, nbytes=None):
     """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector.  ``products``
     (a set), when given, also collects every (op, selector, split-K?) the step launches
-    (host-side planning only: tests/test_conv_coverage.py runs it without a GPU)."""
+    (host-side planning only: tests/test_conv_coverage.py runs it without a GPU).  ``nbytes``
+    (a dict), when given, receives each selector's algorithmic HBM bytes per step: every
+    operand read once and the output written once, fp32 (4 B; bf16 math 2 B) per element."""
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd import engine
     inv = {}
@@ -72,6 +74,12 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None)
         # (engine.x3_forward_terms)
         kid, sp = K.conv_kernel_id(geom, n, h, w, op, strides, copies=(cp and copies) or terms)
         inv[kid] = inv.get(kid, 0.0) + count * (algo or geom).flops(n, h, w)
+        if nbytes is not None:
+            g = algo or geom
+            oh, ow = g.out_hw(h, w)
+            eb = 2 if K.get_conv_math() == K.MATH_BF16 else 4
+            elems = n * h * w * g.cin + g.cout * g.cin * g.kh * g.kw * len(g.pads) + n * oh * ow * g.cout
+            nbytes[kid] = nbytes.get(kid, 0.0) + count * eb * elems
         if products is not None:
             products.add((op, kid, sp > 1))
 
@@ -360,7 +368,8 @@ def main():
         trainer.step(i, batches)
     torch.cuda.synchronize()
 
-    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize)
+    inv_bytes = {}
+    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes)
     step_flops = sum(inv.values())
     # the roofline kernel: the symbol with the most algorithmic FLOPs per step
     dom = max(inv, key=inv.get)
@@ -459,6 +468,11 @@ def main():
                            "frac_of_fp32_mfma_peak": ach / FP32_MFMA_PEAK_TFLOPS,
                            "traffic_unit": "bytes/launch (L2 memory-side FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": tsrc,
+                           # operands read once + output written once, per launch: traffic well
+                           # above it = operand re-reads (per tap / column tile, served by MALL)
+                           "algorithmic_bytes_per_launch": inv_bytes.get(dom, 0.0) * args.steps / k_launches,
+                           "traffic_over_algorithmic": (traffic / (inv_bytes[dom] * args.steps / k_launches)
+                                                        if traffic and inv_bytes.get(dom) else None),
                            "algorithmic_flop_per_launch": k_flops / k_launches,
                            "launched_flop_per_launch": launched_flops / k_launches,
                            "kernel": selector_symbol(dom), "selector": dom,
