@@ -278,8 +278,9 @@ def cpu_baseline(threads):
                          "1 warm-up + 2 timed",
             "c3_images_per_s": 1.0 / c3_s,
             "c1_forward_ce_s": times[-1],
-            "calibration": "the port times within +6 % (step) / -12 % (c1) of the reference's own "
-                           "modules on the same cores (profiles/r1/cpu_calibration.json)"}
+            "calibration": "the port times within +3.3 % (step) / -3.2 % (c1) of the reference's own "
+                           "modules on the same 8 cores, interleaved best of 6 "
+                           "(profiles/r4/cpu_calibration.json)"}
 
 
 def init_distributed(backend, local, init=None, set_device=None):
