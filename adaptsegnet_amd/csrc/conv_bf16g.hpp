@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
   }
 
   static_assert(kG16Stages * STAGE >= WAVES_M * WAVES_N * 32 * 33 * 4, "LDS for the bf16x8 epilogue");
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 8, 1>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 1>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }
 

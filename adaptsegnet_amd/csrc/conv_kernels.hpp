@@ -662,15 +662,12 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
   dx = kw * dil - pad;
 }
 
-// ---- epilogue read-backs -------------------------------------------------------------
-// Every operand the epilogue reads back (the residual and its mask bitmap, the accumulate target)
-// is loaded for a whole 16-row batch before any of it is used: a value used right after its load
-// — or a load issued after a store it may alias, as the in-place residual's is — waits out the
-// full memory latency once per element (the layer-3 conv1 data gradient with its in-place
-// residual took 405 us per launch for the FLOPs of its 131-us conv3 twin, profiles/r4).  8-row
-// batches (16 spilled the register-staged data gradient at 128 VGPRs).  The
-// batch loads land in plain VGPRs (bf16 as zero-extended ushort: a d16 load would merge into its
-// destination) and are converted at their use.
+// ---- epilogue stores and read-backs ----------------------------------------------------
+// The per-element path read the residual / accumulate target between stores; a store may alias
+// them (the in-place residual), so each load waited out the full memory latency once per element
+// (the layer-3 conv1 data gradient took 405 us per launch for the FLOPs of its 131-us conv3 twin,
+// profiles/r4).  The LDS-transposed paths below load a whole 32x32 block's read-backs as 16-B
+// rows before its first store.  Read-back kinds (uniform per launch):
 enum { EK_PLAIN = 0, EK_RES_F32 = 1, EK_RES_BF16 = 2, EK_ACC_F32 = 3, EK_ACC_BF16 = 4, EK_GENERAL = 5 };
 
 __device__ __forceinline__ float bf16_bits_to_float(uint32_t u) { return __uint_as_float(u << 16); }
@@ -687,59 +684,6 @@ template <typename T> __device__ __forceinline__ void st_e(void *base, uint32_t 
 }
 __device__ __forceinline__ uint32_t ld_word(const uint32_t *bits, uint32_t e) {
   return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(bits) + ((e >> 5) << 2));
-}
-
-// The fwd / data-grad store of one launch's tile (stride 1, < 2^30 output elements) for one
-// read-back kind.
-template <int EK, int MODE, int TM, int TN, int RB>
-__device__ __forceinline__ void epi_store_rows(const ConvParams &p, const floatx16 (&acc)[TM][TN], int bm, int bn,
-                                               int wm, int wn, int wtm, int wtn, int hh, int l32, bool full, int M) {
-  const int flags = p.flags;
-  const uint32_t N = (uint32_t)p.N;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = bn + wn * wtn + j * 32 + l32;
-    if (!full && col >= p.N) continue;
-    float bsum = 0.f;
-    if constexpr (MODE == MODE_FWD) {
-      for (int s = 0; s < p.nseg; ++s) {
-        const float *bp = s == 0 ? p.bias[0] : s == 1 ? p.bias[1] : s == 2 ? p.bias[2] : p.bias[3];
-        if (bp) bsum += bp[col];
-      }
-    }
-#pragma unroll
-    for (int ih = 0; ih < (16 / RB) * TM; ++ih) {   // batches of RB rows
-      const int i = ih / (16 / RB), r0 = (ih % (16 / RB)) * RB;
-      float ld[16];
-      uint32_t lw[16], lb[16];
-      if constexpr (EK != EK_PLAIN) {
-#pragma unroll
-        for (int r = r0; r < r0 + RB; ++r) {
-          const int row = bm + wm * wtm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const uint32_t e = (uint32_t)(full || row < M ? row : bm) * N + col;   // clamped: row bm exists
-          if constexpr (EK == EK_RES_F32) ld[r] = ld_e<float>(p.res, e);
-          if constexpr (EK == EK_RES_BF16) lw[r] = ld_e<uint16_t>(p.resb, e);
-          if constexpr (EK == EK_RES_F32 || EK == EK_RES_BF16) lb[r] = p.resbits ? ld_word(p.resbits, e) : ~0u;
-          if constexpr (EK == EK_ACC_F32) ld[r] = ld_e<float>(p.out, e);
-          if constexpr (EK == EK_ACC_BF16) lw[r] = ld_e<uint16_t>(p.outb, e);
-        }
-      }
-#pragma unroll
-      for (int r = r0; r < r0 + RB; ++r) {
-        const int row = bm + wm * wtm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (!full && row >= M) continue;
-        const uint32_t e = (uint32_t)row * N + col;
-        float v = acc[i][j][r] + bsum;
-        if constexpr (EK == EK_ACC_F32) v += ld[r];
-        if constexpr (EK == EK_ACC_BF16) v += bf16_bits_to_float(lw[r]);
-        if constexpr (EK == EK_RES_F32) v += bit_of(lb[r], e) ? ld[r] : 0.f;
-        if constexpr (EK == EK_RES_BF16) v += bit_of(lb[r], e) ? bf16_bits_to_float(lw[r]) : 0.f;
-        v = epi_act(v, flags);
-        if (p.out) st_e<float>(p.out, e, v);   // NULL: bf16 storage, only the copy below
-        if (p.outb) st_e<__bf16>(p.outb, e, (__bf16)v);
-      }
-    }
-  }
 }
 
 __device__ __forceinline__ bool has_bias(const ConvParams &p) {
@@ -907,12 +851,14 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
 // (per segment, optional accumulate) and the fwd / data-grad epilogue (bias, accumulate,
 // residual, activation and its gradient, stride-2 parity scatter, fused BN statistics).
 // `lds` must hold WAVES_M * BN floats and be free (the caller's main loop ended on a barrier).
-// RB: rows per read-back batch (8), or 0: the per-element path only (the kernel built for three
-// blocks per CU, whose 168-VGPR budget the batched variants overflow).  VEC: the LDS-transposed
-// 16-B stores of full tiles — 1: bf16 outputs (epi_store_bf16x8, the bf16-output LDS-DMA kernels),
-// 2: fp32 outputs (epi_store_f32x4, the F32X3 kernels); the kernel's LDS holds WAVES_M * WAVES_N *
-// 4.6 KB; its other tiles take the per-element path (the batched kinds do not fit beside them).
-template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int RB = 8, int VEC = 0>
+// VEC: the LDS-transposed 16-B stores of full tiles — 1: bf16 outputs (epi_store_bf16x8, the
+// bf16-output LDS-DMA kernels), 2: fp32 outputs (epi_store_f32x4, the F32X3 kernels); the
+// kernel's LDS holds WAVES_M * WAVES_N * 4.6 KB.  Every other tile and kernel (VEC 0: the
+// fp32-MFMA and register-staged bf16 kernels) takes the per-element path.  (Round 4's batched
+// per-element read-back kinds took those kernels from 82-97 to 184-217 VGPRs — the stem's
+// forward kernel from three waves per SIMD to one, c4 −1.3 % against round 3 on one box,
+// profiles/r4/c4_r3_ab.txt — and were removed.)
+template <int MODE, int BM, int BN, int WAVES_M, int WAVES_N, bool S2, int VEC = 0>
 __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&acc)[BM / WAVES_M / 32][BN / WAVES_N / 32],
                                                int bm, int bn, int tm, int tn, int split, int M, int Hc,
                                                int Wc, int py, int px, float *lds) {
@@ -970,16 +916,14 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
     }
   } else {
     const int flags = p.flags;
-    // the batched kinds: stride 1, < 2^30 output elements (32-bit byte offsets)
+    // the LDS-transposed kinds: stride 1, < 2^30 output elements (32-bit byte offsets)
     int ek = EK_GENERAL;
-    if (RB > 0 && !S2 && (uint64_t)p.M * (uint64_t)p.N < (1ull << 30) && !(flags & kEpiActGrad)) {
+    if (VEC > 0 && !S2 && (uint64_t)p.M * (uint64_t)p.N < (1ull << 30) && !(flags & kEpiActGrad)) {
       const int rf = flags & (ADAPTSEG_EPI_ACCUMULATE | ADAPTSEG_EPI_RESIDUAL);
       if (rf == 0) ek = EK_PLAIN;
       else if (rf == ADAPTSEG_EPI_RESIDUAL) ek = p.resb ? EK_RES_BF16 : EK_RES_F32;
       else if (rf == ADAPTSEG_EPI_ACCUMULATE) ek = p.out ? EK_ACC_F32 : EK_ACC_BF16;
     }
-#define AS_EPI(EK_) \
-  if constexpr (RB > 0) epi_store_rows<EK_, MODE, TM, TN, RB>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M)
     bool vec = false;
     if constexpr (VEC == 1 && !S2) {
       vec = full && !p.out && p.outb && !p.resbits && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
@@ -1003,17 +947,7 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
         else epi_store_f32x4<EK_ACC_F32, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
       }
     }
-    if (VEC && !vec) {
-      epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);
-    } else if (!vec) switch (ek) {
-      case EK_PLAIN: AS_EPI(EK_PLAIN); break;
-      case EK_RES_F32: AS_EPI(EK_RES_F32); break;
-      case EK_RES_BF16: AS_EPI(EK_RES_BF16); break;
-      case EK_ACC_F32: AS_EPI(EK_ACC_F32); break;
-      case EK_ACC_BF16: AS_EPI(EK_ACC_BF16); break;
-      default: epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row); break;
-    }
-#undef AS_EPI
+    if (!vec) epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);
     if constexpr (MODE == MODE_FWD && !S2) {
       // BatchNorm statistics of this row tile, straight from the accumulators (the BN that
       // consumes this conv then skips its statistics pass over y): per column the tile's
@@ -1520,8 +1454,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N, MINB) igemm_fast_kerne
   }
 
   // ---- epilogue ----
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, MINB >= 3 ? 0 : 8>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py,
-                                                                        px, lds);
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px, lds);
 }
 
 

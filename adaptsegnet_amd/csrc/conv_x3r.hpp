@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3r_kernel(const ConvParams p, c
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] += accs[i][j];
   static_assert(sizeof(lds) >= WAVES_M * WAVES_N * 32 * 36 * 4, "LDS for the f32x4 epilogue");
-  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 8, 2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
+  igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }
 
