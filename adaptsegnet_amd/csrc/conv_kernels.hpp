@@ -668,7 +668,8 @@ __device__ __forceinline__ void seg_geom(const ConvParams &p, const SegRegs &sr,
 // (the layer-3 conv1 data gradient took 405 us per launch for the FLOPs of its 131-us conv3 twin,
 // profiles/r4).  The LDS-transposed paths below load a whole 32x32 block's read-backs as 16-B
 // rows before its first store.  Read-back kinds (uniform per launch):
-enum { EK_PLAIN = 0, EK_RES_F32 = 1, EK_RES_BF16 = 2, EK_ACC_F32 = 3, EK_ACC_BF16 = 4, EK_GENERAL = 5 };
+enum { EK_PLAIN = 0, EK_RES_F32 = 1, EK_RES_BF16 = 2, EK_ACC_F32 = 3, EK_ACC_BF16 = 4, EK_GENERAL = 5,
+       EK_ACTGRAD = 6 };   // (EK_ACTGRAD: an activation gradient from aux, the fp32 path only)
 
 __device__ __forceinline__ float bf16_bits_to_float(uint32_t u) { return __uint_as_float(u << 16); }
 
@@ -755,9 +756,21 @@ __device__ __forceinline__ void epi_store_bf16x8(const ConvParams &p, const floa
 // 32x32 accumulator block at a time through its own 4.6 KB of LDS and writes rows of four fp32
 // per lane (16 B), reading the residual (+ its bitmap word) / accumulate target the same way —
 // a quarter of the per-element path's memory instructions.
-template <int EK, int MODE, int TM, int TN>
+template <int EK, int MODE, int TM, int TN, bool S2>
 __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const floatx16 (&acc)[TM][TN], int bm, int bn,
-                                                int wm, int wn, int wtm, int wtn, int lane, int wave, float *lds) {
+                                                int wm, int wn, int wtm, int wtn, int lane, int wave, float *lds,
+                                                int Hc, int Wc, int py, int px) {
+  // output row of GEMM row `row` (S2: the parity class's pixel back in the NHWC image; a pixel's
+  // channels stay contiguous, so the 16-B rows hold)
+  auto orow = [&](int row) -> uint32_t {
+    if constexpr (S2) {
+      const int jj = row % Wc, t2 = row / Wc;
+      const int ii = t2 % Hc, b = t2 / Hc;
+      return (uint32_t)((b * p.h + 2 * ii + py) * p.w + 2 * jj + px);
+    } else {
+      return (uint32_t)row;
+    }
+  };
   constexpr int LS = 36;                       // padded row stride: 16-B aligned rows for ds_read_b128
   float *w = lds + wave * (32 * LS);
   const int l32 = lane & 31, hh = lane >> 5;
@@ -775,10 +788,10 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
       float4 rd[4];
       uint32_t rb[4];
       if constexpr (EK != EK_PLAIN) {   // the read-backs first (16 B per lane and row)
-        const float *src = EK == EK_RES_F32 ? p.res : p.out;
+        const float *src = EK == EK_RES_F32 ? p.res : EK == EK_ACTGRAD ? p.aux : p.out;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-          const uint32_t e = (uint32_t)(grow + 8 * h) * N + gcol;
+          const uint32_t e = orow(grow + 8 * h) * N + gcol;
           rd[h] = ld_e<float4>(src, e >> 2);
           rb[h] = (EK == EK_RES_F32 && p.resbits) ? ld_word(p.resbits, e) : ~0u;
         }
@@ -788,7 +801,7 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's stores land before its reads
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        const uint32_t e = (uint32_t)(grow + 8 * h) * N + gcol;
+        const uint32_t e = orow(grow + 8 * h) * N + gcol;
         float4 v = *reinterpret_cast<const float4 *>(w + (rr + 8 * h) * LS + c4);
         if constexpr (EK == EK_ACC_F32) {
           v.x += rd[h].x; v.y += rd[h].y; v.z += rd[h].z; v.w += rd[h].w;
@@ -802,6 +815,10 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
         }
         v.x = epi_act(v.x, flags); v.y = epi_act(v.y, flags);
         v.z = epi_act(v.z, flags); v.w = epi_act(v.w, flags);
+        if constexpr (EK == EK_ACTGRAD) {
+          v.x = epi_act_grad(v.x, rd[h].x, flags); v.y = epi_act_grad(v.y, rd[h].y, flags);
+          v.z = epi_act_grad(v.z, rd[h].z, flags); v.w = epi_act_grad(v.w, rd[h].w, flags);
+        }
         st_e<float4>(p.out, e >> 2, v);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's staging
@@ -918,9 +935,12 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
     const int flags = p.flags;
     // the LDS-transposed kinds: stride 1, < 2^30 output elements (32-bit byte offsets)
     int ek = EK_GENERAL;
-    if (VEC > 0 && !S2 && (uint64_t)p.M * (uint64_t)p.N < (1ull << 30) && !(flags & kEpiActGrad)) {
+    // (S2 and activation gradients: the fp32 path only; S2 scatters into the whole image)
+    const uint64_t oelems = S2 ? (uint64_t)p.n * p.h * p.w * p.N : (uint64_t)p.M * p.N;
+    if (VEC > 0 && (!S2 || VEC == 2) && oelems < (1ull << 30) && (!(flags & kEpiActGrad) || VEC == 2)) {
       const int rf = flags & (ADAPTSEG_EPI_ACCUMULATE | ADAPTSEG_EPI_RESIDUAL);
-      if (rf == 0) ek = EK_PLAIN;
+      if (flags & kEpiActGrad) ek = rf == 0 ? EK_ACTGRAD : EK_GENERAL;
+      else if (rf == 0) ek = EK_PLAIN;
       else if (rf == ADAPTSEG_EPI_RESIDUAL) ek = p.resb ? EK_RES_BF16 : EK_RES_F32;
       else if (rf == ADAPTSEG_EPI_ACCUMULATE) ek = p.out ? EK_ACC_F32 : EK_ACC_BF16;
     }
@@ -936,15 +956,20 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
         else epi_store_bf16x8<EK_ACC_BF16, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
       }
     }
-    if constexpr (VEC == 2 && !S2) {
+    if constexpr (VEC == 2) {
       vec = full && p.out && !p.outb && (p.N & 3) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
-            (ek == EK_PLAIN || ek == EK_RES_F32 || ek == EK_ACC_F32) && !(reinterpret_cast<uintptr_t>(p.out) & 15) &&
-            (ek != EK_RES_F32 || !(reinterpret_cast<uintptr_t>(p.res) & 15));
+            (ek == EK_PLAIN || ek == EK_RES_F32 || ek == EK_ACC_F32 || ek == EK_ACTGRAD) &&
+            !(reinterpret_cast<uintptr_t>(p.out) & 15) &&
+            (ek != EK_RES_F32 || !(reinterpret_cast<uintptr_t>(p.res) & 15)) &&
+            (ek != EK_ACTGRAD || !(reinterpret_cast<uintptr_t>(p.aux) & 15));
       if (vec) {
-        if (ek == EK_PLAIN) epi_store_f32x4<EK_PLAIN, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
-        else if (ek == EK_RES_F32)
-          epi_store_f32x4<EK_RES_F32, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
-        else epi_store_f32x4<EK_ACC_F32, MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds);
+#define AS_F32X4(EK_) \
+  epi_store_f32x4<EK_, MODE, TM, TN, S2>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds, Hc, Wc, py, px)
+        if (ek == EK_PLAIN) AS_F32X4(EK_PLAIN);
+        else if (ek == EK_RES_F32) AS_F32X4(EK_RES_F32);
+        else if (ek == EK_ACC_F32) AS_F32X4(EK_ACC_F32);
+        else AS_F32X4(EK_ACTGRAD);
+#undef AS_F32X4
       }
     }
     if (!vec) epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);

@@ -4,8 +4,9 @@ Full tiles of the F32X3 and bf16 LDS-DMA kernels store through a per-wave LDS tr
 16-B rows (epi_store_f32x4 / epi_store_bf16x8); any tile whose output is not 16-B aligned takes
 the per-element path.  Same kernel, same accumulation, same epilogue arithmetic order — so an
 output placed at a 16-B-aligned address and the same output one element off it must be
-bitwise equal, for the plain store, the in-place residual (with its ReLU-mask bitmap) and the
-accumulate, under both conv maths.  Reference: the Bottleneck's data gradient with its
+bitwise equal, for the plain store, the in-place residual (with its ReLU-mask bitmap), the
+accumulate and the stride-2 LeakyReLU-gradient data gradient (parity-class scatter), under both
+conv maths.  Reference: the Bottleneck's data gradient with its
 residual, model/deeplab_multi.py:96-103.
 """
 import pytest
@@ -36,8 +37,8 @@ def terms(t):
     return torch.stack([hi, mid, (r1 - mid.float()).to(torch.bfloat16)], dim=-2)
 
 
-CASES = ["f32x3_fwd", "f32x3_dgrad_res_bits", "f32x3_dgrad_acc", "f32x3_x3r_dgrad", "bf16_dgrad_res",
-         "bf16_dgrad_acc"]
+CASES = ["f32x3_fwd", "f32x3_dgrad_res_bits", "f32x3_dgrad_acc", "f32x3_x3r_dgrad", "f32x3_s2_leaky_grad",
+         "bf16_dgrad_res", "bf16_dgrad_acc"]
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -51,6 +52,10 @@ def test_vector_and_per_element_epilogues_agree_bitwise(case):
         n, h, w = 2, 32, 64            # 4096 rows: whole 128- / 256-row tiles
         cin, cout, ks, dil = (256, 256, 3, 2) if "x3r" in case else (256, 512, 1, 1)
         geom = k.ConvGeom(cin, cout, ks, ks, 1, (dil * (ks // 2),), (dil,))
+        if "s2" in case:   # the discriminator's 4x4 / 2 conv: data gradient by parity class, LeakyReLU'
+            n, h, w, cin, cout, ks = 2, 64, 128, 128, 256, 4
+            geom = k.ConvGeom(cin, cout, ks, ks, 2, (1,), (1,))
+        oh, ow = geom.out_hw(h, w)
         wt = [(torch.randn(cout, ks, ks, cin, generator=g) / (cin * ks * ks) ** 0.5).to(DEV)]
         if case == "f32x3_fwd":
             x = torch.randn(n, h, w, cin, generator=g).to(DEV)
@@ -59,7 +64,7 @@ def test_vector_and_per_element_epilogues_agree_bitwise(case):
             k.conv_fwd(geom, x, n, h, w, wt, out=a)
             k.conv_fwd(geom, x, n, h, w, wt, out=b)
         else:
-            dy = torch.randn(n, h, w, cout, generator=g).to(DEV)
+            dy = torch.randn(n, oh, ow, cout, generator=g).to(DEV)
             dyb = dy.to(torch.bfloat16) if bf16 else (terms(dy) if "x3r" in case else None)
             base = torch.randn(n, h, w, cin, generator=g).to(DEV)
             if bf16:
@@ -80,6 +85,10 @@ def test_vector_and_per_element_epilogues_agree_bitwise(case):
                 else:
                     for o in (a, b):   # the in-place residual: dx = dgrad + g over g
                         k.conv_dgrad(geom, dy, n, h, w, wt, out=o, res=o, dyb=dyb, resbits=bits)
+            elif "leaky" in case:
+                aux = torch.randn(n, h, w, cin, generator=g).to(DEV)   # the activation output (its sign)
+                for o in (a, b):
+                    k.conv_dgrad(geom, dy, n, h, w, wt, out=o, aux=aux)
             else:
                 for o in (a, b):
                     k.conv_dgrad(geom, dy, n, h, w, wt, out=o, dyb=dyb)
