@@ -15,8 +15,9 @@ Conv math: the fp32 configs run F32X3 by default (fp32-accurate convs on the bf1
 exact three-term bf16 operand splits, six bf16 products per fp32 product; conv_x3.hpp),
 ``--conv-math f32`` the fp32-input MFMA kernels; c5 runs bf16 operands.
 
-roofline: the dominant implicit-GEMM conv kernel symbol (most algorithmic FLOPs per step)
-is bracketed by hipEvents inside the library during the timed steps; achieved = its
+roofline: the dominant implicit-GEMM conv kernel symbol (the most measured kernel time per
+step, from hipEvents around every conv launch of one untimed step) is bracketed by hipEvents
+inside the library during the timed steps; achieved = its
 algorithmic FLOPs / its summed launch time, against that kernel's MFMA ceiling: the fp32 MFMA
 peak (157.3 TFLOP/s) for the fp32-input kernels, the bf16 dense peak / 6 (419.4 TFLOP/s of
 fp32 products) for F32X3, the bf16 dense peak (2516.6) for bf16.
@@ -214,15 +215,17 @@ def selector_symbol(sel):
 
 def pmc_traffic(config, sel):
     """Per-launch HBM-side bytes of the dominant kernel from the committed PMC passes
-    (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command)."""
-    for rnd in ("r4", "r3", "r2", "r1"):   # newest committed pass first
-        path = os.path.join(REPO, "profiles", rnd, "pmc", f"traffic_{config}.json")
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        if d.get("kernel") == selector_symbol(sel) and d.get("traffic_bytes_per_launch"):
-            return float(d["traffic_bytes_per_launch"]), os.path.relpath(path, REPO)
+    (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command):
+    profiles/rN/pmc/traffic_<config>[_<kernel>].json, newest round first."""
+    import glob
+    for rnd in ("r5", "r4", "r3", "r2", "r1"):
+        for path in sorted(glob.glob(os.path.join(REPO, "profiles", rnd, "pmc", f"traffic_{config}*.json"))):
+            try:
+                d = json.load(open(path))
+            except (OSError, ValueError):
+                continue
+            if d.get("kernel") == selector_symbol(sel) and d.get("traffic_bytes_per_launch"):
+                return float(d["traffic_bytes_per_launch"]), os.path.relpath(path, REPO)
     return None, None
 
 
@@ -368,9 +371,9 @@ def main():
     inv_bytes = {}
     inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes)
     step_flops = sum(inv.values())
-    # the roofline kernel: the symbol with the most algorithmic FLOPs per step
+    # the roofline kernel: the conv symbol with the most measured kernel time per step (below);
+    # without the untimed timing step (--no-roofline) the one with the most algorithmic FLOPs
     dom = max(inv, key=inv.get)
-    peak, family = kernel_peak(dom)
     hbm = []
     if not args.no_roofline:
         # HBM-bound kernels (interp / loss / BN passes): hipEvent pairs around each of their
@@ -386,15 +389,17 @@ def main():
         K.timing_enable_mem(False)
         K.timing_enable(-1, enable=False)
         by_kernel = []
-        for sel in sorted(inv, key=inv.get, reverse=True)[:6]:
-            ms_, _fl, n_ = K.timing_read_id(sel)
-            if not n_:
-                continue
+        live = {sel: K.timing_read_id(sel) for sel in inv}
+        live = {sel: t for sel, t in live.items() if t[2]}
+        if live:
+            dom = max(live, key=lambda sel: live[sel][0])
+        for sel in sorted(live, key=lambda sel: live[sel][0], reverse=True)[:6]:
+            ms_, _fl, n_ = live[sel]
             pk, fam = kernel_peak(sel)
             a_ = inv[sel] / (ms_ / 1e3) / 1e12   # algorithmic FLOPs of one step / summed launch time
             by_kernel.append({"kernel": selector_symbol(sel), "selector": sel, "achieved": a_, "peak": pk,
                               "unit": "TFLOP/s", "frac": a_ / pk, "kernel_family": fam,
-                              "launches_per_step": n_, "avg_launch_ms": ms_ / n_,
+                              "kernel_ms_per_step": ms_, "launches_per_step": n_, "avg_launch_ms": ms_ / n_,
                               "algorithmic_tflop_per_step": inv[sel] / 1e12,
                               "flop_share_of_step": inv[sel] / step_flops})
         for kid, name in K.MEM_KERNELS.items():
@@ -406,6 +411,7 @@ def main():
                             "algorithmic_bytes_per_launch": by_ / n_, "avg_launch_ms": ms_ / n_,
                             "launches_per_step": n_})
         K.timing_enable(dom)
+    peak, family = kernel_peak(dom)
 
     if world > 1:
         dist.barrier()
@@ -473,11 +479,12 @@ def main():
                            "algorithmic_flop_per_launch": k_flops / k_launches,
                            "launched_flop_per_launch": launched_flops / k_launches,
                            "kernel": selector_symbol(dom), "selector": dom,
+                           "chosen_by": "most measured kernel time per step (by_kernel)",
                            "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,
                            "flop_share_of_step": inv[dom] / step_flops,
-                           # every large conv symbol (forward / data gradient / weight gradient
-                           # carry similar FLOPs), live over the untimed step before the timed one
+                           # the six conv symbols with the most kernel time, live over the
+                           # untimed step before the timed one
                            "by_kernel": by_kernel,
                            "by_kernel_source": "hipEvents around every conv launch of one untimed step"}
         # north_star: HBM GB/s of the interp / loss kernels (and the BN passes) vs the peak,

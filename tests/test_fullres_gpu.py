@@ -1,4 +1,5 @@
-"""Parity at BASELINE's full geometries (batch 1): the large-grid kernel paths end to end.
+"""Parity at BASELINE's full geometries (batch 1, and each config's own bench batch): the
+large-grid kernel paths end to end.
 
 Every other model-level test runs at 41x57-class sizes, where most convs split K and go
 through the slab reduce; at 1024x512 / 1280x720 the layer3/4 convs run unsplit with the
@@ -40,10 +41,10 @@ GEOMS = {
 }
 
 
-def _batch(src, tgt):
-    xs = torch.from_numpy(R.det_images((1, 3, src[1], src[0]), 11)).float()
-    lab = torch.from_numpy(R.det_labels((1, src[1], src[0]), 12))
-    xt = torch.from_numpy(R.det_images((1, 3, tgt[1], tgt[0]), 13)).float()
+def _batch(src, tgt, batch=1):
+    xs = torch.from_numpy(R.det_images((batch, 3, src[1], src[0]), 11)).float()
+    lab = torch.from_numpy(R.det_labels((batch, src[1], src[0]), 12))
+    xt = torch.from_numpy(R.det_images((batch, 3, tgt[1], tgt[0]), 13)).float()
     return xs, lab, xt
 
 
@@ -78,6 +79,22 @@ def test_fullres_step_vs_oracle(geom, bn_train):
     _step_vs_oracle(geom, bn_train, "Vanilla", 1e-3)
 
 
+# BASELINE's own per-GPU batch of each config (bench.py CONFIGS): the engine's batch-dependent
+# planning (row-tile statistics, split-K counts, bf16_only copy skipping, kernel selection by
+# grid size) runs end to end at exactly the shapes the bench lines are measured on
+BENCH_BATCH = {"c2": 4, "c3": 2}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("bn_train", [True, False], ids=["trainBN", "evalBN"])
+@pytest.mark.parametrize("geom", ["c2", "c3"])
+def test_fullres_bench_batch_step_vs_oracle(geom, bn_train):
+    """test_fullres_step_vs_oracle at the bench's batch: c2 single-level Vanilla at B=4
+    (train:385-461), c3 multi-level Vanilla at B=2 (train:578-679); the same bounds as batch 1
+    (losses within 1e-3, update cosine >= 0.97 train BN / 0.99 eval BN)."""
+    _step_vs_oracle(geom, bn_train, "Vanilla", 1e-3, batch=BENCH_BATCH[geom])
+
+
 @pytest.fixture
 def bf16_math():
     from adaptsegnet_amd import kernels as K
@@ -105,6 +122,16 @@ def test_fullres_c5_bf16_step_vs_oracle(bf16_math, bn_train):
                     act_bf16=True)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("bn_train", [True, False], ids=["trainBN", "evalBN"])
+def test_fullres_c5_bench_batch_step_vs_oracle(bf16_math, bn_train):
+    """test_fullres_c5_bf16_step_vs_oracle at BASELINE c5's batch/GPU 4 (the bench line's shape):
+    the same bounds (losses within 2e-2; eval BN every update cosine >= 0.99; train BN the losses,
+    heads and discriminators only, see there)."""
+    _step_vs_oracle("c3", bn_train, "LS", 2e-2, trunk=not bn_train, d_bound=0.85 if bn_train else None,
+                    act_bf16=True, batch=4)
+
+
 def test_fullres_c5_bf16_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monkeypatch):
     """engine.bf16_only at the c5 geometry: one train-BN multi-level LS step with and without the
     skipping of fp32 activations gives bitwise the same losses and parameters (a skipped tensor is
@@ -130,10 +157,12 @@ def test_fullres_c5_bf16_skipping_fp32_copies_is_bitwise_neutral(bf16_math, monk
             assert torch.equal(da[k], db[k]), k
 
 
-def test_fullres_c4_vgg_step_vs_oracle():
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("batch", [1, 8], ids=["B1", "B8"])
+def test_fullres_c4_vgg_step_vs_oracle(batch):
     """BASELINE config c4's program at its own geometry: DeeplabVGG (model/deeplab_vgg.py:24-54)
     single-level Vanilla step (train:385-461, the map upsampled by the caller's interp), source and
-    target 1024x512, batch 1, against the fp32 oracle (R.vgg_forward, the restatement: DeeplabVGG
+    target 1024x512, batch 1 and BASELINE's batch 8, against the fp32 oracle (R.vgg_forward, the restatement: DeeplabVGG
     is unimportable here, so the composition is pinned by the restatement and the per-op goldens,
     SURVEY.md §8c) from identical weights and inputs.  At this size the conv5 / fc6 / fc7 products
     run unsplit with the in-kernel epilogue.  Losses within 1e-3 relative; the generator's update
@@ -144,7 +173,7 @@ def test_fullres_c4_vgg_step_vs_oracle():
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     src = tgt = (1024, 512)
-    xs, lab, xt = _batch(src, tgt)
+    xs, lab, xt = _batch(src, tgt, batch)
     cfg = dict(level="single-level", gan="Vanilla", input_size=src, input_size_target=tgt, gen="vgg")
     st = R.det_state(R.vgg_specs(), 4244)
     P = R.to_torch(st, dtype=torch.float32, trainable=lambda k: True)
@@ -160,7 +189,7 @@ def test_fullres_c4_vgg_step_vs_oracle():
     tr = AdaptSegTrainer(m, None, d2, StepConfig(level="single-level", input_size=src, input_size_target=tgt))
     got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()
     for k, v in ref.items():
-        print(f"c4 {k}: hip={got[k]:.6f} oracle={v:.6f}")
+        print(f"c4 B={batch} {k}: hip={got[k]:.6f} oracle={v:.6f}")
         assert abs(got[k] - v) <= 1e-3 * abs(v) + 1e-6, (k, got[k], v)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     used = [k for k in P if not k.startswith(("classifier.conv2d_list.2", "classifier.conv2d_list.3"))]
@@ -210,12 +239,13 @@ def test_c1_forward_crossentropy2d_vs_oracle():
         assert abs(loss - l_ref) <= 1e-3 * abs(l_ref)
 
 
-def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16=False):
+def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16=False, batch=1):
     """act_bf16: the oracle stores the Bottleneck activations in bf16 as the engine's bf16
-    program does (R.bf16_activation_storage)."""
+    program does (R.bf16_activation_storage).  batch: images per domain (the bench's own batch
+    sizes: test_fullres_bench_batch_step_vs_oracle)."""
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     level, src, tgt = GEOMS[geom]
-    xs, lab, xt = _batch(src, tgt)
+    xs, lab, xt = _batch(src, tgt, batch)
     cfg = dict(level=level, gan=gan, input_size=src, input_size_target=tgt)
     # oracle, fp32 on the host cores
     G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
@@ -231,7 +261,7 @@ def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16
     tr, m, d1, d2 = _hip_trainer(level, src, tgt, bn_train, gan=gan)
     got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()
     for k, v in ref.items():
-        print(f"{geom} {gan} bn_train={bn_train} {k}: hip={got[k]:.6f} oracle={v:.6f}")
+        print(f"{geom} B={batch} {gan} bn_train={bn_train} {k}: hip={got[k]:.6f} oracle={v:.6f}")
         assert abs(got[k] - v) <= tol * abs(v) + 1e-6, (k, got[k], v)
     # parameter updates (new - initial), per group
     g0 = R.det_state(R.g_specs(), 1338)
@@ -249,7 +279,7 @@ def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16
         u_ref = torch.cat([(G[k].detach().double() - torch.from_numpy(g0[k])).flatten() for k in keys])
         u_hip = torch.cat([(sd[k].double() - torch.from_numpy(g0[k])).flatten() for k in keys])
         c = _cos(u_hip, u_ref)
-        print(f"{geom} bn_train={bn_train} G/{gname} update cosine {c:.6f}")
+        print(f"{geom} B={batch} bn_train={bn_train} G/{gname} update cosine {c:.6f}")
         assert c >= bound, (gname, c)
     for dname, dm, DD, seed in (("D1", d1, D1, 2001), ("D2", d2, D2, 2002)):
         if dname == "D1" and level == "single-level":
@@ -259,7 +289,7 @@ def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16
         u_ref = torch.cat([(DD[k].detach().double() - torch.from_numpy(d0[k])).flatten() for k in DD])
         u_hip = torch.cat([(dsd[k].double().cpu() - torch.from_numpy(d0[k])).flatten() for k in DD])
         c = _cos(u_hip, u_ref)
-        print(f"{geom} bn_train={bn_train} {dname} update cosine {c:.6f}")
+        print(f"{geom} B={batch} bn_train={bn_train} {dname} update cosine {c:.6f}")
         assert c >= (d_bound or bound), (dname, c)
 
 

@@ -80,6 +80,36 @@ def shapes(batch, W=1024, H=512):
     return out
 
 
+def vgg_shapes(batch, W=1024, H=512):
+    """config c4: DeeplabVGG (model/deeplab_vgg.py) per-shape products of one step (2 domains:
+    2 forwards, 2 data gradients, 2 weight gradients; conv1_1 has no data gradient), then the
+    discriminator's as in ``shapes``."""
+    from adaptsegnet_amd.model import deeplab_vgg as V
+    out = collections.OrderedDict()
+    h, w = H, W
+    specs = list(V._VGG_FEATURES) + [("C", 512, 1024, 4), ("R",), ("C", 1024, 1024, 4), ("R",)]
+    i = 0
+    for spec in specs:
+        if spec[0] == "C":
+            _, ci, co, d = spec
+            g = K.ConvGeom(ci, co, 3, 3, 1, (d,), (d,))
+            st = (3 * h * w, h * w, w, 1) if ci == 3 else None
+            ops = (0, 2) if ci == 3 else (0, 1, 2)
+            key = (g, batch, h, w, ops, st)
+            if key in out:
+                out[key][0] += 2
+            else:
+                out[key] = [2, f"vgg.c{i}"]
+            i += 1
+        elif spec[0] == "P":
+            h, w = h // 2, w // 2
+    out[(K.ConvGeom(1024, 19, 3, 3, 1, (6, 12), (6, 12)), batch, h, w, (0, 1, 2), None)] = [2, "vgg.aspp"]
+    for k, v in shapes(batch, W, H).items():
+        if v[1].startswith("D."):
+            out[k] = v
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4)
@@ -88,6 +118,8 @@ def main():
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--math", choices=("f32", "f32x3", "f32x3_presplit", "bf16"), default="f32")
+    ap.add_argument("--model", choices=("multi", "vgg"), default="multi",
+                    help="multi: DeeplabMulti (c2 shapes); vgg: DeeplabVGG (config c4, use --batch 8)")
     args = ap.parse_args()
     K.set_conv_math({"f32": K.MATH_F32, "f32x3": K.MATH_F32X3, "f32x3_presplit": K.MATH_F32X3_PRESPLIT,
                      "bf16": K.MATH_BF16}[args.math])
@@ -97,7 +129,8 @@ def main():
     per_op = collections.defaultdict(lambda: [0.0, 0.0])
     print(f"{'conv':<10} {'op':>3} {'n':>2} {'hxw':>9} {'cin':>5} {'cout':>5} {'k':>2} {'sel':>4} {'spl':>3} "
           f"{'cnt':>4} {'avg us':>9} {'TF/s':>7} {'kern us':>9} {'kTF/s':>7}")
-    for (g, n, h, w, ops, st), (count, name) in shapes(args.batch, args.width, args.height).items():
+    table = (vgg_shapes if args.model == "vgg" else shapes)(args.batch, args.width, args.height)
+    for (g, n, h, w, ops, st), (count, name) in table.items():
         if args.filter and args.filter not in name:
             continue
         oh, ow = g.out_hw(h, w)
@@ -108,7 +141,7 @@ def main():
                 if st[1] == 1 else torch.randn(n, g.cin, h, w, device=dev)
         ws = [torch.randn(g.cout, g.kh, g.kw, g.cin, device=dev) * 0.01 for _ in range(g.nseg)]
         # only the ASPP classifiers and the discriminator convs carry a bias
-        has_bias = name.startswith(("aspp", "D."))
+        has_bias = name.startswith(("aspp", "D.", "vgg."))
         bs = [torch.randn(g.cout, device=dev) for _ in range(g.nseg)] if has_bias else None
         dy = torch.randn(n, oh, ow, g.cout, device=dev)
         dws = [torch.zeros_like(t) for t in ws]
