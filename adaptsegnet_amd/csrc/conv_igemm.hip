@@ -1,4 +1,6 @@
-// Implicit-GEMM convolution for gfx950 (MI355X) on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// Implicit-GEMM convolution for gfx950 (MI355X): the fp32-input MFMA kernels
+// (v_mfma_f32_32x32x2_f32, conv math F32) and the host side of every conv family (F32X3 on the
+// bf16 MFMA, conv_x3.hpp / conv_x3r.hpp, the library default; bf16, conv_bf16*.hpp).
 //
 // One kernel template serves the three convolution products of the AdaptSegNet step
 // (reference: every nn.Conv2d of model/deeplab_multi.py and model/discriminator.py):

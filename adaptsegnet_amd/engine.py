@@ -99,8 +99,31 @@ def lowp_storage() -> bool:
     return K.get_conv_math() in (K.MATH_BF16, K.MATH_BF16_WIDE)
 
 
+def _switch(name, default, allowed):
+    """An A/B environment switch of the production numeric path, checked at import: a value
+    outside ``allowed`` (e.g. a mode whose code was removed) raises instead of silently running
+    another path.  switches() reports the active values (bench.py records them)."""
+    raw = _os.environ.get(name, str(default))
+    try:
+        v = int(raw)
+    except ValueError:
+        v = None
+    if v not in allowed:
+        raise ValueError(f"{name}={raw!r}: supported values are {sorted(allowed)}")
+    _SWITCHES[name] = v
+    return v
+
+
+_SWITCHES: dict = {}
+
+
+def switches() -> dict:
+    """The active A/B switch values (environment, read at import)."""
+    return dict(_SWITCHES)
+
+
 # (A/B switch) bf16 gradient storage under the BF16 maths
-BF16_GRADS = int(_os.environ.get("ADAPTSEG_BF16_GRADS", "1"))
+BF16_GRADS = _switch("ADAPTSEG_BF16_GRADS", 1, (0, 1))
 
 
 def lowp_grads() -> bool:
@@ -190,7 +213,7 @@ class BlockRec:
 
 # (A/B switch) the Bottleneck's output ReLU mask as a bitmap (1 bit per element) instead of the
 # stored block output: BN3's backward and the residual gradient read it
-MASK_BITS = int(_os.environ.get("ADAPTSEG_MASK_BITS", "1"))
+MASK_BITS = _switch("ADAPTSEG_MASK_BITS", 1, (0, 1))
 
 
 def _conv_bn(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
@@ -216,7 +239,7 @@ def x3_forward_terms(g) -> bool:
 # (A/B switch) 0: conv2 backward on fp32 operands; 1: its weight gradient on term images (y1's
 # from the forward, dY's from BN2's backward); 2 (default): its data gradient too.  (Mode 3,
 # conv3's backward on term images too, measured -0.6..-0.9 %: experiments/r4_conv3_terms.patch.)
-X3_BWD_TERMS = int(_os.environ.get("ADAPTSEG_X3_BWD_TERMS", "2"))
+X3_BWD_TERMS = _switch("ADAPTSEG_X3_BWD_TERMS", 2, (0, 1, 2))
 
 
 def block_input_fp32(blk, n, h, w) -> bool:

@@ -74,8 +74,9 @@ class ConvGeom:
 
 def set_conv_math(math: int) -> None:
     """Process-wide conv arithmetic: MATH_F32X3 (default: fp32 through exact three-term bf16
-    splits on the bf16 MFMA, fp32-accurate, conv_x3.hpp / conv_x3g.hpp), MATH_F32X3_PRESPLIT (the
-    same arithmetic, every operand split while staged: conv_x3.hpp only), MATH_F32 (the fp32-input MFMA
+    splits on the bf16 MFMA, fp32-accurate, conv_x3.hpp / conv_x3r.hpp), MATH_F32X3_PRESPLIT (the
+    same arithmetic, every product the term-image kernel covers on conv_x3r.hpp, fed bf16 term
+    images the BN passes write), MATH_F32 (the fp32-input MFMA
     kernels) or MATH_BF16 (operands rounded to bf16, fp32 accumulate: BASELINE config c5).  Workspace sizes depend on it,
     so the descriptor cache is keyed on it."""
     _ops.set_math(math)
@@ -112,9 +113,30 @@ class _PackCache:
         # built]}; a weakref.finalize on the weight drops its entry (tensors compare elementwise,
         # so they cannot key a WeakKeyDictionary)
         self.entries = {}
+        # id(first weight) -> its weakref.finalize: ONE per weight, kept across
+        # clear_weight_packs() and reused while alive (a long-lived Parameter gains no more)
+        self.finalizers = {}
         # (geometry, op, math, NHWC input?) -> pack bytes (0: the kernel reads none)
         self.sizes = {}
         self.builds = 0      # packs built (tests)
+
+    def _drop(self, wid):
+        self.entries.pop(wid, None)
+        self.finalizers.pop(wid, None)
+
+    def track(self, weight):
+        """The per-weight pack dict of ``weight`` (created on first use).  Entries are keyed by
+        id(weight); the inner keys add every segment's data_ptr, so a product over several
+        weights (the ASPP's four) is found through its first weight and rebuilt if any segment
+        moved."""
+        wid = id(weight)
+        per = self.entries.get(wid)
+        if per is None:
+            per = self.entries[wid] = {}
+            f = self.finalizers.get(wid)
+            if f is None or not f.alive:
+                self.finalizers[wid] = weakref.finalize(weight, self._drop, wid)
+        return per
 
 
 _PACKS = _PackCache()
@@ -169,11 +191,7 @@ def _wpack(g, n, h, w, strides, weights, op):
         size = _PACKS.sizes[skey] = b.value
     if size == 0:
         return None
-    wid = id(weights[0])
-    per = _PACKS.entries.get(wid)
-    if per is None:
-        per = _PACKS.entries[wid] = {}
-        weakref.finalize(weights[0], _PACKS.entries.pop, wid, None)
+    per = _PACKS.track(weights[0])
     key = (tuple(t.data_ptr() for t in weights), g, op, math)
     e = per.get(key)
     if e is None or e[0].numel() < size:
@@ -272,6 +290,8 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
             out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.bfloat16)
         if res is not None:
             flags |= EPI_RESIDUAL
+        if aux is not None and not flags & EPI_RELU_GRAD:   # the same gating rule as the fp32 branch
+            flags |= EPI_LEAKY_GRAD
         wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
         _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, None, out, (n, g.cin, h, w), _wshape(g),
                             g.stride, g.pads, g.dils, flags)

@@ -331,6 +331,7 @@ def main():
         init_distributed(args.backend, local)
     dev = torch.device("cuda", local)
 
+    from adaptsegnet_amd import engine
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd.model import DeeplabMulti, DeeplabVGG, FCDiscriminator
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
@@ -449,6 +450,7 @@ def main():
                    "step_conv_tflop": step_flops / 1e12,
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
                    "conv_math": conv_math,
+                   "switches": engine.switches(),
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across

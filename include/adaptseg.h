@@ -41,7 +41,9 @@ const char *adaptseg_last_error(void);
 const char *adaptseg_version(void);
 
 /* ------------------------------------------------------------------------------------ */
-/* Convolution (implicit GEMM on fp32 MFMA v_mfma_f32_32x32x2_f32).                      */
+/* Convolution (implicit GEMM on the MFMA: by default F32X3 = fp32-accurate products on   */
+/* v_mfma_f32_32x32x16_bf16 through exact 3-term bf16 splits, conv_x3.hpp / conv_x3r.hpp; */
+/* v_mfma_f32_32x32x2_f32 under ADAPTSEG_MATH_F32; bf16 operands under ADAPTSEG_MATH_BF16). */
 /* Replaces nn.Conv2d in model/deeplab_multi.py:64,70-71,75,128,158-159 (Bottleneck,    */
 /* stem, downsample), Classifier_Module model/deeplab_multi.py:106-121 (ASPP: nseg=4    */
 /* branches summed into one GEMM with concatenated K) and model/discriminator.py:10-14.  */
@@ -70,7 +72,8 @@ enum adaptseg_conv_flags {
 };
 
 /* Conv arithmetic, process-wide (set before sizing workspaces; every conv entry point and
-   *_workspace_size() reads it).  F32: fp32 MFMA, exact fp32 products (default).  BF16: the
+   *_workspace_size() reads it).  The library default is F32X3 (conv_igemm.hip).  F32: fp32
+   MFMA, exact fp32 products.  BF16: the
    operands of each product are rounded to bf16 (RNE) as they are staged into LDS and
    multiplied on v_mfma_f32_32x32x16_bf16 with fp32 accumulation — torch.autocast(bfloat16)
    conv semantics; activations, gradients and epilogues stay fp32 (BASELINE config c5).
@@ -82,9 +85,10 @@ enum adaptseg_conv_math {
   ADAPTSEG_MATH_BF16_WIDE = 2, /* BF16 with 128x256 tiles for fwd / data-grad products with N >= 256 */
   ADAPTSEG_MATH_F32X3 = 3,     /* fp32 on the bf16 MFMA: exact 3-term bf16 splits of both operands,
                                   the 6 products above 2^-23 relative (fp32-accurate; conv_x3.hpp) */
-  ADAPTSEG_MATH_F32X3_PRESPLIT = 4 /* F32X3 arithmetic (bitwise the same results) with the products
-                                  whose operands come in 16-B chunks on the LDS-DMA kernel of
-                                  conv_x3g.hpp, fed PRE-SPLIT bf16 term images (made per call) */
+  ADAPTSEG_MATH_F32X3_PRESPLIT = 4 /* F32X3 arithmetic (bitwise the same results where neither
+                                  splits K) with every product the 256x128x32 term-image kernel
+                                  covers on it (conv_x3r.hpp, LDS-DMA of PRE-SPLIT bf16 term
+                                  images written by the producing BN passes) */
 };
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);

@@ -215,7 +215,7 @@ class _StoreBF16(torch.autograd.Function):
         return (g.to(torch.bfloat16).to(g.dtype) if ctx.round_grad else g), None
 
 
-_ACT_BF16 = [False, False]   # activations stored bf16, gradients stored bf16
+_ACT_BF16 = [False, False, True]   # activations stored bf16, gradients stored bf16, engine's fp32 exceptions
 
 
 class bf16_activation_storage:
@@ -226,14 +226,19 @@ class bf16_activation_storage:
     layer4's last block (it comes from the ASPP head's backward) and, when both heads are trained
     (multi-level), the output of layer3's last block (layer4.0's input gradient, which layer5's
     backward accumulates into).  The stem, the classifiers and the discriminators are unaffected,
-    as in the engine."""
+    as in the engine.
 
-    def __init__(self, grads=True):
+    The exceptions make this oracle model the ENGINE's storage, not torch.autocast's (which would
+    round those two gradients as well): ``exceptions=False`` rounds every stored gradient, the
+    pure-autocast restatement, and tests/test_oracle_golden.py bounds the gap between the two."""
+
+    def __init__(self, grads=True, exceptions=True):
         self.grads = grads
+        self.exceptions = exceptions
 
     def __enter__(self):
         self._prev = list(_ACT_BF16)
-        _ACT_BF16[0], _ACT_BF16[1] = True, self.grads
+        _ACT_BF16[0], _ACT_BF16[1], _ACT_BF16[2] = True, self.grads, self.exceptions
         return self
 
     def __exit__(self, *exc):
@@ -284,7 +289,7 @@ def g_forward(P, x, input_size, train=True, layout=RESNET101, grad_heads=2):
             x1 = _aspp(y, P, "layer5")
         for b in range(nblk):
             last = b == nblk - 1
-            ogb = not (last and (li == 4 or (li == 3 and grad_heads == 2)))
+            ogb = not (_ACT_BF16[2] and last and (li == 4 or (li == 3 and grad_heads == 2)))
             y = _bottleneck(y, P, f"layer{li}.{b}.", stride if b == 0 else 1, dil, b == 0, train, ogb)
     x2 = _aspp(y, P, "layer6")
     size = (int(input_size[1]), int(input_size[0]))

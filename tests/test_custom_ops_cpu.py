@@ -48,3 +48,31 @@ def test_fake_tensor_tracing_of_the_tensor_api():
         u = K.upsample_fwd(torch.empty(2, 8, 10, 19, device="cuda"), 64, 80)
         assert u.shape == (2, 64, 80, 19)
         assert K.ce_fwd(u, torch.empty(2, 64, 80, dtype=torch.int64, device="cuda")).shape == (2,)
+
+
+def test_pack_cache_keeps_one_finalizer_per_weight():
+    """kernels._PackCache: clear_weight_packs() then reusing a weight does not register a second
+    weakref finalizer on it, and dropping the weight removes both its pack dict and
+    its finalizer."""
+    import gc
+    from adaptsegnet_amd import kernels as K
+    t = torch.zeros(8)
+    wid = id(t)
+    K._PACKS.track(t)["k"] = 1
+    K.clear_weight_packs()
+    assert wid not in K._PACKS.entries
+    for _ in range(3):
+        K._PACKS.track(t)
+        K.clear_weight_packs()
+    K._PACKS.track(t)
+    live = [f for f in weakref_finalizers_of(t)]
+    assert len(live) == 1, live
+    assert K._PACKS.finalizers[wid].alive
+    del t
+    gc.collect()
+    assert wid not in K._PACKS.entries and wid not in K._PACKS.finalizers
+
+
+def weakref_finalizers_of(obj):
+    import weakref
+    return [f for f in list(weakref.finalize._registry) if f.peek() and f.peek()[0] is obj]

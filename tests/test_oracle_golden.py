@@ -185,3 +185,39 @@ def test_bf16_activation_storage_rounds_block_outputs_and_their_gradients():
         assert torch.equal(gi, g)
         (gi,) = torch.autograd.grad(R._st(out), out, g)
         assert torch.equal(gi, g.to(torch.bfloat16).double())
+
+
+def test_bf16_oracle_engine_storage_vs_pure_autocast():
+    """The c5 oracle rounds the same gradients the engine stores in bf16 (engine.lowp_grads), so
+    its two fp32 exceptions — the gradients w.r.t. layer4's last block output (from the ASPP
+    backward) and, multi-level, layer3's last (layer5's backward accumulates into it) — are
+    mirrored, not tested.  This bounds what they change against the pure-autocast
+    restatement (every stored gradient rounded): one multi-level LS step, eval-mode BN, fp64
+    elsewhere.  Stated tolerance: losses within 2e-3 relative, per-group update cosine >= 0.999
+    (the same order as one bf16 rounding of two gradients, far inside the c5 GPU tests'
+    2e-2 / 0.99)."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    xs = torch.from_numpy(R.det_images((1, 3, 41, 57), 11))
+    lab = torch.from_numpy(R.det_labels((1, 41, 57), 12))
+    xt = torch.from_numpy(R.det_images((1, 3, 33, 49), 13))
+    cfg = dict(level="multi-level", gan="LS", input_size=(57, 41), input_size_target=(49, 33))
+    runs = []
+    for exc in (True, False):
+        G = R.to_torch(R.det_state(R.g_specs(), 1338), trainable=R.g_trainable)
+        D1 = R.to_torch(R.det_state(R.d_specs(), 2001), trainable=lambda k: True)
+        D2 = R.to_torch(R.det_state(R.d_specs(), 2002), trainable=lambda k: True)
+        opts = R.make_optimizers(G, D1, D2, R.DEFAULT_CFG | cfg)
+        with R.bf16_activation_storage(exceptions=exc):
+            vals = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=False)
+        runs.append((vals, G))
+    (va, Ga), (vb, Gb) = runs
+    g0 = R.det_state(R.g_specs(), 1338)
+    for k in va:
+        assert abs(va[k] - vb[k]) <= 2e-3 * abs(va[k]) + 1e-9, (k, va[k], vb[k])
+    for grp in ("layer5", "layer6", ""):
+        keys = [k for k, t in Ga.items() if t.dtype.is_floating_point and t.requires_grad
+                and (k.startswith(grp) if grp else not k.startswith(("layer5", "layer6")))]
+        ua = torch.cat([(Ga[k].detach() - torch.from_numpy(g0[k])).flatten() for k in keys])
+        ub = torch.cat([(Gb[k].detach() - torch.from_numpy(g0[k])).flatten() for k in keys])
+        c = float(torch.nn.functional.cosine_similarity(ua, ub, dim=0))
+        assert c >= 0.999, (grp or "trunk", c)

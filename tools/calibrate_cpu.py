@@ -9,8 +9,9 @@ CrossEntropy2d — with /root/reference/model/deeplab_multi.py + utils/loss.py a
 oracle/reference_torch.py, and (2) one single-level adversarial step at batch 1, 1024x512 (the
 c2 shape bench.py's ``cpu_baseline`` times) with the reference modules composed as
 train_gta2cityscapes_multi.py:379-464 and with ``oracle_step``.  SURVEY §8(d) asks the
-restatement to match the reference within +-10 %.  Writes profiles/r4/cpu_calibration.json
-(round 1's run: profiles/r1/).
+restatement to match the reference within +-10 %.  Writes profiles/<round>/cpu_calibration.json
+(each round's run in its own directory: profiles/r1/, r4/, r5/ ...), with every rep's time and
+the spread of the interleaved pairs' ratios, not only the best-of ratio.
 """
 from __future__ import annotations
 
@@ -32,7 +33,7 @@ from oracle import reference_torch as R  # noqa: E402
 
 
 def best_of_pair(fa, fb, reps):
-    """min time of fa and of fb over ``reps`` interleaved repetitions (after one warm-up each):
+    """every time of fa and of fb over ``reps`` interleaved repetitions (after one warm-up each):
     alternating keeps allocator / oneDNN-cache / thermal drift from favouring either side (run
     back to back, the same pair measured anywhere from -12 % to +16 % apart)."""
     fa()
@@ -43,13 +44,25 @@ def best_of_pair(fa, fb, reps):
             t0 = time.perf_counter()
             f()
             ts.append(time.perf_counter() - t0)
-    return min(ta), min(tb)
+    return ta, tb
+
+
+def record(out, name, ta, tb):
+    """best-of times, their ratio, and the spread: every rep's time and the ratio of each
+    interleaved pair (port / reference), min / median / max."""
+    out[f"{name}_reference_s"], out[f"{name}_port_s"] = min(ta), min(tb)
+    out[f"{name}_port_over_reference"] = min(tb) / min(ta)
+    out[f"{name}_reference_reps_s"], out[f"{name}_port_reps_s"] = ta, tb
+    pairs = sorted(b / a for a, b in zip(ta, tb))
+    out[f"{name}_pair_ratios"] = pairs
+    out[f"{name}_pair_ratio_min_median_max"] = [pairs[0], float(np.median(pairs)), pairs[-1]]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--round", default="r5", help="writes profiles/<round>/cpu_calibration.json")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     from gen_golden import load_ref, state_to_torch
@@ -77,7 +90,7 @@ def main():
             _, p2 = R.g_forward(G, x1, (321, 321), train=True)
             R.cross_entropy2d(p2, l1)
 
-    out["c1_reference_s"], out["c1_port_s"] = best_of_pair(ref_c1, port_c1, args.reps)
+    record(out, "c1", *best_of_pair(ref_c1, port_c1, args.reps))
 
     # ---- c2 shape, batch 1: one single-level step ------------------------------------------
     xs = torch.from_numpy(R.det_images((1, 3, 512, 1024), 1)).float()
@@ -121,11 +134,10 @@ def main():
     def port_step():
         R.oracle_step(Gp, None, D2p, opts, cfg, 0, [(xs, lab, xt)])
 
-    out["c2b1_step_reference_s"], out["c2b1_step_port_s"] = best_of_pair(ref_step, port_step, args.reps)
-    out["c1_port_over_reference"] = out["c1_port_s"] / out["c1_reference_s"]
-    out["c2b1_port_over_reference"] = out["c2b1_step_port_s"] / out["c2b1_step_reference_s"]
+    record(out, "c2b1_step", *best_of_pair(ref_step, port_step, args.reps))
     out["reps"] = args.reps
-    path = os.path.join(REPO, "profiles", "r4", "cpu_calibration.json")
+    path = os.path.join(REPO, "profiles", args.round, "cpu_calibration.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))
 
