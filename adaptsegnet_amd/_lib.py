@@ -94,6 +94,8 @@ _SIGS = {
     "adaptseg_bn_bwd": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P],
     "adaptseg_maxpool2d_fwd": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "adaptseg_maxpool2d_bwd": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
+    "adaptseg_maxpool2d_fwd_x": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "adaptseg_maxpool2d_bwd_x": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "adaptseg_upsample_workspace_size": [_I, _I, _I, _I, _I, _I, ctypes.POINTER(_SZ)],
     "adaptseg_upsample_bilinear_fwd": [_I, _I, _I, _I, _I, _I, _P, _P, _P],
     "adaptseg_upsample_bilinear_bwd": [_I, _I, _I, _I, _I, _I, _P, _P, _I, _P, _SZ, _P],

@@ -226,6 +226,41 @@ static void bias_grad_split(int rows, int cout, int *per, int *splits) {
   *splits = (int)ceil_div(rows, *per);
 }
 
+// Four channels per lane (Cout % 4 == 0, 1024 % Cout == 0, 16-B aligned dY): 256 / (Cout / 4)
+// row groups per block, each lane summing its column quad over every R-th row of the block's
+// range in fp32, then the R group partials in fixed order through LDS — float4 loads instead of
+// the kernel above's 4-B ones (DeeplabVGG's bias gradients: 6.8 ms per c4 step on it).
+__global__ void __launch_bounds__(256) bias_grad_partial4_kernel(const float4 *__restrict__ dy, int rows, int c4,
+                                                                 int rows_per_split, float4 *partial) {
+  __shared__ float4 red[256];
+  const int R = 256 / c4;                 // row groups
+  const int t = threadIdx.x, cq = t % c4, g = t / c4;
+  const int r0 = blockIdx.x * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < R) {
+#pragma unroll 4
+    for (int r = r0 + g; r < r1; r += R) {
+      const float4 v = dy[(size_t)r * c4 + cq];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[t] = a;
+  __syncthreads();
+  if (t < c4) {
+    float4 sum = red[t];
+    for (int q = 1; q < R; ++q) {
+      const float4 v = red[t + q * c4];
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    partial[(size_t)blockIdx.x * c4 + t] = sum;
+  }
+}
+
+static bool bias_grad_vec(const float *dy, int cout) {
+  return cout % 4 == 0 && 1024 % cout == 0 && !(reinterpret_cast<uintptr_t>(dy) & 15);
+}
+
 struct BiasOut {
   float *db[4];
 };
@@ -434,11 +469,13 @@ void set_splits(Plan &pl) {
   int splits = 1;
   if (pl.mode == MODE_WGRAD && pl.x3r) {
     // one 8-wave block per CU: the grid takes ceil(tiles * s / 256) rounds of 1/s of the K range,
-    // so pick the split count s (<= 16, >= 32 K steps each) with the fewest such units — e.g.
+    // so pick the split count s (<= 256, >= 32 K steps each) with the fewest such units — e.g.
     // layer4.conv2 (144 tiles of 128 rows): s = 1 leaves 112 CUs idle for the whole launch
-    // (MFMA busy 0.315 in isolation), s = 7 runs 4 rounds of 1/7 (0.57 of the s = 1 time)
+    // (MFMA busy 0.315 in isolation), s = 7 runs 4 rounds of 1/7 (0.57 of the s = 1 time).
+    // (Round 4 capped s at 16: the 1x1 weight gradients, 1-8 tiles over K = 32-131k pixels, then
+    // ran 16-128 blocks on 256 CUs — layer1 at 4-33 TF/s, layer3's 1x1 at 107-112.)
     double best = 1e30;
-    for (int s = 1; s <= 16 && (s == 1 || nkt / s >= 32); ++s) {
+    for (int s = 1; s <= 256 && (s == 1 || nkt / s >= 32); ++s) {
       const double t = (double)ceil_div((int64_t)pl.tiles * s, 256) / s;
       if (t < best * 0.97) {
         best = t;
@@ -731,13 +768,35 @@ __global__ void x3_out_copy_kernel(const float *__restrict__ y, __bf16 *__restri
   }
 }
 
+// ... four channels per thread (C % 4 == 0, 16-B aligned y, 8-B aligned terms, < 2^31 float4):
+// one float4 load, three 8-B stores (the kernel above: 2-B stores and a 64-bit division per
+// element)
+__global__ void __launch_bounds__(256) x3_out_copy4_kernel(const float4 *__restrict__ y, uint2 *__restrict__ yb,
+                                                           uint32_t n4, int C4, FastDiv fd_c4) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = fdiv(i, fd_c4);
+    const uint32_t cq = i - pix * C4;
+    uint2 h, m, l;
+    split3(y[i], h, m, l);
+    uint2 *o = yb + pix * 3 * C4 + cq;
+    o[0] = h;
+    o[C4] = m;
+    o[2 * C4] = l;
+  }
+}
+
 // The operand copy of a finished output [n / C][C] (the paths whose kernels do not write it): a
 // bf16 RNE image, or the three term images under the F32X3 maths
 static int out_copy(const float *y, uint16_t *yb, int64_t n, int C, hipStream_t s) {
   if (!yb || n == 0) return ADAPTSEG_OK;
   AS_CHECK_ARG(y, "conv: an operand copy needs the fp32 output on this path");
   const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n, 256), 8192);
-  if (copies_are_terms())
+  if (copies_are_terms() && C % 4 == 0 && n / 4 < (1ll << 31) / 3 && aligned16(y) &&
+      !(reinterpret_cast<uintptr_t>(yb) & 7))
+    x3_out_copy4_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n / 4, 256), 16384), 256, 0, s>>>(
+        reinterpret_cast<const float4 *>(y), reinterpret_cast<uint2 *>(yb), (uint32_t)(n / 4), C / 4,
+        make_fastdiv(C / 4));
+  else if (copies_are_terms())
     x3_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n, C);
   else
     bf16_out_copy_kernel<<<blocks, 256, 0, s>>>(y, reinterpret_cast<__bf16 *>(yb), n);
@@ -1168,7 +1227,11 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
         return ADAPTSEG_ERR_WORKSPACE;
       }
       float *partial = reinterpret_cast<float *>(ws);
-      bias_grad_partial_kernel<<<splits, 256, 0, s>>>(dy, rows, d->k, per, partial);
+      if (bias_grad_vec(dy, d->k))
+        bias_grad_partial4_kernel<<<splits, 256, 0, s>>>(reinterpret_cast<const float4 *>(dy), rows, d->k / 4, per,
+                                                         reinterpret_cast<float4 *>(partial));
+      else
+        bias_grad_partial_kernel<<<splits, 256, 0, s>>>(dy, rows, d->k, per, partial);
       AS_CHECK_LAUNCH("bias_grad_partial");
       bias_grad_final_kernel<<<(unsigned)ceil_div(d->k, 4), 256, 0, s>>>(
           partial, splits, d->k, o, d->nseg, (flags & ADAPTSEG_EPI_ACCUMULATE) ? 1 : 0);

@@ -97,6 +97,110 @@ __global__ void maxpool_bwd_kernel(int n, int C, int H, int W, int OH, int OW, i
   }
 }
 
+// Four channels per thread (C % 4 == 0, 16-B aligned tensors, < 2^31 float4 per tensor): the
+// same scan order, tie rule and NaN rule as the kernels above, one float4 load per window tap and
+// one float4 + uchar4 store (the scalar kernels issue a 4-B access and a 64-bit index division per
+// element: DeeplabVGG's 2x2 pools took 1.1 ms per backward launch at c4, 4x their HBM time).
+__global__ void __launch_bounds__(256) maxpool_fwd4_kernel(int n, int C4, int H, int W, int OH, int OW, int k, int s,
+                                                           int p, FastDiv fd_c4, FastDiv fd_ow, FastDiv fd_oh,
+                                                           const float4 *__restrict__ x, float4 *__restrict__ y,
+                                                           uchar4 *__restrict__ am, uint2 *__restrict__ yt) {
+  const uint32_t total = (uint32_t)n * OH * OW * C4;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t t = fdiv(i, fd_c4);
+    const int c4 = (int)(i - t * C4);
+    const uint32_t t2 = fdiv(t, fd_ow);
+    const int ow = (int)(t - t2 * OW);
+    const uint32_t b = fdiv(t2, fd_oh);
+    const int oh = (int)(t2 - b * OH);
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {-1, -1, -1, -1};
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - p + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - p + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const float4 v4 = x[((b * H + ih) * W + iw) * C4 + c4];
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (bi[q] < 0) bi[q] = kh * k + kw;
+          if (v[q] > best[q] || isnan(v[q])) {
+            best[q] = v[q];
+            bi[q] = kh * k + kw;
+          }
+        }
+      }
+    }
+    const float4 yv = make_float4(best[0], best[1], best[2], best[3]);
+    y[i] = yv;
+    am[i] = make_uchar4((unsigned char)bi[0], (unsigned char)bi[1], (unsigned char)bi[2], (unsigned char)bi[3]);
+    if (yt) {   // the pooled value's F32X3 term images [pixel][3][C] (the next conv's operand)
+      uint2 h, m, l;
+      split3(yv, h, m, l);
+      uint2 *o = yt + t * 3 * C4 + c4;
+      o[0] = h;
+      o[C4] = m;
+      o[2 * C4] = l;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd4_kernel(int n, int C4, int H, int W, int OH, int OW, int k, int s,
+                                                           int p, FastDiv fd_c4, FastDiv fd_w, FastDiv fd_h,
+                                                           const float4 *__restrict__ dy, const uchar4 *__restrict__ am,
+                                                           float4 *__restrict__ dx, uint2 *__restrict__ dxt) {
+  const uint32_t total = (uint32_t)n * H * W * C4;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t t = fdiv(i, fd_c4);
+    const int c4 = (int)(i - t * C4);
+    const uint32_t t2 = fdiv(t, fd_w);
+    const int iw = (int)(t - t2 * W);
+    const uint32_t b = fdiv(t2, fd_h);
+    const int ih = (int)(t2 - b * H);
+    int oh_lo = (ih + p - (k - 1) + s - 1) / s;
+    if (ih + p - (k - 1) < 0) oh_lo = 0;
+    const int oh_hi = min(OH - 1, (ih + p) / s);
+    int ow_lo = (iw + p - (k - 1) + s - 1) / s;
+    if (iw + p - (k - 1) < 0) ow_lo = 0;
+    const int ow_hi = min(OW - 1, (iw + p) / s);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int oh = max(0, oh_lo); oh <= oh_hi; ++oh) {
+      const int kh = ih + p - oh * s;
+      if (kh < 0 || kh >= k) continue;
+      for (int ow = max(0, ow_lo); ow <= ow_hi; ++ow) {
+        const int kw = iw + p - ow * s;
+        if (kw < 0 || kw >= k) continue;
+        const uint32_t o = ((b * OH + oh) * OW + ow) * C4 + c4;
+        const uchar4 a = am[o];
+        const float4 g = dy[o];
+        const unsigned char pos = (unsigned char)(kh * k + kw);
+        acc[0] += a.x == pos ? g.x : 0.f;
+        acc[1] += a.y == pos ? g.y : 0.f;
+        acc[2] += a.z == pos ? g.z : 0.f;
+        acc[3] += a.w == pos ? g.w : 0.f;
+      }
+    }
+    const float4 g = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    dx[i] = g;
+    if (dxt) {   // the routed gradient's term images (the producing conv's weight / data gradients)
+      uint2 h, m, l;
+      split3(g, h, m, l);
+      uint2 *o = dxt + t * 3 * C4 + c4;
+      o[0] = h;
+      o[C4] = m;
+      o[2 * C4] = l;
+    }
+  }
+}
+
+static bool pool_vec(int c, int64_t elems, const void *a, const void *b, const void *am, const void *terms) {
+  return c % 4 == 0 && elems / 4 < (1ll << 31) / 3 && !(reinterpret_cast<uintptr_t>(a) & 15) &&
+         !(reinterpret_cast<uintptr_t>(b) & 15) && !(reinterpret_cast<uintptr_t>(am) & 3) &&
+         !(reinterpret_cast<uintptr_t>(terms) & 7);
+}
+
 // ------------------------------------------------------------------------------------
 // Bilinear upsample, align_corners=True (torch area_pixel_compute_scale semantics).
 // ------------------------------------------------------------------------------------
@@ -714,27 +818,57 @@ int adaptseg_confusion_hist(int64_t npix, const uint8_t *gt, const int32_t *lut,
 
 
 const char *adaptseg_last_error(void) { return g_err; }
-const char *adaptseg_version(void) { return "adaptseg 0.1 gfx950 fp32-mfma"; }
+const char *adaptseg_version(void) { return "adaptseg 0.5 gfx950"; }
 
 int adaptseg_maxpool2d_fwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *x,
                            float *y, uint8_t *argmax, adaptseg_stream_t stream) {
+  return adaptseg_maxpool2d_fwd_x(n, c, h, w, oh, ow, k, s, p, x, y, argmax, nullptr, stream);
+}
+
+int adaptseg_maxpool2d_fwd_x(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *x,
+                             float *y, uint8_t *argmax, uint16_t *y_terms, adaptseg_stream_t stream) {
   AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && k > 0 && k * k <= 255 && s > 0 && p >= 0,
                "maxpool_fwd: bad geometry");
   AS_CHECK_ARG(x && y && argmax, "maxpool_fwd: null pointer");
   AS_CHECK_ARG((h + 2 * p - k) / s + 1 == oh && (w + 2 * p - k) / s + 1 == ow, "maxpool_fwd: output size mismatch");
   int64_t total = (int64_t)n * oh * ow * c;
-  maxpool_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, x, y, argmax);
+  const bool vec = pool_vec(c, std::max<int64_t>(total, (int64_t)n * h * w * c), x, y, argmax, y_terms);
+  AS_CHECK_ARG(vec || !y_terms, "maxpool_fwd: term images need C %% 4 == 0 and aligned tensors");
+  if (vec) {
+    const int c4 = c / 4;
+    maxpool_fwd4_kernel<<<grid1d(total / 4, 256, 16384), 256, 0, as_stream(stream)>>>(
+        n, c4, h, w, oh, ow, k, s, p, make_fastdiv(c4), make_fastdiv(ow), make_fastdiv(oh),
+        reinterpret_cast<const float4 *>(x), reinterpret_cast<float4 *>(y), reinterpret_cast<uchar4 *>(argmax),
+        reinterpret_cast<uint2 *>(y_terms));
+  } else {
+    maxpool_fwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, x, y, argmax);
+  }
   AS_CHECK_LAUNCH("maxpool_fwd");
   return ADAPTSEG_OK;
 }
 
 int adaptseg_maxpool2d_bwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *dy,
                            const uint8_t *argmax, float *dx, adaptseg_stream_t stream) {
+  return adaptseg_maxpool2d_bwd_x(n, c, h, w, oh, ow, k, s, p, dy, argmax, dx, nullptr, stream);
+}
+
+int adaptseg_maxpool2d_bwd_x(int n, int c, int h, int w, int oh, int ow, int k, int s, int p, const float *dy,
+                             const uint8_t *argmax, float *dx, uint16_t *dx_terms, adaptseg_stream_t stream) {
   AS_CHECK_ARG(n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0 && k > 0 && s > 0 && p >= 0,
                "maxpool_bwd: bad geometry");
   AS_CHECK_ARG(dy && argmax && dx, "maxpool_bwd: null pointer");
   int64_t total = (int64_t)n * h * w * c;
-  maxpool_bwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, dy, argmax, dx);
+  const bool vec = pool_vec(c, total, dy, dx, argmax, dx_terms);
+  AS_CHECK_ARG(vec || !dx_terms, "maxpool_bwd: term images need C %% 4 == 0 and aligned tensors");
+  if (vec) {
+    const int c4 = c / 4;
+    maxpool_bwd4_kernel<<<grid1d(total / 4, 256, 16384), 256, 0, as_stream(stream)>>>(
+        n, c4, h, w, oh, ow, k, s, p, make_fastdiv(c4), make_fastdiv(w), make_fastdiv(h),
+        reinterpret_cast<const float4 *>(dy), reinterpret_cast<const uchar4 *>(argmax), reinterpret_cast<float4 *>(dx),
+        reinterpret_cast<uint2 *>(dx_terms));
+  } else {
+    maxpool_bwd_kernel<<<grid1d(total), 256, 0, as_stream(stream)>>>(n, c, h, w, oh, ow, k, s, p, dy, argmax, dx);
+  }
   AS_CHECK_LAUNCH("maxpool_bwd");
   return ADAPTSEG_OK;
 }

@@ -712,28 +712,50 @@ def discriminator_forward(model, x):
 # ---------------------------------------------------------------------------------------
 
 
+# (A/B switch) DeeplabVGG (config c4) on F32X3 term images: 0 off; 1 every conv input's and
+# every conv output gradient's term images are made (the conv epilogues' / pools' copies) and the
+# weight gradients run on the term-image kernel (conv_x3r.hpp); 2 the forwards and data gradients
+# read them too
+VGG_TERMS = _switch("ADAPTSEG_VGG_TERMS", 0, (0, 1, 2))
+
+
+def vgg_terms() -> int:
+    return VGG_TERMS if K.get_conv_math() == K.MATH_F32X3 else 0
+
+
 class _DeeplabVGGFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, x, model, save):
         ctx.set_materialize_grads(False)
         n, c, h, w = x.shape
         prog = model.conv_program()
-        acts = []  # (conv input, h, w, strides, pool record or None)
+        vt = vgg_terms()
+        acts = []  # (conv input, h, w, strides, pool record or None, input's term images or None)
         cur, ch, cw, cs = x, h, w, _input_strides(x)
-        for conv, pool in prog:
+        curt = None
+        for i, (conv, pool) in enumerate(prog):
             g = conv.geom()
+            # the next conv's input terms: from this conv's epilogue, or from the pool after it
+            want_t = vt > 0 and save and i + 1 < len(prog) and g.cout % 8 == 0
             out = K.conv_fwd(g, cur, n, ch, cw, [conv.weight], [conv.bias], strides=cs,
-                             flags=K.EPI_RELU)
-            rec = [cur, ch, cw, cs, None]
+                             flags=K.EPI_RELU, xb=curt if vt >= 2 else None, bf16_out=want_t and not pool)
+            outt = None
+            if want_t and not pool:
+                out, outt = out
+            rec = [cur, ch, cw, cs, None, curt]
             ch, cw = g.out_hw(ch, cw)
             if pool:
                 ph, pw = ch, cw
-                cur, am = K.maxpool_fwd(out, k=2, s=2, p=0)
+                if want_t:
+                    cur, am, curt = K.maxpool_fwd(out, k=2, s=2, p=0, terms=True)
+                else:
+                    cur, am = K.maxpool_fwd(out, k=2, s=2, p=0)
+                    curt = None
                 rec[4] = (am, ph, pw)
                 ch, cw = cur.shape[1], cur.shape[2]
                 del out
             else:
-                cur = out
+                cur, curt = out, outt
             cs = K.nhwc_strides(n, ch, cw, cur.shape[3])
             acts.append(rec)
         branches = model.classifier_branches()
@@ -764,29 +786,41 @@ class _DeeplabVGGFn(torch.autograd.Function):
         if need_w and branches[0].weight.grad is not None:
             _wgrad(ws, gc, g, a, n, ch, cw, [b.weight.grad for b in branches],
                    [b.bias.grad for b in branches])
-        # grad of fc7's pre-activation: dgrad * relu'(a)
-        g = K.conv_dgrad(gc, g, n, ch, cw, [b.weight for b in branches], aux=a,
-                         flags=K.EPI_RELU_GRAD)
+        # grad of fc7's pre-activation: dgrad * relu'(a) (+ its term images for fc7's products)
+        vt = vgg_terms()
+        r = K.conv_dgrad(gc, g, n, ch, cw, [b.weight for b in branches], aux=a,
+                         flags=K.EPI_RELU_GRAD, bf16_out=vt > 0)
+        g, gt = r if vt > 0 else (r, None)
         del a
         prog = model.conv_program()
         dx = None
         for i in reversed(range(len(prog))):
             conv, _ = prog[i]
             geo = conv.geom()
-            xin, ih, iw, cs, _ = acts[i]
+            xin, ih, iw, cs, _, xint = acts[i]
             if need_w and conv.weight.grad is not None:
                 if geo.cin % 4:   # conv1_1 (Cin 3): on a 4-channel padded copy
                     _wgrad_padded(ws, geo, g, xin, n, ih, iw, conv.weight.grad, conv.bias.grad)
                 else:
-                    _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs)
+                    ok = gt is not None and xint is not None
+                    _wgrad(ws, geo, g, xin, n, ih, iw, [conv.weight.grad], [conv.bias.grad], strides=cs,
+                           dyb=gt if ok else None, xb=xint if ok else None)
             if i > 0:
                 # grad of the previous conv's pre-activation.  xin is its post-ReLU output,
                 # or the 2x2 max of it: relu' at the routed (argmax) position = [max > 0].
-                g = K.conv_dgrad(geo, g, n, ih, iw, [conv.weight], aux=xin, flags=K.EPI_RELU_GRAD)
                 prev_pool = acts[i - 1][4]
+                # the previous conv's output-gradient terms: from this data gradient's epilogue,
+                # or from the pool's backward
+                want_t = vt > 0 and i - 1 > 0 and geo.cin % 8 == 0
+                r = K.conv_dgrad(geo, g, n, ih, iw, [conv.weight], aux=xin, flags=K.EPI_RELU_GRAD,
+                                 dyb=gt if vt >= 2 else None, bf16_out=want_t and prev_pool is None)
+                g, gt = r if (want_t and prev_pool is None) else (r, None)
                 if prev_pool is not None:
                     am, ph, pw = prev_pool
-                    g = K.maxpool_bwd(g, am, ph, pw, k=2, s=2, p=0)
+                    if want_t:
+                        g, gt = K.maxpool_bwd(g, am, ph, pw, k=2, s=2, p=0, terms=True)
+                    else:
+                        g = K.maxpool_bwd(g, am, ph, pw, k=2, s=2, p=0)
             elif ctx.needs_input_grad[1]:
                 dx = K.as_nchw(K.conv_dgrad(geo, g, n, ih, iw, [conv.weight]))
             acts[i] = None

@@ -459,20 +459,24 @@ def grid_warp_bwd(flow, x1, x2, dy1, dy2, need_dflow=True, need_dx1=True, need_d
 # ---------------------------------------------------------------------------------------
 # Pooling / interpolation / softmax / losses
 # ---------------------------------------------------------------------------------------
-def maxpool_fwd(x, k=3, s=2, p=1):
+def maxpool_fwd(x, k=3, s=2, p=1, terms=False):
+    """-> (y, argmax), or (y, argmax, y's F32X3 term images [n, oh, ow, 3, c]) with ``terms``."""
     n, h, w, c = x.shape
     oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
     y = torch.empty((n, oh, ow, c), device=x.device, dtype=torch.float32)
     am = torch.empty((n, oh, ow, c), device=x.device, dtype=torch.uint8)
-    _OP.maxpool2d_fwd(x, y, am, k, s, p)
-    return y, am
+    yt = torch.empty((n, oh, ow, 3, c), device=x.device, dtype=torch.bfloat16) if terms else None
+    _OP.maxpool2d_fwd(x, y, am, yt, k, s, p)
+    return (y, am, yt) if terms else (y, am)
 
 
-def maxpool_bwd(dy, am, h, w, k=3, s=2, p=1):
+def maxpool_bwd(dy, am, h, w, k=3, s=2, p=1, terms=False):
+    """-> dx, or (dx, dx's F32X3 term images [n, h, w, 3, c]) with ``terms``."""
     n, oh, ow, c = dy.shape
     dx = torch.empty((n, h, w, c), device=dy.device, dtype=torch.float32)
-    _OP.maxpool2d_bwd(dy, am, dx, k, s, p)
-    return dx
+    dxt = torch.empty((n, h, w, 3, c), device=dy.device, dtype=torch.bfloat16) if terms else None
+    _OP.maxpool2d_bwd(dy, am, dx, dxt, k, s, p)
+    return (dx, dxt) if terms else dx
 
 
 def upsample_fwd(x, oh, ow):

@@ -396,20 +396,22 @@ def _grid_warp_bwd(flow, x1, x2, dy1, dy2, dflow, dx1, dx2):
 
 
 # ---- pooling / interpolation / softmax / losses ------------------------------------------
-@_op("maxpool2d_fwd(Tensor x, Tensor(a!) y, Tensor(b!) argmax, int k, int s, int p) -> ()")
-def _maxpool2d_fwd(x, y, argmax, k, s, p):
+@_op("maxpool2d_fwd(Tensor x, Tensor(a!) y, Tensor(b!) argmax, Tensor(c!)? y_terms, int k, int s, int p) -> ()")
+def _maxpool2d_fwd(x, y, argmax, y_terms, k, s, p):
+    """y_terms: the pooled output's F32X3 term images [n, oh, ow, 3, c] (bf16) or None."""
     n, h, w, c = x.shape
     oh, ow = y.shape[1], y.shape[2]
-    check(_lib.lib().adaptseg_maxpool2d_fwd(n, c, h, w, oh, ow, k, s, p, _p(x), _p(y), _p(argmax), _stream()),
-          "maxpool2d_fwd")
+    check(_lib.lib().adaptseg_maxpool2d_fwd_x(n, c, h, w, oh, ow, k, s, p, _p(x), _p(y), _p(argmax), _p(y_terms),
+                                              _stream()), "maxpool2d_fwd")
 
 
-@_op("maxpool2d_bwd(Tensor dy, Tensor argmax, Tensor(a!) dx, int k, int s, int p) -> ()")
-def _maxpool2d_bwd(dy, argmax, dx, k, s, p):
+@_op("maxpool2d_bwd(Tensor dy, Tensor argmax, Tensor(a!) dx, Tensor(b!)? dx_terms, int k, int s, int p) -> ()")
+def _maxpool2d_bwd(dy, argmax, dx, dx_terms, k, s, p):
+    """dx_terms: the routed gradient's F32X3 term images [n, h, w, 3, c] (bf16) or None."""
     n, oh, ow, c = dy.shape
     h, w = dx.shape[1], dx.shape[2]
-    check(_lib.lib().adaptseg_maxpool2d_bwd(n, c, h, w, oh, ow, k, s, p, _p(dy), _p(argmax), _p(dx), _stream()),
-          "maxpool2d_bwd")
+    check(_lib.lib().adaptseg_maxpool2d_bwd_x(n, c, h, w, oh, ow, k, s, p, _p(dy), _p(argmax), _p(dx), _p(dx_terms),
+                                              _stream()), "maxpool2d_bwd")
 
 
 @_op("upsample_bilinear_fwd(Tensor x, Tensor(a!) y) -> ()")

@@ -67,10 +67,18 @@ class StepConfig:
     # run the target-domain generator forward (+ its D forward) on a second HIP stream while
     # the source-domain backward executes (independent: same weights, read-only, separate
     # gradient kernels); the target backward then waits for the source backward.  Results are
-    # bit-identical to the sequential order.  Off by default: +1-2.5 % images/s at c2/c3/c5,
-    # but every forward conv then shares the GPU with backward kernels, which halves the
-    # per-launch roofline of the dominant kernel that bench.py reports.
-    overlap_domains: bool = False
+    # bit-identical to the sequential order (tests/test_model_gpu.py).  "auto" (the default):
+    # on for DeeplabMulti — the backward alone does not fill the chip, the forward beside it
+    # does: c2 +1.3 %, c3 +1.1 %, c5 +3.6 % (profiles/r5/overlap_ab.txt) — off for DeeplabVGG
+    # (c4 -0.6 %).
+    overlap_domains: bool | str = "auto"
+    # run the discriminator step (its forwards on the detached predictions and its backwards,
+    # train:435-461 / 642-679) on its own HIP stream as soon as the target forward is done, beside
+    # the step's last generator backward: it reads only the detached predictions and D's weights
+    # (unchanged until the optimisers), and writes only D's gradient arena, which that backward
+    # does not touch (D's parameters are frozen while its graph is built).  Results are
+    # bit-identical to the sequential order (tests/test_model_gpu.py).
+    overlap_d: bool = False
     # data parallel: size of the generator's gradient all-reduce buckets (DeeplabMulti); 0 =
     # one all-reduce of the whole arena after its last backward
     bucket_mb: float = 32.0
@@ -128,9 +136,15 @@ class AdaptSegTrainer:
     # -- stream overlap of the two domains -----------------------------------------------------
     _streams: dict = {}
 
+    def _overlap_domains(self) -> bool:
+        ov = self.cfg.overlap_domains
+        if ov == "auto":
+            return not getattr(self.model, "single_output", False)
+        return bool(ov)
+
     def _overlap_begin(self, device):
         """After the source forward: returns (main, side, event) or None (overlap off / CPU)."""
-        if not self.cfg.overlap_domains or device.type != "cuda":
+        if not self._overlap_domains() or device.type != "cuda":
             return None
         side = AdaptSegTrainer._streams.get(device.index)
         if side is None:
@@ -153,6 +167,36 @@ class AdaptSegTrainer:
         finished writing the gradient arena it accumulates into."""
         if ov is not None:
             ov[1].wait_stream(ov[0])
+
+    _d_streams: dict = {}
+
+    def _d_fork(self, device):
+        """After the target forward (+ its D forward), on the stream that ran it: an event the
+        discriminator step's stream waits on, or None (overlap_d off / CPU)."""
+        if not self.cfg.overlap_d or device.type != "cuda":
+            return None
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        return ev
+
+    def _d_ctx(self, ev, device, *tensors):
+        """The discriminator step's stream context: waits for ``ev`` only; ``tensors`` (made on
+        other streams) are marked used on it.  The main stream joins it before the optimisers."""
+        if ev is None:
+            return contextlib.nullcontext()
+        ds = AdaptSegTrainer._d_streams.get(device.index)
+        if ds is None:
+            ds = AdaptSegTrainer._d_streams[device.index] = torch.cuda.Stream(device)
+        ds.wait_event(ev)
+        for t in tensors:
+            t.record_stream(ds)
+        self.__dict__.setdefault("_d_used", set()).add(device.index)
+        return torch.cuda.stream(ds)
+
+    def _d_join(self, device):
+        if device.index in self.__dict__.get("_d_used", ()):
+            torch.cuda.current_stream(device).wait_stream(AdaptSegTrainer._d_streams[device.index])
+            self._d_used.discard(device.index)
 
     @staticmethod
     def _overlap_end(ov, *tensors):
@@ -295,6 +339,8 @@ class AdaptSegTrainer:
                 self._sub_multi(images, labels, images_t, inv, tsize, L, g_done)
         if not batches:
             self._start_sync((self.model,))
+        if batches and c.level != "source-only":
+            self._d_join(next(self.model.parameters()).device)
         self._start_sync((self.D1, self.D2))
         self._finish_sync()
         gs = 1.0 / self.world
@@ -342,6 +388,8 @@ class AdaptSegTrainer:
             pred_target2 = self._pred_single(images_t, tsize, None if flow is None else flow.detach())
             d_out2 = D2(F.softmax2d(pred_target2))
             loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
+            dev_ = d_out2.device
+            dfork = self._d_fork(dev_)
             self._join_source(ov)
             if g_done is not None:
                 g_done.begin()
@@ -353,13 +401,14 @@ class AdaptSegTrainer:
 
         self._set_requires_grad(D2, True)
         pred2 = pred2.detach()
-        loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
-        self._backward([loss_d2], [inv / 2])
-        L.add("loss_D2", loss_d2, inv / 2)
         pred_target2 = pred_target2.detach()
-        loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
-        self._backward([loss_d2], [inv / 2])
-        L.add("loss_D2", loss_d2, inv / 2)
+        with self._d_ctx(dfork, dev_, pred2, pred_target2):
+            loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
+            self._backward([loss_d2], [inv / 2])
+            L.add("loss_D2", loss_d2, inv / 2)
+            loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+            self._backward([loss_d2], [inv / 2])
+            L.add("loss_D2", loss_d2, inv / 2)
 
     def _sub_multi(self, images, labels, images_t, inv, tsize, L, g_done=None):
         """train_gta2cityscapes_multi.py:578-679."""
@@ -380,6 +429,8 @@ class AdaptSegTrainer:
             d_out2 = D2(F.softmax2d(pred_target2))
             loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
             loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
+            dev_ = d_out2.device
+            dfork = self._d_fork(dev_)
             self._join_source(ov)
             if g_done is not None:
                 g_done.begin()
@@ -394,19 +445,20 @@ class AdaptSegTrainer:
         self._set_requires_grad(D1, True)
         self._set_requires_grad(D2, True)
         pred1, pred2 = pred1.detach(), pred2.detach()
-        loss_d1 = F.adv_loss(D1(F.softmax2d(pred1)), 0.0, self.kind)
-        loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
-        self._backward([loss_d1], [inv / 2])
-        self._backward([loss_d2], [inv / 2])
-        L.add("loss_D1", loss_d1, inv / 2)
-        L.add("loss_D2", loss_d2, inv / 2)
         pred_target1, pred_target2 = pred_target1.detach(), pred_target2.detach()
-        loss_d1 = F.adv_loss(D1(F.softmax2d(pred_target1)), 1.0, self.kind)
-        loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
-        self._backward([loss_d1], [inv / 2])
-        self._backward([loss_d2], [inv / 2])
-        L.add("loss_D1", loss_d1, inv / 2)
-        L.add("loss_D2", loss_d2, inv / 2)
+        with self._d_ctx(dfork, dev_, pred1, pred2, pred_target1, pred_target2):
+            loss_d1 = F.adv_loss(D1(F.softmax2d(pred1)), 0.0, self.kind)
+            loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
+            self._backward([loss_d1], [inv / 2])
+            self._backward([loss_d2], [inv / 2])
+            L.add("loss_D1", loss_d1, inv / 2)
+            L.add("loss_D2", loss_d2, inv / 2)
+            loss_d1 = F.adv_loss(D1(F.softmax2d(pred_target1)), 1.0, self.kind)
+            loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+            self._backward([loss_d1], [inv / 2])
+            self._backward([loss_d2], [inv / 2])
+            L.add("loss_D1", loss_d1, inv / 2)
+            L.add("loss_D2", loss_d2, inv / 2)
 
 
 class _GSync:

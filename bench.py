@@ -314,9 +314,12 @@ def main():
                          "bf16 MFMA) or f32 (the fp32-input MFMA kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--overlap", action="store_true",
+    ap.add_argument("--overlap", default="auto", choices=("auto", "on", "off"),
                     help="run the target-domain pass on a second stream, overlapping the source "
-                         "backward (StepConfig.overlap_domains)")
+                         "backward (StepConfig.overlap_domains; auto: on for DeeplabMulti)")
+    ap.add_argument("--overlap-d", action="store_true",
+                    help="run the discriminator step on its own stream beside the last generator "
+                         "backward (StepConfig.overlap_d)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path with several ranks on one GPU)")
@@ -353,7 +356,8 @@ def main():
                     dist.broadcast(t.data, 0)
     model.train()
     scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
-                      overlap_domains=args.overlap)
+                      overlap_domains={"auto": "auto", "on": True, "off": False}[args.overlap],
+                      overlap_d=args.overlap_d)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
@@ -451,6 +455,7 @@ def main():
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
                    "conv_math": conv_math,
                    "switches": engine.switches(),
+                   "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across

@@ -362,6 +362,17 @@ int adaptseg_maxpool2d_fwd(int n, int c, int h, int w, int oh, int ow, int k, in
 int adaptseg_maxpool2d_bwd(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,
                            const float *dy, const uint8_t *argmax, float *dx,
                            adaptseg_stream_t stream);
+/* The same with the output's F32X3 term images (the _x operand copies of the conv consuming it,
+   [..., 3, C] pixel-interleaved; NULL = none): the pooled activation for the next conv's
+   products (DeeplabVGG's 2x2 pools, model/deeplab_vgg.py: pool -> conv), the routed gradient for
+   the pooled conv's weight / data gradients.  Terms need C % 4 == 0 and 16-B aligned fp32
+   tensors (8-B aligned term images), else ADAPTSEG_ERR_ARG. */
+int adaptseg_maxpool2d_fwd_x(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,
+                             const float *x, float *y, uint8_t *argmax, uint16_t *y_terms,
+                             adaptseg_stream_t stream);
+int adaptseg_maxpool2d_bwd_x(int n, int c, int h, int w, int oh, int ow, int k, int s, int p,
+                             const float *dy, const uint8_t *argmax, float *dx, uint16_t *dx_terms,
+                             adaptseg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* nn.Upsample(mode='bilinear', align_corners=True), NHWC (model/deeplab_multi.py:188). */

@@ -246,27 +246,34 @@ def test_adversarial_step_train_bn(data, level, gan):
 @pytest.mark.parametrize("level,gan", LEVEL_GAN)
 def test_domain_overlap_is_bit_identical(data, level, gan):
     """StepConfig.overlap_domains (target-domain pass on a second stream, overlapping the
-    source backward) must not change a single bit of the losses or parameters."""
-    cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33))
-    runs = []
-    for ov in (False, True):
-        from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
-        xs, lab, xt = data
-        m, d1, d2 = build_g(), build_d(2001), build_d(2002)
-        m.train()
-        tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2,
-                             StepConfig(**cfg, overlap_domains=ov))
-        batch = [(xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))]
-        losses = [tr.step(it, batch).values() for it in range(2)]
-        torch.cuda.synchronize()
-        runs.append((losses, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
-                     {k: v.detach().cpu().clone() for k, v in d2.state_dict().items()}))
-    (l0, g0, d0), (l1, g1, d1_) = runs
-    assert l0 == l1
-    for k in g0:
-        assert torch.equal(g0[k], g1[k]), k
-    for k in d0:
-        assert torch.equal(d0[k], d1_[k]), k
+    source backward) and StepConfig.overlap_d (the discriminator step on its own stream beside
+    the last generator backward), alone and together, with iter_size 1 and 2, must not change a
+    single bit of the losses or parameters against the sequential order."""
+    from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
+    xs, lab, xt = data
+    batch = (xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))
+    batch2 = (torch.from_numpy(R.det_images(tuple(xs.shape), 31)).float().to(DEV),
+              torch.from_numpy(R.det_labels(tuple(lab.shape), 32)).to(DEV),
+              torch.from_numpy(R.det_images(tuple(xt.shape), 33)).float().to(DEV))
+    for iters in (1, 2):
+        cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33), iter_size=iters)
+        runs = []
+        for ov, od in ((False, False), (True, False), (False, True), (True, True)):
+            m, d1, d2 = build_g(), build_d(2001), build_d(2002)
+            m.train()
+            tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2,
+                                 StepConfig(**cfg, overlap_domains=ov, overlap_d=od))
+            subs = [batch, batch2][:iters]
+            losses = [tr.step(it, subs).values() for it in range(2)]
+            torch.cuda.synchronize()
+            runs.append((losses, [{k: v.detach().cpu().clone() for k, v in mm.state_dict().items()}
+                                  for mm in (m, d1, d2)]))
+        (l0, s0) = runs[0]
+        for (l1, s1), tag in zip(runs[1:], ("overlap_domains", "overlap_d", "both")):
+            assert l0 == l1, (tag, iters, l0, l1)
+            for a, b in zip(s0, s1):
+                for k in a:
+                    assert torch.equal(a[k], b[k]), (tag, iters, k)
 
 
 @pytest.mark.parametrize("level,gan", LEVEL_GAN)

@@ -297,20 +297,49 @@ def test_batchnorm_eval_and_inplace_bwd():
     assert rel(nchw(gyd), xr.grad) < 1e-5
 
 
-def test_maxpool():
+@pytest.mark.parametrize("c,ksp", [(64, (3, 2, 1)), (19, (3, 2, 1)), (64, (2, 2, 0)), (6, (2, 2, 0))],
+                         ids=["stem-vec4", "stem-scalar", "vgg-vec4", "vgg-scalar"])
+def test_maxpool(c, ksp):
+    """nn.MaxPool2d(3, 2, 1) (deeplab_multi.py:135) and the VGG 2x2 pools (deeplab_vgg.py) on both
+    kernels: four channels per thread (C % 4 == 0) and the scalar one."""
     k = K()
+    ks, st, pd = ksp
     g = torch.Generator().manual_seed(9)
-    x = F.relu(torch.randn(2, 64, 21, 29, generator=g, dtype=torch.float64))  # ties at 0
+    x = F.relu(torch.randn(2, c, 21, 29, generator=g, dtype=torch.float64))  # ties at 0
     xr = x.clone().requires_grad_(True)
-    y = F.max_pool2d(xr, 3, 2, 1)
+    y = F.max_pool2d(xr, ks, st, pd)
     gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     y.backward(gy)
-    yd, am = k.maxpool_fwd(nhwc(x))
+    yd, am = k.maxpool_fwd(nhwc(x), k=ks, s=st, p=pd)
     assert torch.equal(nchw(yd).float(), y.detach().float())
-    dx = k.maxpool_bwd(nhwc(gy), am, 21, 29)
+    dx = k.maxpool_bwd(nhwc(gy), am, 21, 29, k=ks, s=st, p=pd)
     # gradient routing is exact wherever the max is unique (>0); zero ties only feed ReLU zeros
     mask = (x > 0)
     assert rel(nchw(dx) * mask, xr.grad * mask) < 1e-6
+
+
+def test_maxpool_vec4_matches_scalar_bitwise():
+    """The float4 pool kernels against the scalar ones on the same values (a tensor one float off
+    16-B alignment takes the scalar kernel): outputs, argmax (ties, NaN) and routed gradients
+    bitwise."""
+    k = K()
+    g = torch.Generator().manual_seed(4)
+    for ks, st, pd in ((3, 2, 1), (2, 2, 0)):
+        x = F.relu(torch.randn(2, 21, 29, 64, generator=g)).to(DEV)
+        x[0, 3, 5, 7] = float("nan")
+        buf = torch.empty(x.numel() + 1, device=DEV)
+        xm = buf[1:].view(x.shape)
+        xm.copy_(x)
+        ya, ama = k.maxpool_fwd(x, k=ks, s=st, p=pd)
+        yb, amb = k.maxpool_fwd(xm, k=ks, s=st, p=pd)
+        assert torch.equal(ama, amb)
+        assert torch.equal(ya.nan_to_num(7.0), yb.nan_to_num(7.0))
+        gy = torch.randn(ya.shape, generator=g).to(DEV)
+        gbuf = torch.empty(gy.numel() + 1, device=DEV)
+        gm = gbuf[1:].view(gy.shape)
+        gm.copy_(gy)
+        assert torch.equal(k.maxpool_bwd(gy, ama, 21, 29, k=ks, s=st, p=pd),
+                           k.maxpool_bwd(gm, ama, 21, 29, k=ks, s=st, p=pd))
 
 
 @pytest.mark.parametrize("hw,out", [((9, 13), (65, 97)), ((64, 128), (512, 1024)),

@@ -46,8 +46,17 @@ def _frob(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["fp32", "wgrad-terms", "all-terms"])
+def vgg_terms(request, monkeypatch):
+    """engine.VGG_TERMS: the VGG program on fp32 operands, with its weight gradients on the
+    term-image kernel, or with every product reading term images."""
+    from adaptsegnet_amd import engine
+    monkeypatch.setattr(engine, "VGG_TERMS", request.param)
+    return request.param
+
+
 @pytest.mark.gpu
-def test_vgg_forward_backward_gpu():
+def test_vgg_forward_backward_gpu(vgg_terms):
     from adaptsegnet_amd.model import DeeplabVGG
     state = R.det_state(R.vgg_specs(), 4242)
     P = R.to_torch(state, trainable=lambda k: True)
@@ -77,7 +86,7 @@ def test_vgg_forward_backward_gpu():
 
 
 @pytest.mark.gpu
-def test_vgg_single_level_step_gpu():
+def test_vgg_single_level_step_gpu(vgg_terms):
     """One c4-style trainer step: loss_seg2 = CE(interp(VGG(x))) matches the oracle, and the
     update touches every used parameter (SGD, one LR group) and no unused branch."""
     from adaptsegnet_amd.model import DeeplabVGG, FCDiscriminator

@@ -28,9 +28,10 @@ def mangled(name):
         return None
     base, args = name.split("<", 1)
     parts = [a.strip() for a in args.rstrip(">").split(",")]
-    if not all(a.lstrip("-").isdigit() for a in parts):
+    enc = {"false": "Lb0E", "true": "Lb1E"}
+    if not all(a.lstrip("-").isdigit() or a in enc for a in parts):
         return None
-    return base + "I" + "".join(f"Li{a}E" for a in parts)
+    return base + "I" + "".join(enc.get(a, f"Li{a}E") for a in parts)
 
 
 def key_of(name):
@@ -42,7 +43,10 @@ def key_of(name):
 
 
 def grid(r):
-    return r.get("Grid_Size_X") or r.get("Grid_Size") or "?"
+    """total work-items of the dispatch (the trace gives X / Y / Z, the counter CSV the product)"""
+    if r.get("Grid_Size_X"):
+        return str(int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y") or 1) * int(r.get("Grid_Size_Z") or 1))
+    return r.get("Grid_Size") or "?"
 
 
 trace = collections.defaultdict(list)
@@ -81,7 +85,7 @@ def per(ds, f):
 
 print(f"{'kernel':28s} {'grid':>9s} {'n':>3s} {'step us':>8s} {'alone us':>8s} {'MFMA':>6s} {'VALU':>6s} "
       f"{'stall':>6s} {'parked':>6s} {'issue':>6s} {'valu/mf':>7s} {'lds/mf':>6s} {'bankc':>6s} {'MB/launch':>9s}")
-for (k, g) in sorted(set(trace) | set(alone)):
+for (k, g) in sorted(set(trace) | set(alone), key=lambda kg: (kg[0], int(kg[1]) if kg[1].isdigit() else 0)):
     st = trace.get((k, g), [])
     ds = list(alone.get((k, g), {}).values())
     al = mean(d["_us"] for d in ds if d.get("_us", 0) > 0)
