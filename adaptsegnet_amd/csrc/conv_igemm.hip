@@ -55,7 +55,7 @@ __global__ void splitk_reduce_kernel(const ConvParams p, const float *slab, int 
       v = epi_act(v, p.flags);
       if (p.flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], p.flags);
       if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
-      if (p.outb) p.outb[idx] = (__bf16)v;
+      if (p.outb) epi_outb(p, (size_t)row, col, v);
     }
   }
 }
@@ -167,8 +167,17 @@ __global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvParams p,
     }
     if (o) *reinterpret_cast<float4 *>(o) = v;   // (NULL: bf16 storage, only the copy below)
     if (mode != MODE_WGRAD && p.outb) {
-      __bf16 *ob = p.outb + idx;
-      ob[0] = (__bf16)v.x; ob[1] = (__bf16)v.y; ob[2] = (__bf16)v.z; ob[3] = (__bf16)v.w;
+      if (p.outb_terms) {   // the F32X3 term images [row][3][N]
+        uint2 th, tm, tl;
+        split3(v, th, tm, tl);
+        uint2 *ob = reinterpret_cast<uint2 *>(p.outb + (size_t)row * 3 * p.N + col);
+        ob[0] = th;
+        ob[p.N / 4] = tm;
+        ob[p.N / 2] = tl;
+      } else {
+        __bf16 *ob = p.outb + idx;
+        ob[0] = (__bf16)v.x; ob[1] = (__bf16)v.y; ob[2] = (__bf16)v.z; ob[3] = (__bf16)v.w;
+      }
     }
   }
 }
@@ -785,6 +794,13 @@ __global__ void __launch_bounds__(256) x3_out_copy4_kernel(const float4 *__restr
   }
 }
 
+// F32X3 output term images written by the GEMM epilogue / split-K reduce itself (the F32X3
+// kernels: the staged and term-image ones) instead of by out_copy's pass over the finished fp32
+// output: 8-B aligned images, N % 4 == 0, < 2^31 term elements (the epilogue's 32-bit offsets)
+static bool terms_in_epilogue(const Plan &pl, const uint16_t *yb, int64_t n) {
+  return yb && pl.fast && pl.x3 && pl.p.N % 4 == 0 && 3 * n < (1ll << 31) && !(reinterpret_cast<uintptr_t>(yb) & 7);
+}
+
 // The operand copy of a finished output [n / C][C] (the paths whose kernels do not write it): a
 // bf16 RNE image, or the three term images under the F32X3 maths
 static int out_copy(const float *y, uint16_t *yb, int64_t n, int C, hipStream_t s) {
@@ -994,16 +1010,18 @@ int adaptseg_conv2d_fwd_x(const adaptseg_conv_desc *d, const float *x, const uin
   // kernel reads the copy, so a NULL x needs it to survive the alignment checks too
   AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd: x is NULL but the plan (after the alignment checks) needs the fp32 input");
-  const bool terms = copies_are_terms();   // F32X3: term images of y by a pass after the GEMM
+  const bool terms = copies_are_terms();   // F32X3: term images of y (the epilogue's, or a pass after the GEMM)
   AS_CHECK_ARG(y || !terms, "conv fwd: under the F32X3 maths the output is fp32 (y_bf16 is its term images)");
+  const bool fused = terms && terms_in_epilogue(pl, y_bf16, ny);
   p.out = y;
-  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb = (terms && !fused) ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb_terms = fused ? 1 : 0;
   p.res = res;
   p.flags = flags;
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(y, y_bf16, ny, d->k, as_stream(stream));
+  return (st || !terms || fused) ? st : out_copy(y, y_bf16, ny, d->k, as_stream(stream));
 }
 
 int adaptseg_conv2d_bnstats_size(const adaptseg_conv_desc *d, size_t *bytes) {
@@ -1074,8 +1092,11 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
                "conv fwd_bnstats: x is NULL but the plan (after the alignment checks) needs the fp32 input");
   const bool terms = copies_are_terms();
   AS_CHECK_ARG(y || !terms, "conv fwd_bnstats: under the F32X3 maths the output is fp32");
+  const int64_t nyb = (int64_t)d->n * d->oh * d->ow * d->k;
+  const bool fused = terms && terms_in_epilogue(pl, y_bf16, nyb);
   p.out = y;
-  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb = (terms && !fused) ? nullptr : reinterpret_cast<__bf16 *>(y_bf16);
+  p.outb_terms = fused ? 1 : 0;
   p.flags = 0;
   if (pl.fast && p.splits == 1) {
     const int nt = (int)ceil_div(p.M, plan_bm(pl));
@@ -1088,7 +1109,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_FWD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(y, y_bf16, (int64_t)d->n * d->oh * d->ow * d->k, d->k, as_stream(stream));
+  return (st || !terms || fused) ? st : out_copy(y, y_bf16, nyb, d->k, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const float *const *w,
@@ -1153,8 +1174,10 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
   AS_CHECK_ARG(dy || ((pl.g16 || pl.x3ext) && pl.act_ext),
                "conv bwd_data: dy is NULL but the plan (after the alignment checks) needs the fp32 dY");
   const bool terms = copies_are_terms();
+  const bool fused = terms && terms_in_epilogue(pl, dx_bf16, nx);
   p.out = dx;
-  p.outb = terms ? nullptr : reinterpret_cast<__bf16 *>(dx_bf16);
+  p.outb = (terms && !fused) ? nullptr : reinterpret_cast<__bf16 *>(dx_bf16);
+  p.outb_terms = fused ? 1 : 0;
   p.res = res;
   p.resb = reinterpret_cast<const __bf16 *>(res_bf16);
   p.resbits = res_bits;
@@ -1163,7 +1186,7 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
-  return (st || !terms) ? st : out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
+  return (st || !terms || fused) ? st : out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
 }
 
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,

@@ -65,6 +65,7 @@ struct ConvParams {
   int pad_[4], dil_[4];        // per-segment padding / dilation
   FastDiv fd_taps, fd_kw;
   __bf16 *outb;                // FWD / DGRAD: optional bf16 (RNE) copy of the final output (NULL: none)
+  int outb_terms;              //   ... or (1) its F32X3 term images [rows][3][N] (the _x forms' copies)
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
@@ -75,6 +76,20 @@ struct ConvParams {
 // or bf16 in p.resb)
 __device__ __forceinline__ float epi_prev(const ConvParams &p, size_t idx) {
   return p.out ? p.out[idx] : (float)p.outb[idx];
+}
+// The operand copy of output element (row, col): a bf16 RNE image, or its three exact bf16
+// terms pixel-interleaved [row][3][N] (F32X3: the consumer conv's term-image operand)
+__device__ __forceinline__ void epi_outb(const ConvParams &p, size_t row, int col, float v) {
+  if (p.outb_terms) {
+    uint32_t h, m, l;
+    split3_2(v, 0.f, h, m, l);
+    __bf16 *o = p.outb + row * 3 * p.N + col;
+    o[0] = __builtin_bit_cast(__bf16, (uint16_t)h);
+    o[p.N] = __builtin_bit_cast(__bf16, (uint16_t)m);
+    o[2 * p.N] = __builtin_bit_cast(__bf16, (uint16_t)l);
+  } else {
+    p.outb[row * p.N + col] = (__bf16)v;
+  }
 }
 __device__ __forceinline__ float epi_res(const ConvParams &p, size_t idx) {
   const float r = p.resb ? (float)p.resb[idx] : p.res[idx];
@@ -566,7 +581,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) igemm_kernel(const Con
           v = epi_act(v, flags);
           if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
           if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
-          if (p.outb) p.outb[idx] = (__bf16)v;
+          if (p.outb) epi_outb(p, row, col, v);
         }
     }
   }
@@ -783,6 +798,16 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int gcol = bn + wn * wtn + j * 32 + c4;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);   // the summed segment biases of these 4 columns
+    if constexpr (MODE == MODE_FWD) {
+      for (int sg = 0; sg < p.nseg; ++sg) {
+        const float *bp = sg == 0 ? p.bias[0] : sg == 1 ? p.bias[1] : sg == 2 ? p.bias[2] : p.bias[3];
+        if (bp) {
+          const float4 b4 = *reinterpret_cast<const float4 *>(bp + gcol);
+          bsum.x += b4.x; bsum.y += b4.y; bsum.z += b4.z; bsum.w += b4.w;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       __builtin_amdgcn_sched_barrier(0);   // one block's operands live at a time
@@ -803,8 +828,12 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's stores land before its reads
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        const uint32_t e = orow(grow + 8 * h) * N + gcol;
+        const uint32_t orw = orow(grow + 8 * h);
+        const uint32_t e = orw * N + gcol;
         float4 v = *reinterpret_cast<const float4 *>(w + (rr + 8 * h) * LS + c4);
+        if constexpr (MODE == MODE_FWD) {
+          v.x += bsum.x; v.y += bsum.y; v.z += bsum.z; v.w += bsum.w;
+        }
         if constexpr (EK == EK_ACC_F32) {
           v.x += rd[h].x; v.y += rd[h].y; v.z += rd[h].z; v.w += rd[h].w;
         }
@@ -821,7 +850,15 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
           v.x = epi_act_grad(v.x, rd[h].x, flags); v.y = epi_act_grad(v.y, rd[h].y, flags);
           v.z = epi_act_grad(v.z, rd[h].z, flags); v.w = epi_act_grad(v.w, rd[h].w, flags);
         }
-        st_e<float4>(p.out, e >> 2, v);
+        if (p.out) st_e<float4>(p.out, e >> 2, v);
+        if (p.outb) {   // the term images [row][3][N] (outb_terms; < 2^31 elements, the host checks)
+          uint2 th, tm, tl;
+          split3(v, th, tm, tl);
+          const uint32_t e3 = orw * 3 * N + gcol;
+          st_e<uint2>(p.outb, e3 >> 2, th);
+          st_e<uint2>(p.outb, (e3 + N) >> 2, tm);
+          st_e<uint2>(p.outb, (e3 + 2 * N) >> 2, tl);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's staging
     }
@@ -859,7 +896,7 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
         v = epi_act(v, flags);
         if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
         if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
-        if (p.outb) p.outb[idx] = (__bf16)v;
+        if (p.outb) epi_outb(p, out_row(row), col, v);
       }
   }
 }
@@ -959,9 +996,14 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
       }
     }
     if constexpr (VEC == 2) {
-      vec = full && p.out && !p.outb && (p.N & 3) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
+      // (fp32 output and / or its term images; biases as 16-B rows)
+      vec = full && (p.out || p.outb_terms) && (!p.outb || p.outb_terms) && (p.N & 3) == 0 &&
             (ek == EK_PLAIN || ek == EK_RES_F32 || ek == EK_ACC_F32 || ek == EK_ACTGRAD) &&
-            !(reinterpret_cast<uintptr_t>(p.out) & 15) &&
+            !(reinterpret_cast<uintptr_t>(p.out) & 15) && !(reinterpret_cast<uintptr_t>(p.outb) & 7) &&
+            (MODE != MODE_FWD || ((!p.bias[0] || !(reinterpret_cast<uintptr_t>(p.bias[0]) & 15)) &&
+                                  (p.nseg < 2 || !p.bias[1] || !(reinterpret_cast<uintptr_t>(p.bias[1]) & 15)) &&
+                                  (p.nseg < 3 || !p.bias[2] || !(reinterpret_cast<uintptr_t>(p.bias[2]) & 15)) &&
+                                  (p.nseg < 4 || !p.bias[3] || !(reinterpret_cast<uintptr_t>(p.bias[3]) & 15)))) &&
             (ek != EK_RES_F32 || !(reinterpret_cast<uintptr_t>(p.res) & 15)) &&
             (ek != EK_ACTGRAD || !(reinterpret_cast<uintptr_t>(p.aux) & 15));
       if (vec) {

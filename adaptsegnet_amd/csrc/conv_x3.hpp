@@ -258,7 +258,8 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](auto buf_c) {
+    constexpr int buf = decltype(buf_c)::value;
     char *As = lds + buf * STAGE;
     char *Bs = As + 3 * IMG;
     if constexpr (!MC) {
@@ -294,6 +295,29 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
 
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
+  // M/N-contiguous images: each lane's two transposed-read offsets per fragment (conv_bf16.hpp
+  // mc_frag) within one image, computed once; a read adds only the compile-time stage / term
+  // image base, which the DS offset field absorbs
+  uint32_t mca[MC ? TM : 1][2], mcb[MC ? TN : 1][2];
+  if constexpr (MC) {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int kb = 8 * (g >> 1);
+    auto offs = [&](int c0, uint32_t (&o)[2]) {
+      const int ch = ((c0 + 16 * (g & 1)) >> 3) + (pp >> 1);
+      o[0] = (uint32_t)(mc_off(kb + q, ch) + 8 * (pp & 1));
+      o[1] = (uint32_t)(mc_off(kb + 4 + q, ch) + 8 * (pp & 1));
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) offs(wm * WTM + i * 32, mca[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) offs(wn * WTN + j * 32, mcb[j]);
+  }
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)lds;
+  auto mc_read = [&](uint32_t img_base, const uint32_t (&o)[2]) -> bf16x8 {
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(img_base + o[0]));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(img_base + o[1]));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -316,25 +340,31 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
   // the split + LDS stores instead, so a staging wave is not starved behind the other wave's
   // MFMAs (measured: FWD 152.5 vs 148.6 TF/s with the WGRAD choice, WGRAD 142.0 vs 131.8 with
   // the FWD one, tools/dbg/ab_libs.sh).
-  int cur = 0;
-  // One 16-deep K step from LDS buffer `cur`: the six split products of every 32x32 tile,
-  // term-major so consecutive MFMAs write different accumulators.  The K-contiguous kernels
-  // then split + store the NEXT step's staged registers into LDS buffer cur^1 in the same basic
-  // block, and the scheduler interleaves that vector / LDS work between the MFMAs (one MFMA,
-  // three VALU, one LDS store) instead of running it after them.
-  auto compute = [&](auto with_store) {
+  // One 16-deep K step from LDS buffer `cur` (a compile-time stage: the loop below is unrolled
+  // by two, so every fragment and staging address is a loop-invariant VGPR plus an immediate
+  // offset — with a runtime stage the weight gradient spent ~30 v_add_u32 per step rebuilding its
+  // 18 transposed-read addresses): the six split products of every 32x32 tile, term-major so
+  // consecutive MFMAs write different accumulators.  The kernels then split + store the NEXT
+  // step's staged registers into LDS buffer cur^1 in the same basic block, and the scheduler
+  // interleaves that vector / LDS work between the MFMAs (one MFMA, three VALU, one LDS store)
+  // instead of running it after them.
+  auto compute = [&](auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
     const char *As = lds + cur * STAGE;
     const char *Bs = As + 3 * IMG;
     bf16x8 a[3][TM], b[3][TN];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        a[s][i] = MC ? mc_frag(As + s * IMG, wm * WTM + i * 32, 0, lane) : kc16_frag(As + s * IMG, wm * WTM + i * 32, lane);
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (MC) a[s][i] = mc_read(lds_u32 + cur * STAGE + s * IMG, mca[i]);
+        else a[s][i] = kc16_frag(As + s * IMG, wm * WTM + i * 32, lane);
+      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        b[s][j] = MC ? mc_frag(Bs + s * IMGB, wn * WTN + j * 32, 0, lane)
-                     : kc16_frag(Bs + s * IMGB, wn * WTN + j * 32, lane);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (MC) b[s][j] = mc_read(lds_u32 + cur * STAGE + 3 * IMG + s * IMGB, mcb[j]);
+        else b[s][j] = kc16_frag(Bs + s * IMGB, wn * WTN + j * 32, lane);
+      }
     }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2};
     constexpr int TB[6] = {0, 1, 0, 2, 1, 0};
@@ -348,49 +378,32 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
           if (u == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
           else accs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[TA[u]][i], b[TB[u]][j], accs[i][j], 0, 0, 0);
         }
-    if constexpr (decltype(with_store)::value) {
-      store_tile(cur ^ 1);
+    store_tile(std::integral_constant<int, cur ^ 1>{});
 #pragma unroll
-      for (int q = 0; q < 6 * TM * TN; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // 3 VALU
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // 1 LDS store
-      }
+    for (int q = 0; q < 6 * TM * TN; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // 3 VALU
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // 1 LDS store
     }
     __builtin_amdgcn_s_setprio(0);
   };
 
   if (kt0 < kt1) {
-    if constexpr (true) {
-      // T14 order with unconditional staging (past the last step it re-reads step kt1-1 into
-      // the LDS buffer nobody reads again): registers hold step kt+1 while step kt computes
-      const int klast = kt1 - 1;
-      load_tile(kt0);
-      store_tile(0);
-      load_tile(min(kt0 + 1, klast));
+    // T14 order with unconditional staging (past the last step it re-reads step kt1-1 into
+    // the LDS buffer nobody reads again): registers hold step kt+1 while step kt computes
+    const int klast = kt1 - 1;
+    load_tile(kt0);
+    store_tile(std::integral_constant<int, 0>{});
+    load_tile(min(kt0 + 1, klast));
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      compute(std::integral_constant<int, 0>{});
+      load_tile(min(kt + 2, klast));
       __syncthreads();
-      for (int kt = kt0; kt < kt1; ++kt) {
-        compute(std::true_type{});
-        load_tile(min(kt + 2, klast));
-        __syncthreads();
-        cur ^= 1;
-      }
-    } else {
-      load_tile(kt0);
-      store_tile(0);
+      if (kt + 1 >= kt1) break;
+      compute(std::integral_constant<int, 1>{});
+      load_tile(min(kt + 3, klast));
       __syncthreads();
-      for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) load_tile(kt + 1);
-        compute(std::false_type{});
-        if (more) {
-          if constexpr (MC) __builtin_amdgcn_s_setprio(1);
-          store_tile(cur ^ 1);
-          if constexpr (MC) __builtin_amdgcn_s_setprio(0);
-        }
-        __syncthreads();
-        cur ^= 1;
-      }
     }
   }
 

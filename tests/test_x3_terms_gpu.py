@@ -186,3 +186,42 @@ def test_fused_bn_statistics_on_terms():
     ref = y0.double().reshape(-1, cout)
     assert rel(m1, ref.mean(0)) < 1e-5 and rel(m0, ref.mean(0)) < 1e-5
     assert rel(i1, i0) < 1e-6
+
+
+# (n, cin, h, w, cout, k, stride, pad, dil, bias): a split-K grid (few tiles), a large unsplit
+# grid with bias (VGG-like: the vector epilogue with biases), a ragged one (per-element path),
+# and the stride-2 parity data gradient
+EPI_SHAPES = [(1, 64, 9, 11, 64, 3, 1, 1, 1, True), (2, 128, 48, 64, 128, 3, 1, 1, 1, True),
+              (1, 32, 13, 17, 36, 1, 1, 0, 1, False), (2, 64, 20, 24, 128, 1, 2, 0, 1, False)]
+
+
+@pytest.mark.parametrize("shape", EPI_SHAPES, ids=[f"e{i}" for i in range(len(EPI_SHAPES))])
+def test_epilogue_term_images_equal_the_split_of_the_output(shape):
+    """Under F32X3 the _x forms' y_bf16 / dx_bf16 are the output's term images: the F32X3
+    kernels' epilogues (and split-K reduce) now write them in the same pass as the fp32 output
+    (conv_kernels.hpp epi_outb / epi_store_f32x4) instead of out_copy's pass over the finished
+    output.  Either way they must be torch's exact three-term RNE split of the fp32 output,
+    bitwise: forward with bias + ReLU (DeeplabVGG's conv, deeplab_vgg.py:34-43), forward with the
+    fused BN statistics, data gradient with the ReLU' epilogue on aux and with a residual."""
+    k = K()
+    n, cin, h, w, cout, ks, st, pd, dl, bias = shape
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(n, h, w, cin, generator=g).to(DEV)
+    wt = (torch.randn(cout, ks, ks, cin, generator=g) * 0.1).to(DEV)
+    b = torch.randn(cout, generator=g).to(DEV) if bias else None
+    geo = k.ConvGeom(cin, cout, ks, ks, st, (pd,), (dl,))
+    oh, ow = geo.out_hw(h, w)
+    y, yt = k.conv_fwd(geo, x, n, h, w, [wt], [b] if bias else None, flags=k.EPI_RELU, bf16_out=True)
+    assert yt.shape == (n, oh, ow, 3, cout)
+    assert torch.equal(yt, terms(y)), "forward bias + ReLU"
+    if not bias:
+        y2, _st = k.conv_fwd_bnstats(geo, x, n, h, w, [wt])
+        y3 = k.conv_fwd(geo, x, n, h, w, [wt])
+        assert torch.equal(y2, y3)
+    dy = torch.randn(n, oh, ow, cout, generator=g).to(DEV)
+    aux = F.relu(torch.randn(n, h, w, cin, generator=g)).to(DEV)
+    dx, dxt = k.conv_dgrad(geo, dy, n, h, w, [wt], aux=aux, flags=k.EPI_RELU_GRAD, bf16_out=True)
+    assert torch.equal(dxt, terms(dx)), "data gradient with ReLU'"
+    res = torch.randn(n, h, w, cin, generator=g).to(DEV)
+    dx2, dxt2 = k.conv_dgrad(geo, dy, n, h, w, [wt], res=res, bf16_out=True)
+    assert torch.equal(dxt2, terms(dx2)), "data gradient with residual"
