@@ -83,7 +83,7 @@ def per(ds, f):
     return mean(out)
 
 
-print(f"{'kernel':28s} {'grid':>9s} {'n':>3s} {'step us':>8s} {'alone us':>8s} {'MFMA':>6s} {'VALU':>6s} "
+print(f"{'kernel':44s} {'grid':>9s} {'n':>3s} {'step us':>8s} {'alone us':>8s} {'MFMA':>6s} {'VALU':>6s} "
       f"{'stall':>6s} {'parked':>6s} {'issue':>6s} {'valu/mf':>7s} {'lds/mf':>6s} {'bankc':>6s} {'MB/launch':>9s}")
 for (k, g) in sorted(set(trace) | set(alone), key=lambda kg: (kg[0], int(kg[1]) if kg[1].isdigit() else 0)):
     st = trace.get((k, g), [])
@@ -100,5 +100,5 @@ for (k, g) in sorted(set(trace) | set(alone), key=lambda kg: (kg[0], int(kg[1]) 
     bc = per(ds, lambda d: d["SQ_LDS_BANK_CONFLICT"] / d["SQ_LDS_IDX_ACTIVE"])
     fe = per(ds, lambda d: 2 * 1024 * d["FETCH_SIZE"])
     wr = per(ds, lambda d: 1024 * d["WRITE_SIZE"])
-    print(f"{k[:28]:28s} {g:>9s} {len(st):3d} {mean(st):8.1f} {al:8.1f} {mf:6.3f} {vb:6.3f} {wi:6.3f} {wa:6.3f} "
+    print(f"{k[:44]:44s} {g:>9s} {len(st):3d} {mean(st):8.1f} {al:8.1f} {mf:6.3f} {vb:6.3f} {wi:6.3f} {wa:6.3f} "
           f"{ai:6.3f} {vpm:7.2f} {lpm:6.2f} {bc:6.3f} {(fe + wr) / 1e6:9.1f}")
