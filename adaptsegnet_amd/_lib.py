@@ -43,6 +43,17 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class BnSumDesc(ctypes.Structure):
+    """adaptseg_bnsum_desc (include/adaptseg.h)."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("x_bf16", ctypes.c_void_p),
+        ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+        ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p), ("mask", ctypes.c_int),
+        ("partial", ctypes.c_void_p), ("partial_bytes", ctypes.c_size_t),
+    ]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_int64
@@ -70,6 +81,11 @@ _SIGS = {
     "adaptseg_conv2d_bwd_data_x": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data_xg": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight_x": [_DESC, _P, _P, _P, _P, _PP, _PP, _I, _P, _SZ, _P],
+    "adaptseg_conv2d_bnsum_tiles": [_DESC, _I, ctypes.POINTER(_I)],
+    "adaptseg_conv2d_bwd_data_bnsum": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(BnSumDesc),
+                                       ctypes.POINTER(_I), _P, _SZ, _P],
+    "adaptseg_bn_bwd_sums": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _P, _SZ,
+                             _P],
     "adaptseg_bn_fwd_train_x": [_L, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_bn_fwd_train_tiles_x": [_L, _I, _P, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I,
                                       _P],

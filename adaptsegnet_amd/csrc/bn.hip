@@ -761,9 +761,12 @@ static void bn_bwd_kernels(int64_t rows, int c, const TD *dy, typename Act<TY>::
                            const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
                            float *dx, uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight,
                            float *dbias, float *partial, float *coef, double reduce_bytes, double apply_bytes,
-                           bool dterms, const uint32_t *dbits, hipStream_t s) {
+                           bool dterms, const uint32_t *dbits, hipStream_t s, const float *sums, int sum_tiles) {
   int slot;
-  if (train) {
+  if (train && sums) {   // the reduction fused into the producing data gradient's epilogue
+    bn_bwd_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(rows, c, sum_tiles, sums, save_invstd, coef, dweight,
+                                                                   dbias);
+  } else if (train) {
     const int rqn = reduce_qn(QN, c);
     const ReducePlan r = reduce_plan(rows, c, rqn);
     timing_begin(kTBnReduceBwd, s, reduce_bytes, &slot);
@@ -789,7 +792,8 @@ template <typename TX, typename TY = TX, typename TD = float>
 int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, const TX *x, const float *weight,
                          const float *bias, const float *save_mean, const float *save_invstd, float *dx,
                          uint16_t *dx_bf16, TD *dres, int rmode, int train, float *dweight, float *dbias, void *ws,
-                         size_t ws_bytes, hipStream_t s, const uint32_t *dbits = nullptr) {
+                         size_t ws_bytes, hipStream_t s, const uint32_t *dbits = nullptr, const float *sums = nullptr,
+                         int sum_tiles = 0) {
   float *partial = reinterpret_cast<float *>(ws), *coef = nullptr;
   const double eb = sizeof(TX);   // bytes per activation element (x)
   const bool terms = std::is_same<TY, X3>::value;   // y stored as F32X3 term images
@@ -808,7 +812,7 @@ int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, co
   // dres out
   const double db = sizeof(TD);    // bytes per gradient element (dy, dres)
   const double mb = dbits ? 0.125 : 0.0;   // bytes per element of a mask bitmap
-  const double reduce_bytes = (db + eb + mb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
+  const double reduce_bytes = sums ? 0.0 : (db + eb + mb + ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c;
   const double apply_bytes = (db * (1 + (dres ? 1 : 0)) + 4.0 * (dx ? 1 : 0) + eb * (train ? 1 : 0) + mb +
                               ((rmode == 1 || rmode == 3) ? ebt : 0.0)) * rows * c +
                              (dx_bf16 ? (dterms ? 6.0 : 2.0) * rows * c : 0.0);
@@ -816,13 +820,14 @@ int bn_bwd_launch(int64_t rows, int c, const TD *dy, typename Act<TY>::ptr y, co
     if (qn == 2) {
       bn_bwd_kernels<TX, TY, 2, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
                                     train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, dbits,
-                                    s);
+                                    s, sums, sum_tiles);
       AS_CHECK_LAUNCH("bn_bwd");
       return ADAPTSEG_OK;
     }
   }
   bn_bwd_kernels<TX, TY, 1, TD>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, dbits, s);
+                                train, dweight, dbias, partial, coef, reduce_bytes, apply_bytes, dterms, dbits, s,
+                                sums, sum_tiles);
   AS_CHECK_LAUNCH("bn_bwd");
   return ADAPTSEG_OK;
 }
@@ -1058,7 +1063,8 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_
                        const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16, const float *weight,
                        const float *bias, const float *save_mean, const float *save_invstd, float *dx, uint16_t *dx_bf16,
                        float *dres, uint16_t *dres_bf16, int relu, int train, float *dweight, float *dbias, void *ws,
-                       size_t ws_bytes, adaptseg_stream_t stream, const uint32_t *dy_bits = nullptr) {
+                       size_t ws_bytes, adaptseg_stream_t stream, const uint32_t *dy_bits = nullptr,
+                       const float *sums = nullptr, int sum_tiles = 0) {
   AS_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "bn_bwd: C%%4==0 required");
   const bool xb = x_bf16 != nullptr, terms = copies_are_terms();
   AS_CHECK_ARG((dy != nullptr) != (dy_bf16 != nullptr), "bn_bwd: exactly one of dy / dy_bf16");
@@ -1084,19 +1090,19 @@ static int bn_bwd_impl(int64_t rows, int c, const float *dy, const uint16_t *dy_
   if (terms && y_bf16)
     return bn_bwd_launch<float, X3>(rows, c, dy, reinterpret_cast<const __bf16 *>(y_bf16), x, weight, bias,
                                     save_mean, save_invstd, dx, dx_bf16, dres, rmode, train, dweight, dbias, ws,
-                                    ws_bytes, s, dy_bits);
+                                    ws_bytes, s, dy_bits, sums, sum_tiles);
   if (xb || (!x && y_bf16)) {
     const __bf16 *yb = reinterpret_cast<const __bf16 *>(y_bf16), *xbb = reinterpret_cast<const __bf16 *>(x_bf16);
     if (dy_bf16)
       return bn_bwd_launch<__bf16, __bf16, __bf16>(rows, c, reinterpret_cast<const __bf16 *>(dy_bf16), yb, xbb, weight,
                                                    bias, save_mean, save_invstd, dx, dx_bf16,
                                                    reinterpret_cast<__bf16 *>(dres_bf16), rmode, train, dweight, dbias,
-                                                   ws, ws_bytes, s, dy_bits);
+                                                   ws, ws_bytes, s, dy_bits, sums, sum_tiles);
     return bn_bwd_launch<__bf16>(rows, c, dy, yb, xbb, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode,
-                                 train, dweight, dbias, ws, ws_bytes, s, dy_bits);
+                                 train, dweight, dbias, ws, ws_bytes, s, dy_bits, sums, sum_tiles);
   }
   return bn_bwd_launch<float>(rows, c, dy, y, x, weight, bias, save_mean, save_invstd, dx, dx_bf16, dres, rmode, train,
-                              dweight, dbias, ws, ws_bytes, s, dy_bits);
+                              dweight, dbias, ws, ws_bytes, s, dy_bits, sums, sum_tiles);
 }
 
 int adaptseg_bn_bwd(int64_t rows, int c, const float *dy, const float *y, const float *x, const float *weight,
@@ -1121,6 +1127,16 @@ int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_
                        size_t ws_bytes, adaptseg_stream_t stream) {
   return bn_bwd_impl(rows, c, dy, dy_bf16, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16,
                      dres, dres_bf16, relu, train, nullptr, nullptr, ws, ws_bytes, stream, dy_bits);
+}
+
+int adaptseg_bn_bwd_sums(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const uint32_t *dy_bits,
+                         const float *y, const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16,
+                         const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                         float *dx, uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu,
+                         const float *partial, int ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(partial && ntiles > 0, "bn_bwd_sums: null partial sums / ntiles %d", ntiles);
+  return bn_bwd_impl(rows, c, dy, dy_bf16, y, y_bf16, x, x_bf16, weight, bias, save_mean, save_invstd, dx, dx_bf16,
+                     dres, dres_bf16, relu, 1, nullptr, nullptr, ws, ws_bytes, stream, dy_bits, partial, ntiles);
 }
 
 int adaptseg_bn_bwd_affine(int64_t rows, int c, const float *dy, const float *y, const float *x,

@@ -1127,10 +1127,24 @@ int adaptseg_conv2d_bwd_data_x(const adaptseg_conv_desc *d, const float *dy, con
                                      ws_bytes, stream);
 }
 
-int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
-                                const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
-                                const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags,
-                                void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+}  // extern "C"
+
+namespace adaptseg {
+
+// Fused BN backward sums: the row tiles of the data-gradient plan (0: it cannot fuse them — a
+// thin / tap-GEMM / per-element / split-K / stride-2 product)
+static int bnsum_plan_tiles(const Plan &pl, const adaptseg_conv_desc *d) {
+  if (use_thin(d, ADAPTSEG_CONV_BWD_DATA) || tapgemm_eligible(d)) return 0;
+  if (!pl.fast || pl.s2 || pl.p.splits != 1 || pl.g16) return 0;   // (g16: compiled out, igemm_epilogue)
+  return (int)ceil_div(pl.p.M, plan_bm(pl));
+}
+
+// adaptseg_conv2d_bwd_data_xg, and with bs the fused BN backward sums where the final plan can
+// produce them (*bs_tiles = its row tiles, else 0)
+static int bwd_data_impl(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                         const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
+                         const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags, void *ws,
+                         size_t ws_bytes, adaptseg_stream_t stream, const adaptseg_bnsum_desc *bs, int *bs_tiles) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
   if (st) return st;
@@ -1183,10 +1197,73 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
   p.resbits = res_bits;
   p.aux = aux;
   p.flags = flags;
+  if (bs) {
+    const int nt = bnsum_plan_tiles(pl, d);
+    const bool xal = bs->x ? aligned16(bs->x) : !(reinterpret_cast<uintptr_t>(bs->x_bf16) & 7);
+    const bool cal = aligned16(bs->mean) && aligned16(bs->invstd) && (!bs->weight || aligned16(bs->weight)) &&
+                     (!bs->bias || aligned16(bs->bias));
+    if (nt > 0 && xal && cal && d->c % 4 == 0 && (size_t)2 * d->c * nt * sizeof(float) <= bs->partial_bytes) {
+      p.bs_part = bs->partial;
+      p.bs_x = bs->x;
+      p.bs_xb = reinterpret_cast<const __bf16 *>(bs->x_bf16);
+      p.bs_mean = bs->mean;
+      p.bs_is = bs->invstd;
+      p.bs_w = bs->weight;
+      p.bs_b = bs->bias;
+      p.bs_bits = bs->bits;
+      p.bs_mask = bs->mask;
+      p.bs_ntiles = nt;
+      *bs_tiles = nt;
+    }
+  }
   st = attach_wpack(pl, w_pack);
   if (st) return st;
   st = run_plan(pl, MODE_DGRAD, ws, ws_bytes, as_stream(stream));
+  if (st && bs_tiles) *bs_tiles = 0;
   return (st || !terms || fused) ? st : out_copy(dx, dx_bf16, nx, d->c, as_stream(stream));
+}
+
+}  // namespace adaptseg
+
+extern "C" {
+
+int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
+                                const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags,
+                                void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return bwd_data_impl(d, dy, dy_bf16, w, w_pack, res, res_bf16, res_bits, aux, dx, dx_bf16, flags, ws, ws_bytes,
+                       stream, nullptr, nullptr);
+}
+
+int adaptseg_conv2d_bnsum_tiles(const adaptseg_conv_desc *d, int with_copy, int *ntiles) {
+  AS_CHECK_ARG(ntiles, "conv2d_bnsum_tiles: null");
+  *ntiles = 0;
+  Plan pl;
+  int st = make_plan(d, ADAPTSEG_CONV_BWD_DATA, pl);
+  if (st) return st;
+  if (with_copy) {
+    pl.act_ext = d;   // any non-NULL: the plan with the caller's copy of dY
+    x3_terms(pl);
+  }
+  *ntiles = bnsum_plan_tiles(pl, d);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv2d_bwd_data_bnsum(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                   const float *const *w, const void *w_pack, const float *res,
+                                   const uint16_t *res_bf16, const uint32_t *res_bits, float *dx, uint16_t *dx_bf16,
+                                   int flags, const adaptseg_bnsum_desc *bs, int *ntiles, void *ws, size_t ws_bytes,
+                                   adaptseg_stream_t stream) {
+  AS_CHECK_ARG(bs && ntiles, "conv bwd_data_bnsum: null bnsum descriptor / ntiles");
+  *ntiles = 0;
+  AS_CHECK_ARG((bs->x != nullptr) != (bs->x_bf16 != nullptr), "conv bwd_data_bnsum: exactly one of x / x_bf16");
+  AS_CHECK_ARG(bs->mean && bs->invstd && bs->partial, "conv bwd_data_bnsum: null mean / invstd / partial");
+  AS_CHECK_ARG(bs->mask >= 0 && bs->mask <= 2, "conv bwd_data_bnsum: mask %d (0 none, 1 ReLU from x, 2 bitmap)",
+               bs->mask);
+  AS_CHECK_ARG(bs->mask != 2 || (bs->bits && d->c % 32 == 0),
+               "conv bwd_data_bnsum: a bitmap mask needs bits and C %% 32 == 0");
+  return bwd_data_impl(d, dy, dy_bf16, w, w_pack, res, res_bf16, res_bits, nullptr, dx, dx_bf16, flags, ws, ws_bytes,
+                       stream, bs, ntiles);
 }
 
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,

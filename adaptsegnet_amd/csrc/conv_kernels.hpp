@@ -68,6 +68,16 @@ struct ConvParams {
   int outb_terms;              //   ... or (1) its F32X3 term images [rows][3][N] (the _x forms' copies)
   float *stats;                // FWD (splits == 1, no epilogue flags): per-row-tile BN statistics
   int stats_ntiles;            //   [ntiles] counts, [N][ntiles] means, [N][ntiles] M2
+  // DGRAD (splits == 1, no parity scatter): the backward sums of the BatchNorm whose incoming
+  // gradient this output is — per row tile tm and column c, s1 = sum g', s2 = sum g' (x - mean)
+  // into bs_part[c][tm] / bs_part[N + c][tm], g' = the output value masked (bs_mask 1: ReLU of the
+  // BN output, recomputed from its input x; 2: the bitmap bs_bits [rows][N / 32]; 0: none)
+  float *bs_part;              //   NULL: none
+  const float *bs_x;           //   the BN input x [M][N]: fp32, or ...
+  const __bf16 *bs_xb;         //   ... bf16 (bf16 activation storage)
+  const float *bs_mean, *bs_is, *bs_w, *bs_b;
+  const uint32_t *bs_bits;
+  int bs_mask, bs_ntiles;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
 };
 
@@ -708,6 +718,50 @@ __device__ __forceinline__ bool has_bias(const ConvParams &p) {
   return p.bias[0] || (p.nseg > 1 && (p.bias[1] || (p.nseg > 2 && (p.bias[2] || (p.nseg > 3 && p.bias[3])))));
 }
 
+// ---- fused BatchNorm backward sums (ConvParams::bs_part) ---------------------------------
+// The BN input of four consecutive columns at element e (e % 4 == 0), stored fp32 or bf16
+__device__ __forceinline__ float4 bs_x4(const ConvParams &p, uint32_t e) {
+  if (p.bs_x) return ld_e<float4>(p.bs_x, e >> 2);
+  const uint2 u = ld_e<uint2>(p.bs_xb, e >> 2);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float bs_x1(const ConvParams &p, size_t idx) {
+  return p.bs_x ? p.bs_x[idx] : (float)p.bs_xb[idx];
+}
+// The per-channel constants of four columns: mean, invstd, weight, bias (absent affine: 1, 0)
+struct BsCol4 {
+  float4 m, is, w, b;
+};
+__device__ __forceinline__ BsCol4 bs_col4(const ConvParams &p, int col) {
+  BsCol4 c;
+  c.m = *reinterpret_cast<const float4 *>(p.bs_mean + col);
+  c.is = *reinterpret_cast<const float4 *>(p.bs_is + col);
+  c.w = p.bs_w ? *reinterpret_cast<const float4 *>(p.bs_w + col) : make_float4(1.f, 1.f, 1.f, 1.f);
+  c.b = p.bs_b ? *reinterpret_cast<const float4 *>(p.bs_b + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  return c;
+}
+// g' of one element: the output value v masked as the BN backward masks its incoming gradient —
+// mask 1: the BN's ReLU, recomputed from x with bn.hip's bn_affine expression (so the bit is the
+// forward's); 2: the bitmap bit
+__device__ __forceinline__ float bs_gate(int mask, float v, float x, float m, float is, float w, float b, uint32_t bit) {
+  if (mask == 1) return (x - m) * is * w + b > 0.f ? v : 0.f;
+  if (mask == 2) return bit ? v : 0.f;
+  return v;
+}
+// s1 += g', s2 += g' (x - mean) over four columns; bits = the mask word shifted to column 0
+__device__ __forceinline__ void bs_acc4(const ConvParams &p, const BsCol4 &c, float4 v, float4 x, uint32_t bits,
+                                        float4 &s1, float4 &s2) {
+  const int mk = p.bs_mask;
+  const float gx = bs_gate(mk, v.x, x.x, c.m.x, c.is.x, c.w.x, c.b.x, bits & 1u);
+  const float gy = bs_gate(mk, v.y, x.y, c.m.y, c.is.y, c.w.y, c.b.y, bits & 2u);
+  const float gz = bs_gate(mk, v.z, x.z, c.m.z, c.is.z, c.w.z, c.b.z, bits & 4u);
+  const float gw = bs_gate(mk, v.w, x.w, c.m.w, c.is.w, c.w.w, c.b.w, bits & 8u);
+  s1.x += gx; s1.y += gy; s1.z += gz; s1.w += gw;
+  s2.x += gx * (x.x - c.m.x); s2.y += gy * (x.y - c.m.y);
+  s2.z += gz * (x.z - c.m.z); s2.w += gw * (x.w - c.m.w);
+}
+
 // bf16-only outputs (bf16 activation / gradient storage, config c5; no bias) of a full tile: each wave
 // stages one 32x32 accumulator block at a time through its own 4.2 KB of LDS and writes rows of
 // eight bf16 per lane (16 B), reading the bf16 residual / accumulate target the same way —
@@ -773,10 +827,12 @@ __device__ __forceinline__ void epi_store_bf16x8(const ConvParams &p, const floa
 // 32x32 accumulator block at a time through its own 4.6 KB of LDS and writes rows of four fp32
 // per lane (16 B), reading the residual (+ its bitmap word) / accumulate target the same way —
 // a quarter of the per-element path's memory instructions.
+// With fused BN sums (p.bs_part) each lane also accumulates its four columns' s1 / s2 over its
+// rows; on return lanes 0..7 of the wave hold them (column chunk wn * wtn + j * 32 + 4 lane).
 template <int EK, int MODE, int TM, int TN, bool S2>
 __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const floatx16 (&acc)[TM][TN], int bm, int bn,
                                                 int wm, int wn, int wtm, int wtn, int lane, int wave, float *lds,
-                                                int Hc, int Wc, int py, int px) {
+                                                int Hc, int Wc, int py, int px, float4 (&bs1)[TN], float4 (&bs2)[TN]) {
   // output row of GEMM row `row` (S2: the parity class's pixel back in the NHWC image; a pixel's
   // channels stay contiguous, so the 16-B rows hold)
   auto orow = [&](int row) -> uint32_t {
@@ -795,9 +851,15 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
   const int rr = lane >> 3;                    // ... of rows rr + 8 h, h = 0..3
   const uint32_t N = (uint32_t)p.N;
   const int flags = p.flags;
+  // (fused BN sums on the plain store only: beside the residual / accumulate read-backs the
+  // register-staged F32X3 build, 128 VGPRs, spills; those tiles take the general path)
+  const bool bs = MODE == MODE_DGRAD && EK == EK_PLAIN && p.bs_part;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int gcol = bn + wn * wtn + j * 32 + c4;
+    bs1[j] = bs2[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    BsCol4 bc;
+    if (bs) bc = bs_col4(p, gcol);
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);   // the summed segment biases of these 4 columns
     if constexpr (MODE == MODE_FWD) {
       for (int sg = 0; sg < p.nseg; ++sg) {
@@ -821,6 +883,16 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
           const uint32_t e = orow(grow + 8 * h) * N + gcol;
           rd[h] = ld_e<float4>(src, e >> 2);
           rb[h] = (EK == EK_RES_F32 && p.resbits) ? ld_word(p.resbits, e) : ~0u;
+        }
+      }
+      float4 xv[4];   // the BN input of these rows (fused BN sums)
+      uint32_t xw[4];
+      if (bs) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t e = orow(grow + 8 * h) * N + gcol;
+          xv[h] = bs_x4(p, e);
+          xw[h] = p.bs_mask == 2 ? ld_word(p.bs_bits, e) >> (e & 31) : ~0u;
         }
       }
 #pragma unroll
@@ -850,6 +922,7 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
           v.x = epi_act_grad(v.x, rd[h].x, flags); v.y = epi_act_grad(v.y, rd[h].y, flags);
           v.z = epi_act_grad(v.z, rd[h].z, flags); v.w = epi_act_grad(v.w, rd[h].w, flags);
         }
+        if (bs) bs_acc4(p, bc, v, xv[h], xw[h], bs1[j], bs2[j]);
         if (p.out) st_e<float4>(p.out, e >> 2, v);
         if (p.outb) {   // the term images [row][3][N] (outb_terms; < 2^31 elements, the host checks)
           uint2 th, tm, tl;
@@ -863,19 +936,40 @@ __device__ __forceinline__ void epi_store_f32x4(const ConvParams &p, const float
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's staging
     }
   }
+  if (bs) {   // the 8 lanes of a column chunk (rows rr = lane >> 3) -> lanes 0..7
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        bs1[j].x += __shfl_xor(bs1[j].x, o); bs1[j].y += __shfl_xor(bs1[j].y, o);
+        bs1[j].z += __shfl_xor(bs1[j].z, o); bs1[j].w += __shfl_xor(bs1[j].w, o);
+        bs2[j].x += __shfl_xor(bs2[j].x, o); bs2[j].y += __shfl_xor(bs2[j].y, o);
+        bs2[j].z += __shfl_xor(bs2[j].z, o); bs2[j].w += __shfl_xor(bs2[j].w, o);
+      }
+  }
 }
 
 // The general store (stride-2 parity scatter, activation gradients, accumulate + residual, or
-// outputs of >= 2^30 elements): per-element read-backs.
-template <int MODE, int TM, int TN, typename ROWF>
+// outputs of >= 2^30 elements): per-element read-backs.  Fused BN sums (p.bs_part; never with the
+// parity scatter): on return lanes 0..31 hold their column's s1 / s2 over the wave's rows.
+template <int MODE, int TM, int TN, typename ROWF, bool BS = true>
 __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 (&acc)[TM][TN], int bm, int bn,
                                                   int wm, int wn, int wtm, int wtn, int hh, int l32, bool full, int M,
-                                                  ROWF out_row) {
+                                                  ROWF out_row, float (&gs1)[TN], float (&gs2)[TN]) {
   const int flags = p.flags;
+  const bool bs = BS && MODE == MODE_DGRAD && p.bs_part;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = bn + wn * wtn + j * 32 + l32;
+    gs1[j] = gs2[j] = 0.f;
     if (!full && col >= p.N) continue;
+    float bm1 = 0.f, bi1 = 0.f, bw1 = 1.f, bb1 = 0.f;
+    if (bs) {
+      bm1 = p.bs_mean[col];
+      bi1 = p.bs_is[col];
+      if (p.bs_w) bw1 = p.bs_w[col];
+      if (p.bs_b) bb1 = p.bs_b[col];
+    }
     float bsum = 0.f;
     if constexpr (MODE == MODE_FWD) {
       for (int s = 0; s < p.nseg; ++s) {
@@ -884,7 +978,20 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
       }
     }
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      // the BN input of the block's 16 rows, loaded before its first store (a store may alias it
+      // for all the compiler knows, which would serialise each load behind the previous store)
+      float xs[16];
+      uint32_t xb[16];
+      if (bs) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(bm + wm * wtm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh, M - 1);
+          const size_t idx = (size_t)row * p.N + col;
+          xs[r] = bs_x1(p, idx);
+          xb[r] = p.bs_mask == 2 ? (p.bs_bits[idx >> 5] >> (idx & 31)) & 1u : 1u;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = bm + wm * wtm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -895,9 +1002,62 @@ __device__ __forceinline__ void epi_store_general(const ConvParams &p, floatx16 
         if (flags & ADAPTSEG_EPI_RESIDUAL) v += epi_res(p, idx);
         v = epi_act(v, flags);
         if (flags & kEpiActGrad) v = epi_act_grad(v, p.aux[idx], flags);
+        if (bs) {
+          const float g = bs_gate(p.bs_mask, v, xs[r], bm1, bi1, bw1, bb1, xb[r]);
+          gs1[j] += g;
+          gs2[j] += g * (xs[r] - bm1);
+        }
         if (p.out) p.out[idx] = v;   // NULL: bf16 storage, only the copy below
         if (p.outb) epi_outb(p, out_row(row), col, v);
       }
+    }
+  }
+  if (bs) {   // lanes l32 and l32 + 32 hold the same column
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      gs1[j] += __shfl_xor(gs1[j], 32);
+      gs2[j] += __shfl_xor(gs2[j], 32);
+    }
+  }
+}
+
+// The fused BN sums of the block's row tile tm (igemm_epilogue, after the stores): each wave's
+// per-lane column sums (f32x4 layout: lanes 0..7 x 4 columns; general layout: lanes 0..31) are
+// summed over the WAVES_M waves of a column range through LDS and written to bs_part[c][tm],
+// bs_part[N + c][tm].  The LDS must be free of the stores' staging (a barrier first).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int TN>
+__device__ __forceinline__ void bs_finish(const ConvParams &p, bool vec, const float4 (&bs1)[TN],
+                                          const float4 (&bs2)[TN], const float (&gs1)[TN], const float (&gs2)[TN],
+                                          int bn, int tm, int wm, int wn, int lane, float *lds) {
+  constexpr int WTN = BN / WAVES_N;
+  float *red1 = lds, *red2 = lds + WAVES_M * BN;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = wn * WTN + j * 32;
+    if (vec) {
+      if (lane < 8) {
+        *reinterpret_cast<float4 *>(red1 + wm * BN + cl + 4 * lane) = bs1[j];
+        *reinterpret_cast<float4 *>(red2 + wm * BN + cl + 4 * lane) = bs2[j];
+      }
+    } else if (lane < 32) {
+      red1[wm * BN + cl + lane] = gs1[j];
+      red2[wm * BN + cl + lane] = gs2[j];
+    }
+  }
+  __syncthreads();
+  const int nt = p.bs_ntiles;
+  for (int c = threadIdx.x; c < BN; c += 64 * WAVES_M * WAVES_N) {
+    const int col = bn + c;
+    if (col >= p.N) continue;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < WAVES_M; ++q) {
+      s1 += red1[q * BN + c];
+      s2 += red2[q * BN + c];
+    }
+    p.bs_part[(size_t)col * nt + tm] = s1;
+    p.bs_part[((size_t)p.N + col) * nt + tm] = s2;
   }
 }
 
@@ -984,8 +1144,11 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
       else if (rf == ADAPTSEG_EPI_ACCUMULATE) ek = p.out ? EK_ACC_F32 : EK_ACC_BF16;
     }
     bool vec = false;
+    float4 bs1[TN], bs2[TN];   // fused BN sums, per lane (epi_store_f32x4 / epi_store_general)
+    float gs1[TN], gs2[TN];
     if constexpr (VEC == 1 && !S2) {
-      vec = full && !p.out && p.outb && !p.resbits && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
+      // (fused BN sums: the general path)
+      vec = full && !p.out && p.outb && !p.resbits && !p.bs_part && (p.N & 7) == 0 && (MODE != MODE_FWD || !has_bias(p)) &&
             (ek == EK_PLAIN || ek == EK_RES_BF16 || ek == EK_ACC_BF16) &&
             !(reinterpret_cast<uintptr_t>(p.outb) & 15) && (ek != EK_RES_BF16 || !(reinterpret_cast<uintptr_t>(p.resb) & 15));
       if (vec) {
@@ -1005,10 +1168,10 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
                                   (p.nseg < 3 || !p.bias[2] || !(reinterpret_cast<uintptr_t>(p.bias[2]) & 15)) &&
                                   (p.nseg < 4 || !p.bias[3] || !(reinterpret_cast<uintptr_t>(p.bias[3]) & 15)))) &&
             (ek != EK_RES_F32 || !(reinterpret_cast<uintptr_t>(p.res) & 15)) &&
-            (ek != EK_ACTGRAD || !(reinterpret_cast<uintptr_t>(p.aux) & 15));
+            (ek != EK_ACTGRAD || !(reinterpret_cast<uintptr_t>(p.aux) & 15)) && (ek == EK_PLAIN || !p.bs_part);
       if (vec) {
 #define AS_F32X4(EK_) \
-  epi_store_f32x4<EK_, MODE, TM, TN, S2>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds, Hc, Wc, py, px)
+  epi_store_f32x4<EK_, MODE, TM, TN, S2>(p, acc, bm, bn, wm, wn, WTM, WTN, lane, wave, lds, Hc, Wc, py, px, bs1, bs2)
         if (ek == EK_PLAIN) AS_F32X4(EK_PLAIN);
         else if (ek == EK_RES_F32) AS_F32X4(EK_RES_F32);
         else if (ek == EK_ACC_F32) AS_F32X4(EK_ACC_F32);
@@ -1016,7 +1179,15 @@ __device__ __forceinline__ void igemm_epilogue(const ConvParams &p, floatx16 (&a
 #undef AS_F32X4
       }
     }
-    if (!vec) epi_store_general<MODE, TM, TN>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row);
+    // (the fused BN sums are compiled out of the bf16-output LDS-DMA kernels, VEC 1: the host
+    // plans them for no such product — bnsum_plan_tiles — and they would spill the BK-32 builds)
+    constexpr bool BS = MODE == MODE_DGRAD && !S2 && VEC != 1;
+    if (!vec)
+      epi_store_general<MODE, TM, TN, decltype(out_row), BS>(p, acc, bm, bn, wm, wn, WTM, WTN, hh, l32, full, M, out_row,
+                                                              gs1, gs2);
+    if constexpr (BS) {
+      if (p.bs_part) bs_finish<BM, BN, WAVES_M, WAVES_N, TN>(p, vec, bs1, bs2, gs1, gs2, bn, tm, wm, wn, lane, lds);
+    }
     if constexpr (MODE == MODE_FWD && !S2) {
       // BatchNorm statistics of this row tile, straight from the accumulators (the BN that
       // consumes this conv then skips its statistics pass over y): per column the tile's

@@ -187,18 +187,40 @@ def bn_forward(bn, x, res, relu, training, tiles=None):
 
 
 def bn_backward(bn, dy, y, x, st, relu, dx=None, dres=None, mask_from_x=False, bf16=False, fp32=True,
-                dybits=None):
+                dybits=None, sums=None):
     """mask_from_x: a BN+ReLU without residual recomputes its ReLU mask from x in train
     mode instead of reading the saved output y (one activation read less per pass).
     bf16: return (dx, bf16 copy of dx) for the bf16-math data gradient that consumes dx.
-    dybits: a mask bitmap applied to dy first (the Bottleneck's BN3 / downsample BN)."""
+    dybits: a mask bitmap applied to dy first (the Bottleneck's BN3 / downsample BN).
+    sums: the backward sums the producing data gradient fused (bn_sums_spec), or None."""
     mean, invstd, train = st
     if not train:  # eval-mode backward needs 1/sqrt(var+eps) of the running statistics
         invstd = torch.rsqrt(bn.running_var + bn.eps)
     elif mask_from_x and relu:
         y = None
     return K.bn_bwd(dy, y, x, bn.weight, mean, invstd, relu=relu, dx=dx, dres=dres, train=train,
-                    bias=bn.bias, bf16_out=bf16, fp32_out=fp32 or not bf16, dybits=dybits)
+                    bias=bn.bias, bf16_out=bf16, fp32_out=fp32 or not bf16, dybits=dybits, sums=sums)
+
+
+# (A/B switch) the BN backward reduction of a Bottleneck's BN1 / BN2 fused into the epilogue of the
+# data gradient that produces its incoming gradient (adaptseg_conv2d_bwd_data_bnsum): the BN
+# backward then skips its pass over dy and x.  fp32 gradient storage only (the bf16-output
+# epilogue would leave its 16-B store path).  Bit 1: BN2's (conv3's data gradient), bit 2: BN1's
+# (conv2's).  Off by default: alone the fused chain is 5 % faster over the c2 shapes
+# (tools/bnsum_bench.py), in the step it is slower — c2 -0.9 / -0.8 % (BN2), -0.0 / -0.3 % (BN1),
+# -1.0 / -1.3 % (both), c3 within +-0.6 % — because the main chain then reaches the next data
+# gradient while the previous product's weight gradient still holds the CUs: the step's GEMM
+# kernel time grew 15 ms against 7 ms of BN time removed (profiles/r5/bn_sums_ab.txt).
+BN_SUMS = _switch("ADAPTSEG_BN_SUMS", 0, (0, 1, 2, 3))
+
+
+def bn_sums_spec(bn, x, st, which=3):
+    """K.BnSum of a train-mode BN+ReLU (mask recomputed from x) for conv_dgrad(bnsum=...), or None.
+    which: the BN_SUMS bit of this BN."""
+    mean, invstd, train = st
+    if not (BN_SUMS & which and train) or lowp_grads():
+        return None
+    return K.BnSum(x, mean, invstd, bn.weight, bn.bias, K.BNSUM_RELU_X)
 
 
 # ---------------------------------------------------------------------------------------
@@ -383,7 +405,9 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     else:
         r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
     dc3, dc3b = r if sh else (r, None)
-    dy2 = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg)
+    bs2 = bn_sums_spec(blk.bn2, rec.c2, rec.s2, 1)
+    r = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg, bnsum=bs2)
+    dy2, sums2 = r if bs2 is not None else (r, None)
     if need_w and blk.conv3.weight.grad is not None:
         _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
@@ -396,19 +420,21 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
         f2 = False
     r = bn_backward(blk.bn2, dy2, rec.y2b if (sh or rec.y2 is None) else rec.y2, rec.c2, rec.s2, relu=True,
                     dx=None if lg else dy2,
-                    mask_from_x=True, bf16=sh or t2, fp32=f2)
+                    mask_from_x=True, bf16=sh or t2, fp32=f2, sums=sums2)
     # BN2's output: in place over dy2, or (bf16 gradient storage) a new fp32 tensor / None
     dy2, dy2b = r if (sh or t2) else (r, None)
     if not f2:
         dy2 = None   # not written: its consumers read dy2b
-    dy1 = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b if (sh or not f2) else None,
-                       bf16_only=lg)
+    bs1 = bn_sums_spec(blk.bn1, rec.c1, rec.s1, 2)
+    r = K.conv_dgrad(g2, dy2, n, oh, ow, [blk.conv2.weight], dyb=dy2b if (sh or not f2) else None,
+                     bf16_only=lg, bnsum=bs1)
+    dy1, sums1 = r if bs1 is not None else (r, None)
     if need_w and blk.conv2.weight.grad is not None:
         _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
     r = bn_backward(blk.bn1, dy1, rec.y1b if (sh or rec.y1 is None) else rec.y1, rec.c1, rec.s1, relu=True,
                     dx=None if lg else dy1,
-                    mask_from_x=True, bf16=sh, fp32=f1)
+                    mask_from_x=True, bf16=sh, fp32=f1, sums=sums1)
     dy1, dy1b = r if sh else (r, None)
     if not f1:
         dy1 = None

@@ -277,36 +277,67 @@ def _aligned16(*ts) -> bool:
     return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
+def conv_bnsum_tiles(g: ConvGeom, n: int, h: int, w: int, with_copy: bool = False) -> int:
+    """Row tiles of the fused BN backward sums of this data gradient (0: its plan cannot fuse them)."""
+    d = _desc(g, n, h, w, nhwc_strides(n, h, w, g.cin))[0]
+    nt = ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv2d_bnsum_tiles(ctypes.byref(d), 1 if with_copy else 0, ctypes.byref(nt)),
+          "conv2d_bnsum_tiles")
+    return nt.value
+
+
+@dataclass
+class BnSum:
+    """The BN whose incoming gradient a data gradient produces (conv_dgrad ``bnsum``): its input
+    x (fp32 or bf16, [.., C]), saved mean / invstd, affine weight / bias, and the mask its
+    backward applies — BNSUM_RELU_X (ReLU recomputed from x), BNSUM_BITS (``bits``) or BNSUM_NONE."""
+    x: torch.Tensor
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    weight: torch.Tensor | None
+    bias: torch.Tensor | None
+    mask: int
+    bits: torch.Tensor | None = None
+
+
+BNSUM_NONE, BNSUM_RELU_X, BNSUM_BITS = 0, 1, 2
+
+
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, out=None,
                res=None, aux=None, flags: int = 0, dyb=None, bf16_out: bool = False, bf16_only: bool = False,
-               resbits=None):
+               resbits=None, bnsum: BnSum | None = None):
     """dx[n,h,w,cin] (+)= conv_transpose(dy, w) (+res) (*leaky'(aux), or relu'(aux) with EPI_RELU_GRAD).
     bf16_out: also return a bf16 copy of dx written by the epilogue -> (dx, dxb).
     bf16_only (or a bf16 ``out``): dx stored in bf16 only — bf16 gradient storage (BF16 maths);
     ``res`` may be fp32 or bf16 (adaptseg_conv2d_bwd_data_xg).  resbits: a mask bitmap
-    (mask_bits_like) gating res element-wise."""
-    if bf16_only or (out is not None and out.dtype == torch.bfloat16):
-        if out is None:
-            out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.bfloat16)
-        if res is not None:
-            flags |= EPI_RESIDUAL
-        if aux is not None and not flags & EPI_RELU_GRAD:   # the same gating rule as the fp32 branch
-            flags |= EPI_LEAKY_GRAD
-        wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
-        _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, None, out, (n, g.cin, h, w), _wshape(g),
-                            g.stride, g.pads, g.dils, flags)
-        return out
+    (mask_bits_like) gating res element-wise.
+    bnsum: also compute, in the epilogue, the backward sums of that BN over dx — then the result
+    is (the usual return value, (partial, ntiles) or None when the plan cannot fuse them)."""
+    low = bf16_only or (out is not None and out.dtype == torch.bfloat16)
+    dev = (dy if dy is not None else dyb).device
     if out is None:
-        out = torch.empty((n, h, w, g.cin), device=(dy if dy is not None else dyb).device, dtype=torch.float32)
+        out = torch.empty((n, h, w, g.cin), device=dev, dtype=torch.bfloat16 if low else torch.float32)
     if res is not None:
         flags |= EPI_RESIDUAL
-    if aux is not None and not flags & EPI_RELU_GRAD:
+    if aux is not None and not flags & EPI_RELU_GRAD:   # the same gating rule in both storages
         flags |= EPI_LEAKY_GRAD
-    outb = _bf16_like(out, bf16_out)
+    outb = None if low else _bf16_like(out, bf16_out)
+    dx, dxb = (None, out) if low else (out, outb)
     wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
-    _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, out, outb, (n, g.cin, h, w), _wshape(g),
-                        g.stride, g.pads, g.dils, flags)
-    return (out, outb) if bf16_out else out
+    ret = out if (low or not bf16_out) else (out, outb)
+    nt = 0
+    if bnsum is not None and aux is None:
+        nt = conv_bnsum_tiles(g, n, h, w, with_copy=dyb is not None and _aligned16(dyb))
+    if nt == 0:
+        _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, dx, dxb, (n, g.cin, h, w), _wshape(g),
+                            g.stride, g.pads, g.dils, flags)
+        return ret if bnsum is None else (ret, None)
+    partial = torch.empty(2 * g.cin * nt, device=dev, dtype=torch.float32)
+    b = bnsum
+    _OP.conv2d_bwd_data_bnsum(dy, dyb, list(weights), wp, res, resbits, dx, dxb, (n, g.cin, h, w), _wshape(g),
+                              g.stride, g.pads, g.dils, flags, b.x, b.mean, b.invstd, b.weight, b.bias, b.bits,
+                              int(b.mask), partial, nt)
+    return ret, (partial, nt)
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
@@ -388,18 +419,23 @@ def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu
 
 
 def bn_bwd(dy, y, x, weight, mean, invstd, relu=True, dx=None, dres=None, train=True, bias=None,
-           bf16_out=False, fp32_out=True, dybits=None):
+           bf16_out=False, fp32_out=True, dybits=None, sums=None):
     """dx = BN-backward(g), g = dy*[y>0] if relu; dres receives g.  dx/dres may alias dy.
     y=None with relu (train mode): the mask is recomputed from x, weight and bias.
     dybits: a mask bitmap (mask_bits_like) applied to dy first, g = dy * bit.
     bf16_out: return (dx, dxb) with a bf16 (RNE) copy of dx (a bf16-math data-gradient operand);
-    fp32_out=False (with bf16_out): only the copy is written, dx is None."""
+    fp32_out=False (with bf16_out): only the copy is written, dx is None.
+    sums: (partial, ntiles) from conv_dgrad(bnsum=...) over this dy (train mode): the reduction
+    pass is skipped."""
     if not (fp32_out or not bf16_out):
         dx = None
     elif dx is None:
         dx = torch.empty(dy.shape, device=dy.device, dtype=torch.float32)
     dxb = _bf16_like(dy, bf16_out)
-    _OP.bn_bwd(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
+    if sums is not None and train:
+        _OP.bn_bwd_sums(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), sums[0], int(sums[1]))
+    else:
+        _OP.bn_bwd(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, int(relu), bool(train))
     return (dx, dxb) if bf16_out else dx
 
 

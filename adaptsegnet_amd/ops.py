@@ -250,6 +250,39 @@ def _conv2d_bwd_data(dy, dyb, weight, wpack, res, resbits, aux, dx, dxb, in_shap
         "conv2d_bwd_data")
 
 
+@_op("conv2d_bwd_data_bnsum(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? resbits, "
+     "Tensor(a!)? dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, int[] dil, int flags, "
+     "Tensor bnx, Tensor mean, Tensor invstd, Tensor? bnw, Tensor? bnb, Tensor? bits, int mask, Tensor(c!) partial, "
+     "int ntiles) -> ()")
+def _conv2d_bwd_data_bnsum(dy, dyb, weight, wpack, res, resbits, dx, dxb, in_shape, w_shape, stride, pad, dil, flags,
+                           bnx, mean, invstd, bnw, bnb, bits, mask, partial, ntiles):
+    """conv2d_bwd_data that also writes the fused BN backward sums of its output (the BN whose
+    incoming gradient it is; adaptseg_conv2d_bwd_data_bnsum) into partial [2][Cin][ntiles]."""
+    n, c, h, w = in_shape
+    d, ws, oh, ow = _wdesc(in_shape, _nhwc_strides(n, h, w, c), w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_BWD_DATA], partial.device)
+    nx, ny = n * h * w * c, n * oh * ow * w_shape[0]
+    if partial.dtype != torch.float32 or partial.numel() != 2 * c * ntiles:
+        raise RuntimeError(f"conv2d_bwd_data_bnsum: partial must be float32 [2][{c}][{ntiles}]")
+    bs = _lib.BnSumDesc()
+    bs.x, bs.x_bf16 = _pfb(bnx, nx, "conv2d_bwd_data_bnsum bnx")
+    bs.mean, bs.invstd, bs.weight, bs.bias = _p(mean), _p(invstd), _p(bnw), _p(bnb)
+    bs.bits = _pbits(bits, nx, "conv2d_bwd_data_bnsum bits")
+    bs.mask = int(mask)
+    bs.partial = _p(partial)
+    bs.partial_bytes = partial.numel() * 4
+    nt = ctypes.c_int(0)
+    check(_lib.lib().adaptseg_conv2d_bwd_data_bnsum(
+        ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_data_bnsum dy"), _pc(dyb, ny, "conv2d_bwd_data_bnsum dyb"),
+        _ptrs(weight), _p(wpack), *_pfb(res, nx, "conv2d_bwd_data_bnsum res"),
+        _pbits(resbits, nx, "conv2d_bwd_data_bnsum resbits"), _pf(dx, nx, "conv2d_bwd_data_bnsum dx"),
+        _pc(dxb, nx, "conv2d_bwd_data_bnsum dxb"), flags, ctypes.byref(bs), ctypes.byref(nt), wp, wsz, _stream()),
+        "conv2d_bwd_data_bnsum")
+    if nt.value != ntiles:
+        raise RuntimeError(f"conv2d_bwd_data_bnsum: planned {ntiles} BN-sum tiles, the launch produced {nt.value} "
+                           f"(unaligned operand?)")
+
+
 @_op("conv2d_bwd_weight(Tensor? dy, Tensor? dyb, Tensor? x, Tensor? xb, Tensor(a!)[] dw, Tensor(b!)[] db, "
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_bwd_weight(dy, dyb, x, xb, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
@@ -342,6 +375,23 @@ def _bn_bwd(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, tr
         *_pfb(x, n, "bn_bwd x"), _p(weight), _p(bias), _p(mean), _p(invstd), _pf(dx, n, "bn_bwd dx"),
         _pc(dxb, n, "bn_bwd dxb"), *_pfb(dres, n, "bn_bwd dres"), int(act), 1 if train else 0, wp, wsz, _stream()),
         "bn_bwd")
+
+
+@_op("bn_bwd_sums(Tensor dy, Tensor? dybits, Tensor? y, Tensor? x, Tensor? weight, Tensor? bias, Tensor mean, "
+     "Tensor invstd, Tensor(a!)? dx, Tensor(c!)? dxb, Tensor(b!)? dres, int act, Tensor partial, int ntiles) -> ()")
+def _bn_bwd_sums(dy, dybits, y, x, weight, bias, mean, invstd, dx, dxb, dres, act, partial, ntiles):
+    """bn_bwd in train mode whose reduction the producing data gradient's epilogue already did
+    (conv2d_bwd_data_bnsum): adaptseg_bn_bwd_sums."""
+    rows, c = _rc(dy)
+    n = rows * c
+    if partial.dtype != torch.float32 or partial.numel() != 2 * c * ntiles:
+        raise RuntimeError(f"bn_bwd_sums: partial must be float32 [2][{c}][{ntiles}]")
+    wp, wsz = _ws_args(bn_ws_bytes(rows, c), dy.device)
+    check(_lib.lib().adaptseg_bn_bwd_sums(
+        rows, c, *_pfb(dy, n, "bn_bwd_sums dy"), _pbits(dybits, n, "bn_bwd_sums dybits"), *_pfb(y, n, "bn_bwd_sums y"),
+        *_pfb(x, n, "bn_bwd_sums x"), _p(weight), _p(bias), _p(mean), _p(invstd), _pf(dx, n, "bn_bwd_sums dx"),
+        _pc(dxb, n, "bn_bwd_sums dxb"), *_pfb(dres, n, "bn_bwd_sums dres"), int(act), _p(partial), int(ntiles), wp,
+        wsz, _stream()), "bn_bwd_sums")
 
 
 @_op("bn_bwd_affine(Tensor dy, Tensor? y, Tensor x, Tensor? weight, Tensor? bias, Tensor mean, "

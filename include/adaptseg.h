@@ -196,6 +196,36 @@ int adaptseg_conv2d_bwd_data_xg(const adaptseg_conv_desc *d, const float *dy, co
                                 const float *const *w, const void *w_pack, const float *res, const uint16_t *res_bf16,
                                 const uint32_t *res_bits, const float *aux, float *dx, uint16_t *dx_bf16, int flags,
                                 void *ws, size_t ws_bytes, adaptseg_stream_t stream);
+/* The BatchNorm backward reduction fused into the data gradient that produces the BN's incoming
+   gradient (a Bottleneck's conv3 -> bn2 and conv2 -> bn1 data gradients, the next block's conv1
+   data gradient -> bn3; model/deeplab_multi.py:83-103 under torch's batch_norm_backward): the
+   epilogue also sums, per row tile and channel, g' and g' * (x - mean), where g' is the output
+   value masked as the BN backward masks it.  adaptseg_bn_bwd_sums then skips its own reduction
+   pass over dy and x.  Replaces the separate read of dy (and the reduction launch) per BN. */
+typedef struct {
+  const float *x;          /* the BN input [rows][c] (the conv output it normalised): fp32 ...  */
+  const uint16_t *x_bf16;  /* ... or bf16 (bf16 activation storage): exactly one                 */
+  const float *mean, *invstd;      /* the forward's saved statistics (16-byte aligned)        */
+  const float *weight, *bias;      /* affine parameters (NULL: 1 / 0)                          */
+  const uint32_t *bits;    /* mask 2: bitmap [rows][c / 32] (adaptseg_bn_fwd_*_xm relu_bits)      */
+  int mask;                /* 0 none; 1 ReLU of the BN output, recomputed from x (bn_bwd's mask
+                              from x); 2 the bitmap (bn_bwd_xg's dy_bits)                       */
+  float *partial;          /* out: [2][c][ntiles] per-row-tile sums                             */
+  size_t partial_bytes;
+} adaptseg_bnsum_desc;
+/* Row tiles the fused sums of product `d` come in (0: its plan cannot fuse them — thin /
+   tap-GEMM / split-K / stride-2 / per-element products); with_copy as for bnstats_tiles_x
+   (the plan with the caller's copy of dY).  Host-side planning, no GPU. */
+int adaptseg_conv2d_bnsum_tiles(const adaptseg_conv_desc *d, int with_copy, int *ntiles);
+/* adaptseg_conv2d_bwd_data_xg (no activation-gradient epilogue) that also writes the fused sums
+   of `bs` when its final plan can (*ntiles = the row tiles written, else 0: the caller runs the
+   BN backward's own reduction).  Tiles count rows of the output; every (channel, tile) is
+   written exactly once. */
+int adaptseg_conv2d_bwd_data_bnsum(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
+                                   const float *const *w, const void *w_pack, const float *res,
+                                   const uint16_t *res_bf16, const uint32_t *res_bits, float *dx, uint16_t *dx_bf16,
+                                   int flags, const adaptseg_bnsum_desc *bs, int *ntiles, void *ws, size_t ws_bytes,
+                                   adaptseg_stream_t stream);
 /* Weight gradient with bf16 copies of BOTH operands (dY from adaptseg_bn_bwd_x, x from the
    forward's adaptseg_bn_*_x; either NULL = neither used): the LDS-DMA weight-gradient kernel
    (Cin and Cout multiples of 8) reads them; other kernels ignore them.  Exception: the
@@ -318,6 +348,15 @@ int adaptseg_bn_bwd_xg(int64_t rows, int c, const float *dy, const uint16_t *dy_
                        const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
                        float *dx, uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu, int train, void *ws,
                        size_t ws_bytes, adaptseg_stream_t stream);
+
+/* adaptseg_bn_bwd_xg in train mode with the reduction already done: `partial` [2][c][ntiles]
+   from adaptseg_conv2d_bwd_data_bnsum over this dy (same mask: relu with y == NULL <-> bnsum
+   mask 1, dy_bits <-> mask 2).  Runs the finalisation and the apply pass only. */
+int adaptseg_bn_bwd_sums(int64_t rows, int c, const float *dy, const uint16_t *dy_bf16, const uint32_t *dy_bits,
+                         const float *y, const uint16_t *y_bf16, const float *x, const uint16_t *x_bf16,
+                         const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                         float *dx, uint16_t *dx_bf16, float *dres, uint16_t *dres_bf16, int relu,
+                         const float *partial, int ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream);
 
 /* adaptseg_bn_bwd in train mode for a BN whose affine parameters are trainable (the warper's
    NaiveConvolution norms, model/custom_layers.py:25-33): additionally dbias[c] += sum(g),

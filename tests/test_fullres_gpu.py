@@ -95,6 +95,38 @@ def test_fullres_bench_batch_step_vs_oracle(geom, bn_train):
     _step_vs_oracle(geom, bn_train, "Vanilla", 1e-3, batch=BENCH_BATCH[geom])
 
 
+def test_fullres_fused_bn_sums_match_unfused(monkeypatch):
+    """engine.BN_SUMS (the BN1 / BN2 backward reductions fused into the producing data
+    gradients' epilogues) at the c2 geometry, train-mode BN, batch 1: the losses are the
+    forward's and stay bit-identical; the parameter updates differ only by the reductions'
+    summation order (every group's update cosine >= 0.9999 against the unfused step); and with
+    the switch on, the step against the fp32 oracle holds test_fullres_step_vs_oracle's bounds."""
+    from adaptsegnet_amd import engine
+    level, src, tgt = GEOMS["c2"]
+    xs, lab, xt = _batch(src, tgt)
+    runs = []
+    for mode in (0, 3):
+        monkeypatch.setattr(engine, "BN_SUMS", mode)
+        tr, m, d1, d2 = _hip_trainer(level, src, tgt, True)
+        got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()
+        runs.append((got, {k: v.detach().cpu().double() for k, v in m.state_dict().items()},
+                     {k: v.detach().cpu().double() for k, v in d2.state_dict().items()}))
+    (l0, g0, dd0), (l1, g1, dd1) = runs
+    assert l0 == l1, (l0, l1)
+    init = _sd(R.g_specs(), 1338)
+    keys = [k for k in g0 if g0[k].is_floating_point() and not k.startswith("layer5") and "running" not in k]
+    u0 = torch.cat([(g0[k] - init[k].double()).flatten() for k in keys])
+    u1 = torch.cat([(g1[k] - init[k].double()).flatten() for k in keys])
+    c = _cos(u1, u0)
+    print(f"fused BN sums: G update cosine vs unfused {c:.8f}")
+    assert c >= 0.9999, c
+    dinit = _sd(R.d_specs(), 2002)
+    cd = _cos(torch.cat([(dd1[k] - dinit[k].double()).flatten() for k in dd1]),
+              torch.cat([(dd0[k] - dinit[k].double()).flatten() for k in dd0]))
+    assert cd >= 0.9999, cd
+    _step_vs_oracle("c2", True, "Vanilla", 1e-3)
+
+
 @pytest.fixture
 def bf16_math():
     from adaptsegnet_amd import kernels as K

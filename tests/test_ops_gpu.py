@@ -547,6 +547,66 @@ def test_conv_dgrad_into_bn_relu_backward(shape, conv_math):
     assert rel(nchw(dx), xr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("mask", ["relu_x", "bits", "none"])
+@pytest.mark.parametrize("shape", [(4, 256, 64, 72, 64, 1), (2, 256, 96, 96, 256, 3), (4, 256, 75, 61, 64, 1),
+                                   (2, 64, 150, 121, 64, 3), (2, 128, 20, 18, 48, 1)],
+                         ids=["1x1", "3x3-dil2", "1x1-ragged", "3x3-c64", "1x1-small"])
+def test_conv_dgrad_fused_bn_sums(shape, mask, conv_math):
+    """The BN backward reduction fused into the data-gradient epilogue (conv_dgrad(bnsum=...),
+    adaptseg_conv2d_bwd_data_bnsum -> adaptseg_bn_bwd_sums): the data gradient is bit-identical to
+    the unfused one; the per-tile sums add up to sum g' and sum g' (x - mean) (fp64 reference,
+    g' = dx masked by the BN's ReLU recomputed from x / by the forward's bitmap / unmasked); and
+    the BN backward that consumes them matches fp64 autograd as the unfused chain does.  The
+    ragged shape ends on a partial row tile and the Cin-64 one fills half of every 128-column
+    tile (both: the per-element epilogue); a split-K plan cannot fuse (the sums come back None
+    and the unfused BN backward runs)."""
+    k = K()
+    n, cin, h, w, cout, ks = shape
+    g = torch.Generator().manual_seed(23)
+    pad = ks // 2 * (2 if ks == 3 else 1)
+    geom = k.ConvGeom(cin, cout, ks, ks, 1, (pad,), (2 if ks == 3 else 1,))
+    bx = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64) * 2 + 0.3
+    bw = torch.rand(cin, generator=g, dtype=torch.float64) + 0.5
+    bb = torch.randn(cin, generator=g, dtype=torch.float64) * 0.2
+    wt = torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) * 0.05
+    xr = bx.clone().requires_grad_(True)
+    bn_out = F.batch_norm(xr, None, None, bw, bb, True, 0.1, 1e-5)
+    a = F.relu(bn_out) if mask != "none" else bn_out
+    y = F.conv2d(a, wt, None, 1, geom.pads[0], geom.dils[0])
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    bxd = nhwc(bx)
+    bwd, bbd = bw.float().to(DEV), bb.float().to(DEV)
+    bits = k.mask_bits_like(bxd) if mask == "bits" else None
+    yfw, mean, invstd = k.bn_fwd_train(bxd, bwd, bbd, torch.zeros(cin, device=DEV), torch.ones(cin, device=DEV),
+                                       0.1, 1e-5, relu=mask != "none", ybits=bits)
+    code = {"relu_x": k.BNSUM_RELU_X, "bits": k.BNSUM_BITS, "none": k.BNSUM_NONE}[mask]
+    dyd, wd = nhwc(dy), [w_cl(wt)]
+    plain = k.conv_dgrad(geom, dyd, n, h, w, wd)
+    dx, sums = k.conv_dgrad(geom, dyd, n, h, w, wd, bnsum=k.BnSum(bxd, mean, invstd, bwd, bbd, code, bits))
+    assert torch.equal(dx, plain)
+    split = k.conv_kernel_id(geom, n, h, w, 1)[1] > 1
+    assert (sums is None) == split
+    if sums is not None:
+        part, nt = sums
+        assert nt == k.conv_bnsum_tiles(geom, n, h, w)
+        s = part.view(2, cin, nt).double().sum(-1).cpu()
+        gd = dx.double().cpu().reshape(-1, cin)
+        xd = bxd.double().cpu().reshape(-1, cin)
+        m64 = mean.double().cpu()
+        if mask == "relu_x":
+            gd = torch.where(yfw.reshape(-1, cin).cpu() > 0, gd, 0.0)   # the forward's ReLU decision
+        elif mask == "bits":
+            word = bits.cpu().reshape(-1, cin // 32).long() & 0xffffffff
+            bit = (word.repeat_interleave(32, dim=1) >> torch.arange(cin).remainder(32)) & 1
+            gd = gd * bit
+        assert rel(s[0], gd.sum(0)) < 1e-5
+        assert rel(s[1], (gd * (xd - m64)).sum(0)) < 1e-5
+    relu = mask == "relu_x"
+    k.bn_bwd(dx, None, bxd, bwd, mean, invstd, relu=relu, dx=dx, bias=bbd, dybits=bits, sums=sums)
+    assert rel(nchw(dx), xr.grad) < 1e-4
+
+
 @pytest.mark.parametrize("size_average", [True, False])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_crossentropy2d_module(size_average, weighted):
