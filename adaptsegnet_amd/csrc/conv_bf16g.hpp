@@ -40,6 +40,12 @@ __device__ __forceinline__ void glds16(const void *src, uint32_t lds_dst) {
 }
 
 constexpr int kG16Stages = 3;
+
+// s_waitcnt vmcnt(N): this wave's LDS-DMA loads but the last N have landed
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 constexpr int g16_stage_bytes(int bm, int bn, int bk) { return (bm + bn) * bk * 2; }
 
 // Byte offset of 16-B chunk ch of row r in a K-contiguous image of BK bf16 per row.  BK 64:
@@ -277,10 +283,11 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
 // tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
 // KB, two blocks per CU.  BN 256 (with BM 256): two B images, 8 waves of 64x128, a 3 x 32 KB ring
 // and one block per CU — half the operand bytes per MFMA of 256x128.
-template <int BM, int BN = 128>
-__global__ void __launch_bounds__(512, BN == 256 ? 1 : 2) igemm_bf16g_wgrad_kernel(const ConvParams p,
-                                                                                   const __bf16 *__restrict__ dyb,
-                                                                                   const __bf16 *__restrict__ xb) {
+// NS: LDS ring depth, NS - 1 K steps in flight across each barrier (3: 2; the 256x128 tile runs
+// one block per CU under the 256-block split target, so a 6-deep ring, 144 KB, fits too).
+template <int BM, int BN = 128, int NS = kG16Stages>
+__global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16g_wgrad_kernel(
+    const ConvParams p, const __bf16 *__restrict__ dyb, const __bf16 *__restrict__ xb) {
   constexpr int BKP = 32;
   static_assert(BN == 128 || (BN == 256 && BM == 256), "wgrad tiles 128x128, 256x128, 256x256");
   constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
@@ -289,8 +296,9 @@ __global__ void __launch_bounds__(512, BN == 256 ? 1 : 2) igemm_bf16g_wgrad_kern
   constexpr int NB = BN / 128;                // B images
   constexpr int IMG = BKP * 256;              // one [32 k][128] bf16 image
   constexpr int STAGE = (NA + NB) * IMG;
+  static_assert(NS >= 3 && NS * STAGE <= 160 * 1024, "ring depth");
 
-  __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -382,21 +390,22 @@ __global__ void __launch_bounds__(512, BN == 256 ? 1 : 2) igemm_bf16g_wgrad_kern
   };
 
   if (kt0 < kt1) {
+    // step kt lives in stage (kt - kt0) % NS; steps past the last re-read it into stages nobody
+    // reads again, so every wave always has NS - 2 steps' NA + NB instructions outstanding
     const int klast = kt1 - 1;
-    issue(kt0, 0);
-    issue(min(kt0 + 1, klast), 1);
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i) issue(min(kt0 + i, klast), i);
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
-      // step kt landed, step kt+1's NA + NB instructions in flight
-      static_assert(NA + NB >= 2 && NA + NB <= 4, "vmcnt below counts 2-4 instructions per step");
-      if constexpr (NA + NB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if constexpr (NA + NB == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      // step kt landed (steps kt+1 .. kt+NS-2 in flight) ...
+      wait_vmcnt<(NS - 2) * (NA + NB)>();
+      // ... in every wave after the barrier, which also retires every wave's reads of step kt-1's
+      // stage, the one step kt+NS-1 overwrites
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");   // no LDS access moves above the barrier
-      issue(min(kt + 2, klast), st == 0 ? 2 : st - 1);
+      issue(min(kt + NS - 1, klast), st == 0 ? NS - 1 : st - 1);
       compute(st);
-      st = st == 2 ? 0 : st + 1;
+      st = st == NS - 1 ? 0 : st + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

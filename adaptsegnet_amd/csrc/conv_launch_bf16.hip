@@ -193,6 +193,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(
                                              base + al256(g16_act_elems(pl) * sizeof(__bf16)));
+      // (a 6-deep ring for the 256x128 tile, 4-deep for 128x128 — five / three steps in flight
+      // instead of two: per shape within +-3 %, c5 -0.6 %, profiles/r5/g16_wgrad_ring_ab.txt)
       if (pl.g16_bm == 256) igemm_bf16g_wgrad_kernel<256><<<grid, block, 0, s>>>(p, act, act2);
       else igemm_bf16g_wgrad_kernel<128><<<grid, block, 0, s>>>(p, act, act2);
       return hipGetLastError();
