@@ -72,6 +72,12 @@ class StepConfig:
     # does: c2 +1.3 %, c3 +1.1 %, c5 +3.6 % (profiles/r5/overlap_ab.txt) — off for DeeplabVGG
     # (c4 -0.6 %).
     overlap_domains: bool | str = "auto"
+    # with overlap_domains: enqueue the target forward BEFORE the source backward, so its kernels
+    # are in the side stream's queue when the backward starts instead of after the host has
+    # issued the whole backward (≈1,000 launches); same kernels, same inputs, bit-identical.
+    # Off: within ±0.6 % at c2 / c3 / c5 (profiles/r5/target_first_ab.txt) — the host already
+    # runs far enough ahead of the GPU
+    target_first: bool = False
     # run the discriminator step (its forwards on the detached predictions and its backwards,
     # train:435-461 / 642-679) on its own HIP stream as soon as the target forward is done, beside
     # the step's last generator backward: it reads only the detached predictions and D's weights
@@ -381,14 +387,22 @@ class AdaptSegTrainer:
         pred2 = self._pred_single(images, c.input_size, flow)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         ov = self._overlap_begin(pred2.device)
+
+        def target_forward():
+            with self._target_ctx(ov):
+                pt2 = self._pred_single(images_t, tsize, None if flow is None else flow.detach())
+                return pt2, F.adv_loss(D2(F.softmax2d(pt2)), 0.0, self.kind)
+
+        first = ov is not None and c.target_first
+        if first:
+            pred_target2, loss_adv_target2 = target_forward()
         self._backward([loss_seg2], [inv])
         L.add("loss_seg2", loss_seg2, inv)
+        if not first:
+            pred_target2, loss_adv_target2 = target_forward()
 
         with self._target_ctx(ov):
-            pred_target2 = self._pred_single(images_t, tsize, None if flow is None else flow.detach())
-            d_out2 = D2(F.softmax2d(pred_target2))
-            loss_adv_target2 = F.adv_loss(d_out2, 0.0, self.kind)
-            dev_ = d_out2.device
+            dev_ = loss_adv_target2.device
             dfork = self._d_fork(dev_)
             self._join_source(ov)
             if g_done is not None:
@@ -419,17 +433,24 @@ class AdaptSegTrainer:
         loss_seg1 = F.cross_entropy2d(pred1, labels, c.ignore_label)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         ov = self._overlap_begin(pred2.device)
+
+        def target_forward():
+            with self._target_ctx(ov):
+                pt1, pt2 = self.model(images_t, tsize)
+                return (pt1, pt2, F.adv_loss(D1(F.softmax2d(pt1)), 0.0, self.kind),
+                        F.adv_loss(D2(F.softmax2d(pt2)), 0.0, self.kind))
+
+        first = ov is not None and c.target_first
+        if first:
+            pred_target1, pred_target2, loss_adv1, loss_adv2 = target_forward()
         self._backward([loss_seg2, loss_seg1], [inv, c.lambda_seg * inv])
         L.add("loss_seg1", loss_seg1, inv)
         L.add("loss_seg2", loss_seg2, inv)
+        if not first:
+            pred_target1, pred_target2, loss_adv1, loss_adv2 = target_forward()
 
         with self._target_ctx(ov):
-            pred_target1, pred_target2 = self.model(images_t, tsize)
-            d_out1 = D1(F.softmax2d(pred_target1))
-            d_out2 = D2(F.softmax2d(pred_target2))
-            loss_adv1 = F.adv_loss(d_out1, 0.0, self.kind)
-            loss_adv2 = F.adv_loss(d_out2, 0.0, self.kind)
-            dev_ = d_out2.device
+            dev_ = loss_adv2.device
             dfork = self._d_fork(dev_)
             self._join_source(ov)
             if g_done is not None:

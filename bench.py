@@ -320,6 +320,9 @@ def main():
     ap.add_argument("--overlap-d", action="store_true",
                     help="run the discriminator step on its own stream beside the last generator "
                          "backward (StepConfig.overlap_d)")
+    ap.add_argument("--target-first", action="store_true",
+                    help="with the domain overlap, enqueue the target forward before the source "
+                         "backward (StepConfig.target_first)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path with several ranks on one GPU)")
@@ -357,7 +360,7 @@ def main():
     model.train()
     scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
                       overlap_domains={"auto": "auto", "on": True, "off": False}[args.overlap],
-                      overlap_d=args.overlap_d)
+                      overlap_d=args.overlap_d, target_first=args.target_first)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
@@ -456,6 +459,7 @@ def main():
                    "conv_math": conv_math,
                    "switches": engine.switches(),
                    "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
+                   "target_first": bool(scfg.target_first),
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across
