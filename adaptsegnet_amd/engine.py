@@ -743,6 +743,11 @@ def discriminator_forward(model, x):
 # weight gradients run on the term-image kernel (conv_x3r.hpp); 2 the forwards and data gradients
 # read them too
 VGG_TERMS = _switch("ADAPTSEG_VGG_TERMS", 0, (0, 1, 2))
+# ... only for tensors of at least this many channels (the term images of a conv's input need
+# Cin, of its output gradient Cout >= it): the wide late layers, where the term-image kernel's
+# weight gradient is 1.5-1.7x the staged one (profiles/r5/conv_shapes_c4_presplit.txt), without
+# the 6-B-per-element term copies of the 64- / 128-channel layers at 512x1024 / 256x512
+VGG_TERMS_MIN_C = _switch("ADAPTSEG_VGG_TERMS_MIN_C", 0, (0, 256, 512, 1024))
 
 
 def vgg_terms() -> int:
@@ -762,7 +767,7 @@ class _DeeplabVGGFn(torch.autograd.Function):
         for i, (conv, pool) in enumerate(prog):
             g = conv.geom()
             # the next conv's input terms: from this conv's epilogue, or from the pool after it
-            want_t = vt > 0 and save and i + 1 < len(prog) and g.cout % 8 == 0
+            want_t = vt > 0 and save and i + 1 < len(prog) and g.cout % 8 == 0 and g.cout >= VGG_TERMS_MIN_C
             out = K.conv_fwd(g, cur, n, ch, cw, [conv.weight], [conv.bias], strides=cs,
                              flags=K.EPI_RELU, xb=curt if vt >= 2 else None, bf16_out=want_t and not pool)
             outt = None
@@ -837,7 +842,7 @@ class _DeeplabVGGFn(torch.autograd.Function):
                 prev_pool = acts[i - 1][4]
                 # the previous conv's output-gradient terms: from this data gradient's epilogue,
                 # or from the pool's backward
-                want_t = vt > 0 and i - 1 > 0 and geo.cin % 8 == 0
+                want_t = vt > 0 and i - 1 > 0 and geo.cin % 8 == 0 and geo.cin >= VGG_TERMS_MIN_C
                 r = K.conv_dgrad(geo, g, n, ih, iw, [conv.weight], aux=xin, flags=K.EPI_RELU_GRAD,
                                  dyb=gt if vt >= 2 else None, bf16_out=want_t and prev_pool is None)
                 g, gt = r if (want_t and prev_pool is None) else (r, None)

@@ -87,15 +87,22 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
     def vgg_pass(wh):
         w, h = wh
         st = (3 * h * w, h * w, w, 1)
-        for i, (conv, pool) in enumerate(model.conv_program()):
+        # the term images engine._DeeplabVGGFn makes (engine.VGG_TERMS / VGG_TERMS_MIN_C): conv i's
+        # input terms when its Cin qualifies, its output-gradient terms when its Cout does (the
+        # last conv's always, from the classifier's data gradient)
+        vt, thr = engine.vgg_terms(), engine.VGG_TERMS_MIN_C
+        prog = model.conv_program()
+        for i, (conv, pool) in enumerate(prog):
             g = conv.geom()
-            add(g, batch, h, w, 0, st)
+            xt = vt > 0 and i > 0 and g.cin % 8 == 0 and g.cin >= thr
+            dt = vt > 0 and (i == len(prog) - 1 or (i > 0 and g.cout % 8 == 0 and g.cout >= thr))
+            add(g, batch, h, w, 0, st, terms=vt >= 2 and xt)
             if i > 0:
-                add(g, batch, h, w, 1)
+                add(g, batch, h, w, 1, terms=vt >= 2 and dt)
             if g.cin % 4:   # conv1_1: weight gradient on the 4-channel padded input
                 add(dataclasses.replace(g, cin=4), batch, h, w, 2, (4 * h * w, 1, 4 * w, 4), algo=g)
             else:
-                add(g, batch, h, w, 2, st)
+                add(g, batch, h, w, 2, st, terms=xt and dt)
             h, w = g.out_hw(h, w)
             if pool:
                 h, w = h // 2, w // 2

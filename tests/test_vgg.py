@@ -46,12 +46,14 @@ def _frob(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["fp32", "wgrad-terms", "all-terms"])
+@pytest.fixture(params=[(0, 0), (1, 0), (2, 0), (2, 512)], ids=["fp32", "wgrad-terms", "all-terms", "all-terms-c512"])
 def vgg_terms(request, monkeypatch):
     """engine.VGG_TERMS: the VGG program on fp32 operands, with its weight gradients on the
-    term-image kernel, or with every product reading term images."""
+    term-image kernel, or with every product reading term images — for every layer, or only
+    where the tensors have >= 512 channels (engine.VGG_TERMS_MIN_C)."""
     from adaptsegnet_amd import engine
-    monkeypatch.setattr(engine, "VGG_TERMS", request.param)
+    monkeypatch.setattr(engine, "VGG_TERMS", request.param[0])
+    monkeypatch.setattr(engine, "VGG_TERMS_MIN_C", request.param[1])
     return request.param
 
 
