@@ -82,6 +82,7 @@ _SIGS = {
     "adaptseg_conv2d_bwd_data_xg": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight_x": [_DESC, _P, _P, _P, _P, _PP, _PP, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bnsum_tiles": [_DESC, _I, ctypes.POINTER(_I)],
+    "adaptseg_timing_reserve": [_L],
     "adaptseg_conv2d_bwd_data_bnsum": [_DESC, _P, _P, _PP, _P, _P, _P, _P, _P, _P, _I, ctypes.POINTER(BnSumDesc),
                                        ctypes.POINTER(_I), _P, _SZ, _P],
     "adaptseg_bn_bwd_sums": [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _P, _SZ,

@@ -464,7 +464,10 @@ void set_splits(Plan &pl) {
   // short BN / split-K kernels then wait for CU slots.  384 measured c2 +2.4 %, c3 +2.6 %
   // (256 / 320 / 448 / 1024: +1.2 / +1.7 / +2.0 / +0.1 % at c2).  Rounding the split count to
   // nearest instead of down measured -0.2..-0.8 % (profiles/r3/x3_wgrad_split_rounding_ab.txt).
-  constexpr int kX3WgradTarget = 384;
+#ifndef ADAPTSEG_X3_WGRAD_TARGET
+#define ADAPTSEG_X3_WGRAD_TARGET 384   // (a compile-time knob of experiment builds, EXTRA=-D...)
+#endif
+  constexpr int kX3WgradTarget = ADAPTSEG_X3_WGRAD_TARGET;
   // The LDS-DMA bf16 weight gradient (side stream) to ~256 blocks: half the split-K slab
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
@@ -483,8 +486,11 @@ void set_splits(Plan &pl) {
     // (MFMA busy 0.315 in isolation), s = 7 runs 4 rounds of 1/7 (0.57 of the s = 1 time).
     // (Round 4 capped s at 16: the 1x1 weight gradients, 1-8 tiles over K = 32-131k pixels, then
     // ran 16-128 blocks on 256 CUs — layer1 at 4-33 TF/s, layer3's 1x1 at 107-112.)
+#ifndef ADAPTSEG_X3R_WGRAD_MIN_KSTEPS
+#define ADAPTSEG_X3R_WGRAD_MIN_KSTEPS 32
+#endif
     double best = 1e30;
-    for (int s = 1; s <= 256 && (s == 1 || nkt / s >= 32); ++s) {
+    for (int s = 1; s <= 256 && (s == 1 || nkt / s >= ADAPTSEG_X3R_WGRAD_MIN_KSTEPS); ++s) {
       const double t = (double)ceil_div((int64_t)pl.tiles * s, 256) / s;
       if (t < best * 0.97) {
         best = t;
@@ -1360,6 +1366,26 @@ int adaptseg_timing_enable(int enable, int selector) {
   g_timing.enabled = enable != 0;
   g_timing.selector = selector;
   if (enable) g_timing.used = 0;  // disabling keeps the recorded launches readable
+  return ADAPTSEG_OK;
+}
+
+// Create event pairs up front (outside a timed region): a pair created on demand inside one — the
+// pool ran out when the timed steps launch the roofline kernel more often than the untimed
+// all-kernel step did — cost milliseconds each (c4 with its term-image data gradient as the
+// roofline kernel: 195 -> 347 ms per step, profiles/r5/vgg_terms_thr_ab.txt)
+int adaptseg_timing_reserve(int64_t pairs) {
+  AS_CHECK_ARG(pairs >= 0 && pairs <= (1 << 20), "timing_reserve: bad count %lld", (long long)pairs);
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  while ((int64_t)g_timing.events.size() < pairs) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      set_error("timing_reserve: hipEventCreate failed");
+      return ADAPTSEG_ERR_HIP;
+    }
+    g_timing.events.push_back({a, b});
+    g_timing.flops.push_back(0.0);
+    g_timing.ids.push_back(0);
+  }
   return ADAPTSEG_OK;
 }
 

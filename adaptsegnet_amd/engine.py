@@ -742,12 +742,14 @@ def discriminator_forward(model, x):
 # every conv output gradient's term images are made (the conv epilogues' / pools' copies) and the
 # weight gradients run on the term-image kernel (conv_x3r.hpp); 2 the forwards and data gradients
 # read them too
-VGG_TERMS = _switch("ADAPTSEG_VGG_TERMS", 0, (0, 1, 2))
+VGG_TERMS = _switch("ADAPTSEG_VGG_TERMS", 2, (0, 1, 2))
 # ... only for tensors of at least this many channels (the term images of a conv's input need
 # Cin, of its output gradient Cout >= it): the wide late layers, where the term-image kernel's
 # weight gradient is 1.5-1.7x the staged one (profiles/r5/conv_shapes_c4_presplit.txt), without
-# the 6-B-per-element term copies of the 64- / 128-channel layers at 512x1024 / 256x512
-VGG_TERMS_MIN_C = _switch("ADAPTSEG_VGG_TERMS_MIN_C", 0, (0, 256, 512, 1024))
+# the 6-B-per-element term copies of the 64- / 128-channel layers at 512x1024 / 256x512.  Same
+# box (profiles/r5/vgg_terms_thr_ab.txt): mode 2 at >= 512 channels +1.1 % (41.73 / 41.63 vs
+# 41.31 / 41.14 images/s), at >= 1024 +0.7 %, at >= 256 -0.9 %; mode 1 -5 %
+VGG_TERMS_MIN_C = _switch("ADAPTSEG_VGG_TERMS_MIN_C", 512, (0, 256, 512, 1024))
 
 
 def vgg_terms() -> int:

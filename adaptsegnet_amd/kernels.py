@@ -674,6 +674,11 @@ MEM_KERNELS = {1000: "upsample_fwd_kernel", 1001: "upsample_bwd_{x,y}_kernel", 1
                1015: "splitk_reduce{4}_kernel"}
 
 
+def timing_reserve(pairs: int):
+    """Create ``pairs`` timing event pairs now (outside the timed region)."""
+    check(_lib.lib().adaptseg_timing_reserve(int(pairs)), "timing_reserve")
+
+
 def timing_enable_mem(enable: bool = True):
     """Record every HBM-bound interp / loss / BN-apply launch with its algorithmic bytes."""
     check(_lib.lib().adaptseg_timing_enable_mem(1 if enable else 0), "timing_enable_mem")

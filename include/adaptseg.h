@@ -540,6 +540,9 @@ int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream)
 /* ------------------------------------------------------------------------------------ */
 int adaptseg_timing_enable(int enable, int selector);
 int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launches);
+/* Create `pairs` event pairs now, so a timed region records into existing events (creating one
+   inside it costs milliseconds). */
+int adaptseg_timing_reserve(int64_t pairs);
 /* HBM-bound kernels (the interp / loss / BN passes): when enabled, every launch of upsample
    fwd (id 1000) / bwd (1001), softmax fwd (1002) / bwd (1003), cross-entropy fwd (1004) / bwd
    (1005), BN apply (1006) / backward apply (1007), the warper's up2_relu_cat fwd (1008) / bwd
