@@ -17,15 +17,16 @@ root, sym = sys.argv[1], sys.argv[2]
 
 
 def mangled_key(name):
-    """'k<1, 128, 256>' -> 'kILi1ELi128ELi256E': rocprofv3 leaves symbols with bf16 (DF16b)
-    parameters mangled, so an integer-argument template is also matched in that form."""
+    """'k<1, 128, 256>' -> 'kILi1ELi128ELi256EE' ('false' -> Lb0E): rocprofv3 leaves symbols
+    with bf16 (DF16b) parameters mangled, so an int / bool template is also matched in that form."""
     if "<" not in name:
         return None
     base, args = name.split("<", 1)
     parts = [a.strip() for a in args.rstrip(">").split(",")]
-    if not all(a.lstrip("-").isdigit() for a in parts):
+    enc = {"false": "Lb0E", "true": "Lb1E"}
+    if not all(a.lstrip("-").isdigit() or a in enc for a in parts):
         return None
-    return base + "I" + "".join(f"Li{a}E" for a in parts) + "E"
+    return base + "I" + "".join(enc.get(a, f"Li{a}E") for a in parts) + "E"
 
 
 MKEY = mangled_key(sym)
