@@ -419,7 +419,12 @@ static void x3_terms_flags(Plan &pl) {
   // weight gradients under the default maths run on the side stream beside the main chain's
   // register-staged blocks: the 128-row tile (96 KB LDS, <= 128 VGPRs) leaves a CU room for one
   // of them, the 256-row one (144 KB) does not
-  if (pl.mode == MODE_WGRAD && conv_math() == ADAPTSEG_MATH_F32X3) pl.x3r_bm = 128;
+#ifndef ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT
+#define ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT 0   // 0: always the 128-row tile under F32X3
+#endif
+  if (pl.mode == MODE_WGRAD && conv_math() == ADAPTSEG_MATH_F32X3 &&
+      !(ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT > 0 && pl.p.M >= ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT))
+    pl.x3r_bm = 128;
 }
 static void x3_terms(Plan &pl) {
   if (!copies_are_terms() || !pl.fast || !pl.x3 || !pl.x3r_ok || !pl.act_ext) return;
