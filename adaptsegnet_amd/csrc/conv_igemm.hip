@@ -418,9 +418,11 @@ static void x3_terms_flags(Plan &pl) {
   pl.x3g = pl.x3r = pl.x3ext = true;
   // weight gradients under the default maths run on the side stream beside the main chain's
   // register-staged blocks: the 128-row tile (96 KB LDS, <= 128 VGPRs) leaves a CU room for one
-  // of them, the 256-row one (144 KB) does not
+  // of them, the 256-row one (144 KB) does not — except for Cout >= 1024 (DeeplabVGG's fc6 / fc7,
+  // whose main chain runs on the term-image kernel too): there the 256-row tile halves the dY
+  // re-reads, c4 +0.4 % over three alternating pairs (profiles/r5/x3r_wgrad_bm256_ab.txt)
 #ifndef ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT
-#define ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT 0   // 0: always the 128-row tile under F32X3
+#define ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT 1024   // 0: always the 128-row tile under F32X3
 #endif
   if (pl.mode == MODE_WGRAD && conv_math() == ADAPTSEG_MATH_F32X3 &&
       !(ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT > 0 && pl.p.M >= ADAPTSEG_X3R_WGRAD_BM256_MIN_COUT))
