@@ -156,3 +156,29 @@ def test_bf16_operand_abi_checks_on_host():
         assert st == 1
     finally:
         K.set_conv_math(K.MATH_F32X3)
+
+
+def test_fused_bn_sum_planning_on_host():
+    """adaptseg_conv2d_bnsum_tiles (host planning, no GPU): the fused BN backward sums come in one
+    partial per output row tile of the data-gradient plan — 128-row tiles on the register-staged
+    F32X3 kernel, 256 on the term-image one (with dY's copy) — and none where the plan cannot fuse
+    them (a stride-2 parity-class product, a thin one); adaptseg_conv2d_bwd_data_bnsum rejects a
+    descriptor without its partial buffer before any launch, and adaptseg_timing_reserve rejects
+    a negative count."""
+    from adaptsegnet_amd import kernels as K
+    L = _lib.lib()
+    g1 = K.ConvGeom(256, 64, 1, 1, 1)
+    n, h, w = 4, 64, 72
+    assert K.conv_bnsum_tiles(g1, n, h, w) == -(-n * h * w // 128)
+    g3 = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
+    assert K.conv_bnsum_tiles(g3, 2, 96, 96, with_copy=True) == -(-2 * 96 * 96 // 256)
+    assert K.conv_bnsum_tiles(K.ConvGeom(64, 128, 3, 3, 2, (1,), (1,)), 2, 64, 64) == 0   # parity classes
+    assert K.conv_bnsum_tiles(K.ConvGeom(64, 2, 3, 3, 1, (1,), (1,)), 2, 32, 32) == 0     # thin (Cout 2)
+    d = K._desc(g1, n, h, w, K.nhwc_strides(n, h, w, g1.cin))[0]
+    bs = _lib.BnSumDesc()
+    nt = ctypes.c_int(-1)
+    assert L.adaptseg_conv2d_bwd_data_bnsum(ctypes.byref(d), None, None, None, None, None, None, None, None, None, 0,
+                                            ctypes.byref(bs), ctypes.byref(nt), None, 0, None) == 1
+    assert nt.value == 0 and b"x / x_bf16" in L.adaptseg_last_error()
+    assert L.adaptseg_timing_reserve(-1) == 1
+    assert L.adaptseg_timing_reserve(0) == 0
