@@ -259,9 +259,10 @@ def x3_forward_terms(g) -> bool:
 
 
 # (A/B switch) 0: conv2 backward on fp32 operands; 1: its weight gradient on term images (y1's
-# from the forward, dY's from BN2's backward); 2 (default): its data gradient too.  (Mode 3,
-# conv3's backward on term images too, measured -0.6..-0.9 %: experiments/r4_conv3_terms.patch.)
-X3_BWD_TERMS = _switch("ADAPTSEG_X3_BWD_TERMS", 2, (0, 1, 2))
+# from the forward, dY's from BN2's backward); 2 (default): its data gradient too; 3: conv3's data
+# and weight gradients too (dY3's terms from BN3's backward, y2's from BN2's forward) — parity
+# green, measured c2 -0.7 %, c3 -1.0 % (profiles/r5/x3_conv3_terms_ab.txt; round 4: -0.6..-0.9 %)
+X3_BWD_TERMS = _switch("ADAPTSEG_X3_BWD_TERMS", 2, (0, 1, 2, 3))
 
 
 def block_input_fp32(blk, n, h, w) -> bool:
@@ -307,7 +308,10 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2,
                                fp32=not thin1 and need1)
     c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
-    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh, fp32=not thin2)
+    # conv3's backward on term images (X3_BWD_TERMS 3): BN2 also writes y2's terms for its weight
+    # gradient (the forward still reads the fp32 y2)
+    terms3 = not sh and save and X3_BWD_TERMS >= 3 and x3_forward_terms(g2) and g3.cin % 32 == 0
+    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh or terms3, fp32=not thin2)
     c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
     cd = sd = None
     if blk.downsample is not None:
@@ -334,6 +338,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
         rec.xb, rec.y1b, rec.y2b = xb, y1b if (sh or keep1) else None, y2b
+        if terms3:
+            rec.y2 = None   # the backward reads y2's terms (weight gradient, eval-mode mask)
         if sh and bits3 is None:
             rec.out = outb   # bf16 storage: the BN3 backward's mask source is the bf16 output
     return out, rec, outb
@@ -400,11 +406,14 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     # is still wanted (f*: a consumer without a bf16-operand kernel) writes it to its own buffer
     lg = lowp_grads()
     bits = rec.bits3
+    t3 = not sh and rec.y2b is not None   # F32X3: conv3's backward on term images (X3_BWD_TERMS 3)
+    if t3:
+        f3 = False
     if bits is not None:   # g = gout * bit: BN3's input gradient; the residual gradient stays implicit
-        r = bn_backward(blk.bn3, gout, None, rec.c3, rec.s3, relu=False, dybits=bits, bf16=sh, fp32=f3)
+        r = bn_backward(blk.bn3, gout, None, rec.c3, rec.s3, relu=False, dybits=bits, bf16=sh or t3, fp32=f3)
     else:
-        r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh, fp32=f3)
-    dc3, dc3b = r if sh else (r, None)
+        r = bn_backward(blk.bn3, gout, rec.out, rec.c3, rec.s3, relu=True, dres=gout, bf16=sh or t3, fp32=f3)
+    dc3, dc3b = r if (sh or t3) else (r, None)
     bs2 = bn_sums_spec(blk.bn2, rec.c2, rec.s2, 1)
     r = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg, bnsum=bs2)
     dy2, sums2 = r if bs2 is not None else (r, None)

@@ -140,8 +140,12 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
                     add(conv.geom(), batch, ch, cw, 0, cp=xcp, terms=fwd_terms)
                     if backward and (li < 4 or "l6" in heads_bwd):
                         # engine.block_backward: conv2's backward on term images (X3_BWD_TERMS)
-                        add(conv.geom(), batch, ch, cw, 1, cp=True, terms=fwd_terms and engine.X3_BWD_TERMS >= 2)
-                        add(conv.geom(), batch, ch, cw, 2, cp=xcp, terms=fwd_terms and engine.X3_BWD_TERMS >= 1)
+                        c3t = (conv is blk.conv3 and not copies and engine.X3_BWD_TERMS >= 3 and
+                               engine.x3_forward_terms(blk.conv2.geom()) and conv.geom().cin % 32 == 0)
+                        add(conv.geom(), batch, ch, cw, 1, cp=True,
+                            terms=(fwd_terms and engine.X3_BWD_TERMS >= 2) or c3t)
+                        add(conv.geom(), batch, ch, cw, 2, cp=xcp,
+                            terms=(fwd_terms and engine.X3_BWD_TERMS >= 1) or c3t)
                 h, w = oh, ow
         g6 = engine.aspp_geom(model.layer6)
         add(g6, batch, h, w, 0)
