@@ -662,9 +662,63 @@ def deeplab_multi_forward(model, x, input_size):
 # ---------------------------------------------------------------------------------------
 
 
+class DiscForward:
+    """A discriminator forward kept for a second backward.  The reference runs D twice on the
+    same target prediction with the same weights (train_gta2cityscapes_multi.py:423 / :617-618
+    for the generator's adversarial loss, :454 / :665-666 for D's own step — D's optimiser steps
+    only after both): the second forward recomputes the first bit for bit, so its activations are kept from
+    the first (``discriminator_forward(..., keep=)``) and ``discriminator_replay`` returns the
+    same output as a new autograd node whose backward yields D's weight gradients."""
+    __slots__ = ("acts", "actsb", "dims", "n", "out")
+
+    def __init__(self):
+        self.acts = self.actsb = self.dims = self.n = self.out = None
+
+    def tensors(self):
+        """Every tensor the replay reads (for record_stream across the step's streams)."""
+        ts = [t for t in (self.acts or ()) if t is not None] + [t for t in (self.actsb or ()) if t is not None]
+        return ts + ([self.out] if self.out is not None else [])
+
+
+def _disc_backward(model, acts, actsb, dims, n, gout, need_w, need_dx):
+    """The FCDiscriminator backward over saved activations (``acts`` / ``actsb`` are released
+    as it goes).  Returns the input gradient (NCHW) when ``need_dx``."""
+    convs = model._convs()
+    sh = lowp_storage()   # (F32X3 term images would cost the D convs a separate copy pass)
+    if need_w:
+        model._arena.claim(model._pidx["all"])
+    g = K.nhwc_view(gout)
+    if not g.is_contiguous():
+        g = g.contiguous()
+    ws = WgradStream(g.device) if need_w else None
+    dx, gb = None, None
+    for i in reversed(range(len(convs))):
+        conv = convs[i]
+        geo = conv.geom()
+        ch, cw, cs = dims[i]
+        if need_w and conv.weight.grad is not None:
+            if geo.cin % 4:   # D.conv1 (Cin 19): on a 20-channel padded copy
+                _wgrad_padded(ws, geo, g, acts[i], n, ch, cw, conv.weight.grad, conv.bias.grad)
+            else:
+                _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
+                       strides=cs, dyb=gb, xb=actsb[i])
+        if i > 0:
+            # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
+            ph, pw, _ = dims[i - 1]
+            nb = sh and _copy_pays(convs[i - 1].geom(), n, ph, pw, (1, 2) if need_w else (1,))
+            r = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i], dyb=gb, bf16_out=nb)
+            g, gb = r if nb else (r, None)
+        elif need_dx:
+            dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], dyb=gb))
+        acts[i] = actsb[i] = None
+    if ws is not None:
+        ws.join()
+    return dx
+
+
 class _FCDiscriminatorFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, x, model, save):
+    def forward(ctx, anchor, x, model, save, keep=None):
         ctx.set_materialize_grads(False)
         convs = model._convs()
         n, c, h, w = x.shape
@@ -685,58 +739,63 @@ class _FCDiscriminatorFn(torch.autograd.Function):
             cur, curb = out if nb else (out, None)
             ch, cw = oh, ow
             cs = K.nhwc_strides(n, ch, cw, g.cout)
+        y = K.as_nchw(cur)
         if save:
             ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n = model, acts, actsb, dims, n
             ctx.need_w = anchor.requires_grad
-        return K.as_nchw(cur)
+        if keep is not None:   # (own lists: this node's backward releases its entries)
+            keep.acts, keep.actsb, keep.dims, keep.n = list(acts), list(actsb), dims, n
+            keep.out = y.detach()   # (no reference to the generator's graph through y's grad_fn)
+        return y
 
     @staticmethod
     def backward(ctx, gout):
         if gout is None:
-            return None, None, None, None
-        model, acts, actsb, dims, n = ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n
-        convs = model._convs()
-        sh = lowp_storage()   # (F32X3 term images would cost the D convs a separate copy pass)
-        need_w = ctx.need_w
-        if need_w:
-            model._arena.claim(model._pidx["all"])
-        g = K.nhwc_view(gout)
-        if not g.is_contiguous():
-            g = g.contiguous()
-        ws = WgradStream(g.device) if need_w else None
-        dx, gb = None, None
-        for i in reversed(range(len(convs))):
-            conv = convs[i]
-            geo = conv.geom()
-            ch, cw, cs = dims[i]
-            if need_w and conv.weight.grad is not None:
-                if geo.cin % 4:   # D.conv1 (Cin 19): on a 20-channel padded copy
-                    _wgrad_padded(ws, geo, g, acts[i], n, ch, cw, conv.weight.grad, conv.bias.grad)
-                else:
-                    _wgrad(ws, geo, g, acts[i], n, ch, cw, [conv.weight.grad], [conv.bias.grad],
-                           strides=cs, dyb=gb, xb=actsb[i])
-            if i > 0:
-                # grad wrt the previous layer's pre-activation: dgrad * leaky'(act)
-                ph, pw, _ = dims[i - 1]
-                nb = sh and _copy_pays(convs[i - 1].geom(), n, ph, pw, (1, 2) if need_w else (1,))
-                r = K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], aux=acts[i], dyb=gb, bf16_out=nb)
-                g, gb = r if nb else (r, None)
-            elif ctx.needs_input_grad[1]:
-                dx = K.as_nchw(K.conv_dgrad(geo, g, n, ch, cw, [conv.weight], dyb=gb))
-            acts[i] = actsb[i] = None
-        if ws is not None:
-            ws.join()
-        return None, dx, None, None
+            return None, None, None, None, None
+        dx = _disc_backward(ctx.model, ctx.acts, ctx.actsb, ctx.dims, ctx.n, gout, ctx.need_w,
+                            ctx.needs_input_grad[1])
+        return None, dx, None, None, None
 
 
-def discriminator_forward(model, x):
+class _DiscReplayFn(torch.autograd.Function):
+    """The kept forward's output again, as a node whose backward is D's weight gradients."""
+
+    @staticmethod
+    def forward(ctx, anchor, model, keep):
+        ctx.set_materialize_grads(False)
+        ctx.model, ctx.keep = model, keep
+        return keep.out.clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        keep = ctx.keep
+        if gout is not None:
+            _disc_backward(ctx.model, keep.acts, keep.actsb, keep.dims, keep.n, gout, True, False)
+        keep.acts = keep.actsb = keep.out = None
+        return None, None, None
+
+
+def discriminator_forward(model, x, keep=None):
+    """FCDiscriminator.forward(x) (model/discriminator.py:27-34) on the HIP engine.  ``keep``: a
+    DiscForward that receives this forward's activations for ``discriminator_replay``."""
     if not x.is_cuda:
         raise RuntimeError("adaptsegnet_amd FCDiscriminator runs on the HIP engine only; "
                            f"got input on {x.device}")
     model._ensure_arena(x.device)
     need_w = any(p.requires_grad for p in model._arena.params)
     grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
-    return _FCDiscriminatorFn.apply(model._anchors[need_w], x, model, grad)
+    return _FCDiscriminatorFn.apply(model._anchors[need_w], x, model, grad, keep)
+
+
+def discriminator_replay(model, keep):
+    """The output of the forward ``keep`` holds, bit-identical to running D again on the same
+    input with the same weights, whose backward accumulates D's weight gradients (D's parameters
+    must require grad by then)."""
+    if keep is None or keep.out is None:
+        raise RuntimeError("discriminator_replay: no kept forward (or it was replayed already)")
+    if not all(p.requires_grad for p in model._arena.params):
+        raise RuntimeError("discriminator_replay: D's parameters do not require grad")
+    return _DiscReplayFn.apply(model._anchors[True], model, keep)
 
 
 # ---------------------------------------------------------------------------------------

@@ -40,6 +40,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
+from . import engine
 from . import functional as F
 from . import kernels as K
 from .optim import SGD, Adam, lr_poly
@@ -85,6 +86,10 @@ class StepConfig:
     # does not touch (D's parameters are frozen while its graph is built).  Results are
     # bit-identical to the sequential order (tests/test_model_gpu.py).
     overlap_d: bool = False
+    # D's own step on the target prediction reuses the forward the generator's adversarial loss
+    # ran (same input, same weights: bit-identical, engine.DiscForward) instead of running D and
+    # its softmax again — one D forward per discriminator and step fewer
+    d_reuse: bool = True
     # data parallel: size of the generator's gradient all-reduce buckets (DeeplabMulti); 0 =
     # one all-reduce of the whole arena after its last backward
     bucket_mb: float = 32.0
@@ -212,6 +217,23 @@ class AdaptSegTrainer:
         main.wait_stream(side)
         for t in tensors:
             t.record_stream(main)   # produced on the side stream, read on the main stream
+
+    def _d_keep(self, D):
+        """A DiscForward to keep D's target forward in (d_reuse, HIP-engine discriminators)."""
+        return engine.DiscForward() if self.cfg.d_reuse and hasattr(D, "_convs") else None
+
+    @staticmethod
+    def _d_out(D, x, keep):
+        return D(x) if keep is None else engine.discriminator_forward(D, x, keep=keep)
+
+    @staticmethod
+    def _d_again(D, pred, keep):
+        """D on the detached target prediction for D's own step: the kept forward when there is one."""
+        return D(F.softmax2d(pred)) if keep is None else engine.discriminator_replay(D, keep)
+
+    @staticmethod
+    def _kept(*keeps):
+        return [t for k in keeps if k is not None for t in k.tensors()]
 
     def _backward(self, losses, scales):
         dev = losses[0].device
@@ -387,11 +409,12 @@ class AdaptSegTrainer:
         pred2 = self._pred_single(images, c.input_size, flow)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         ov = self._overlap_begin(pred2.device)
+        keep2 = self._d_keep(D2)
 
         def target_forward():
             with self._target_ctx(ov):
                 pt2 = self._pred_single(images_t, tsize, None if flow is None else flow.detach())
-                return pt2, F.adv_loss(D2(F.softmax2d(pt2)), 0.0, self.kind)
+                return pt2, F.adv_loss(self._d_out(D2, F.softmax2d(pt2), keep2), 0.0, self.kind)
 
         first = ov is not None and c.target_first
         if first:
@@ -411,16 +434,16 @@ class AdaptSegTrainer:
             L.add("loss_adv_target2", loss_adv_target2, inv)
             if g_done is not None:
                 g_done.end()
-        self._overlap_end(ov, pred_target2, loss_adv_target2)
+        self._overlap_end(ov, pred_target2, loss_adv_target2, *self._kept(keep2))
 
         self._set_requires_grad(D2, True)
         pred2 = pred2.detach()
         pred_target2 = pred_target2.detach()
-        with self._d_ctx(dfork, dev_, pred2, pred_target2):
+        with self._d_ctx(dfork, dev_, pred2, pred_target2, *self._kept(keep2)):
             loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
             self._backward([loss_d2], [inv / 2])
             L.add("loss_D2", loss_d2, inv / 2)
-            loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+            loss_d2 = F.adv_loss(self._d_again(D2, pred_target2, keep2), 1.0, self.kind)
             self._backward([loss_d2], [inv / 2])
             L.add("loss_D2", loss_d2, inv / 2)
 
@@ -433,12 +456,13 @@ class AdaptSegTrainer:
         loss_seg1 = F.cross_entropy2d(pred1, labels, c.ignore_label)
         loss_seg2 = F.cross_entropy2d(pred2, labels, c.ignore_label)
         ov = self._overlap_begin(pred2.device)
+        keep1, keep2 = self._d_keep(D1), self._d_keep(D2)
 
         def target_forward():
             with self._target_ctx(ov):
                 pt1, pt2 = self.model(images_t, tsize)
-                return (pt1, pt2, F.adv_loss(D1(F.softmax2d(pt1)), 0.0, self.kind),
-                        F.adv_loss(D2(F.softmax2d(pt2)), 0.0, self.kind))
+                return (pt1, pt2, F.adv_loss(self._d_out(D1, F.softmax2d(pt1), keep1), 0.0, self.kind),
+                        F.adv_loss(self._d_out(D2, F.softmax2d(pt2), keep2), 0.0, self.kind))
 
         first = ov is not None and c.target_first
         if first:
@@ -461,21 +485,21 @@ class AdaptSegTrainer:
             L.add("loss_adv_target2", loss_adv2, inv)
             if g_done is not None:
                 g_done.end()
-        self._overlap_end(ov, pred_target1, pred_target2, loss_adv1, loss_adv2)
+        self._overlap_end(ov, pred_target1, pred_target2, loss_adv1, loss_adv2, *self._kept(keep1, keep2))
 
         self._set_requires_grad(D1, True)
         self._set_requires_grad(D2, True)
         pred1, pred2 = pred1.detach(), pred2.detach()
         pred_target1, pred_target2 = pred_target1.detach(), pred_target2.detach()
-        with self._d_ctx(dfork, dev_, pred1, pred2, pred_target1, pred_target2):
+        with self._d_ctx(dfork, dev_, pred1, pred2, pred_target1, pred_target2, *self._kept(keep1, keep2)):
             loss_d1 = F.adv_loss(D1(F.softmax2d(pred1)), 0.0, self.kind)
             loss_d2 = F.adv_loss(D2(F.softmax2d(pred2)), 0.0, self.kind)
             self._backward([loss_d1], [inv / 2])
             self._backward([loss_d2], [inv / 2])
             L.add("loss_D1", loss_d1, inv / 2)
             L.add("loss_D2", loss_d2, inv / 2)
-            loss_d1 = F.adv_loss(D1(F.softmax2d(pred_target1)), 1.0, self.kind)
-            loss_d2 = F.adv_loss(D2(F.softmax2d(pred_target2)), 1.0, self.kind)
+            loss_d1 = F.adv_loss(self._d_again(D1, pred_target1, keep1), 1.0, self.kind)
+            loss_d2 = F.adv_loss(self._d_again(D2, pred_target2, keep2), 1.0, self.kind)
             self._backward([loss_d1], [inv / 2])
             self._backward([loss_d2], [inv / 2])
             L.add("loss_D1", loss_d1, inv / 2)

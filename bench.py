@@ -56,12 +56,13 @@ CONFIGS = {
 }
 
 
-def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None, nbytes=None):
+def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None, nbytes=None, d_reuse=True):
     """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector.  ``products``
     (a set), when given, also collects every (op, selector, split-K?) the step launches
     (host-side planning only: tests/test_conv_coverage.py runs it without a GPU).  ``nbytes``
     (a dict), when given, receives each selector's algorithmic HBM bytes per step: every
-    operand read once and the output written once, fp32 (4 B; bf16 math 2 B) per element."""
+    operand read once and the output written once, fp32 (4 B; bf16 math 2 B) per element.
+    ``d_reuse``: StepConfig.d_reuse — D's own step on the target reuses the adversarial forward."""
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd import engine
     inv = {}
@@ -153,18 +154,20 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
             add(g6, batch, h, w, 1)
             add(g6, batch, h, w, 2)
 
-    def d_pass(wh, dgrad_input, wgrad):
+    def d_pass(wh, dgrad_input, wgrad, forward=True):
         w, h = wh
         for i, conv in enumerate(D._convs()):
             g = conv.geom()
             if i == 0:   # Cin 19; weight gradient on a 20-channel padded copy (engine._wgrad_padded)
-                add(g, batch, h, w, 0, (19 * h * w, 1, w * 19, 19))
+                if forward:
+                    add(g, batch, h, w, 0, (19 * h * w, 1, w * 19, 19))
                 if dgrad_input:
                     add(g, batch, h, w, 1)
                 if wgrad:
                     add(dataclasses.replace(g, cin=20), batch, h, w, 2, (20 * h * w, 1, w * 20, 20), algo=g)
             else:
-                add(g, batch, h, w, 0)
+                if forward:
+                    add(g, batch, h, w, 0)
                 add(g, batch, h, w, 1)
                 if wgrad:
                     add(g, batch, h, w, 2)
@@ -177,7 +180,7 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
     for _ in range(nD):
         d_pass(tsize, True, False)        # G step through the frozen D
         d_pass(src_wh, False, True)       # D step, source
-        d_pass(tsize, False, True)        # D step, target
+        d_pass(tsize, False, True, not d_reuse)   # D step, target (d_reuse: the G step's forward)
     return inv
 
 
@@ -331,6 +334,9 @@ def main():
     ap.add_argument("--overlap-d", action="store_true",
                     help="run the discriminator step on its own stream beside the last generator "
                          "backward (StepConfig.overlap_d)")
+    ap.add_argument("--no-d-reuse", action="store_true",
+                    help="run D again on the target prediction for its own step instead of reusing "
+                         "the adversarial forward (StepConfig.d_reuse off)")
     ap.add_argument("--target-first", action="store_true",
                     help="with the domain overlap, enqueue the target forward before the source "
                          "backward (StepConfig.target_first)")
@@ -371,7 +377,8 @@ def main():
     model.train()
     scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
                       overlap_domains={"auto": "auto", "on": True, "off": False}[args.overlap],
-                      overlap_d=args.overlap_d, target_first=args.target_first)
+                      overlap_d=args.overlap_d, target_first=args.target_first,
+                      d_reuse=not args.no_d_reuse)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
@@ -388,7 +395,7 @@ def main():
     torch.cuda.synchronize()
 
     inv_bytes = {}
-    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes)
+    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes, d_reuse=scfg.d_reuse)
     step_flops = sum(inv.values())
     # the roofline kernel: the conv symbol with the most measured kernel time per step (below);
     # without the untimed timing step (--no-roofline) the one with the most algorithmic FLOPs
@@ -473,7 +480,7 @@ def main():
                    "conv_math": conv_math,
                    "switches": engine.switches(),
                    "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
-                   "target_first": bool(scfg.target_first),
+                   "target_first": bool(scfg.target_first), "d_reuse": bool(scfg.d_reuse),
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across

@@ -248,8 +248,9 @@ def test_domain_overlap_is_bit_identical(data, level, gan):
     """StepConfig.overlap_domains (target-domain pass on a second stream, overlapping the
     source backward) and StepConfig.overlap_d (the discriminator step on its own stream beside
     the last generator backward), alone and together, and the target forward enqueued before the
-    source backward (StepConfig.target_first), with iter_size 1 and 2, must not change a single
-    bit of the losses or parameters against the sequential order."""
+    source backward (StepConfig.target_first), and D's own step reusing the adversarial forward
+    on the target (StepConfig.d_reuse), with iter_size 1 and 2, must not change a single bit of
+    the losses or parameters against the sequential order that runs every D forward."""
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
     xs, lab, xt = data
     batch = (xs.float().to(DEV), lab.to(DEV), xt.float().to(DEV))
@@ -259,19 +260,21 @@ def test_domain_overlap_is_bit_identical(data, level, gan):
     for iters in (1, 2):
         cfg = dict(level=level, gan=gan, input_size=(57, 41), input_size_target=(49, 33), iter_size=iters)
         runs = []
-        for ov, od, tf in ((False, False, False), (True, False, False), (False, True, False), (True, True, False),
-                           (True, False, True)):
+        for ov, od, tf, dr in ((False, False, False, False), (False, False, False, True), (True, False, False, True),
+                               (False, True, False, True), (True, True, False, True), (True, False, True, True),
+                               (True, True, False, False)):
             m, d1, d2 = build_g(), build_d(2001), build_d(2002)
             m.train()
             tr = AdaptSegTrainer(m, d1 if level == "multi-level" else None, d2,
-                                 StepConfig(**cfg, overlap_domains=ov, overlap_d=od, target_first=tf))
+                                 StepConfig(**cfg, overlap_domains=ov, overlap_d=od, target_first=tf, d_reuse=dr))
             subs = [batch, batch2][:iters]
             losses = [tr.step(it, subs).values() for it in range(2)]
             torch.cuda.synchronize()
             runs.append((losses, [{k: v.detach().cpu().clone() for k, v in mm.state_dict().items()}
                                   for mm in (m, d1, d2)]))
         (l0, s0) = runs[0]
-        for (l1, s1), tag in zip(runs[1:], ("overlap_domains", "overlap_d", "both", "target_first")):
+        for (l1, s1), tag in zip(runs[1:], ("d_reuse", "overlap_domains", "overlap_d", "both", "target_first",
+                                            "both, no d_reuse")):
             assert l0 == l1, (tag, iters, l0, l1)
             for a, b in zip(s0, s1):
                 for k in a:
