@@ -515,7 +515,7 @@ def _input_strides(x):
 
 class _DeeplabMultiFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, x, model, out_h, out_w, save):
+    def forward(ctx, anchor, x, model, out_h, out_w, save, first_head=True):
         ctx.set_materialize_grads(False)
         training = model.training
         n, c, h, w = x.shape
@@ -542,7 +542,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             ch, cw = nh, nw
         p3, h3, w3 = cur, ch, cw
         p3b = curb
-        x1 = aspp_forward(model.layer5, p3, n, h3, w3, xb=p3b)
+        x1 = aspp_forward(model.layer5, p3, n, h3, w3, xb=p3b) if first_head else None
         q, qb = p3, p3b
         recs4 = []
         n4 = len(model.layer4)
@@ -553,7 +553,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             recs4.append(rec)
         del curb
         x2 = aspp_forward(model.layer6, q, n, h3, w3, xb=qb)
-        x1_up = K.upsample_fwd(x1, out_h, out_w)
+        x1_up = K.upsample_fwd(x1, out_h, out_w) if first_head else None
         x2_up = K.upsample_fwd(x2, out_h, out_w)
         if save:
             ctx.model = model
@@ -565,7 +565,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             ctx.p3, ctx.q = p3, q
             ctx.p3b, ctx.qb = p3b, qb   # bf16 copies for the classifiers' weight gradients (or None)
             ctx.need_w = anchor.requires_grad
-        return K.as_nchw(x1_up), K.as_nchw(x2_up)
+        return (K.as_nchw(x1_up) if first_head else None), K.as_nchw(x2_up)
 
     @staticmethod
     def backward(ctx, g1_up, g2_up):
@@ -614,7 +614,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             done(None)
             if ws is not None:
                 ws.join()
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         blocks = [b for layer in (model.layer1, model.layer2, model.layer3) for b in layer]
         g = gp3
         for i in reversed(range(len(blocks))):
@@ -639,11 +639,12 @@ class _DeeplabMultiFn(torch.autograd.Function):
         ctx.x = None
         if ws is not None:
             ws.join()
-        return None, dx, None, None, None, None
+        return None, dx, None, None, None, None, None
 
 
-def deeplab_multi_forward(model, x, input_size):
-    """ResNetMulti.forward(x, input_size) (model/deeplab_multi.py:174-194) on the HIP engine."""
+def deeplab_multi_forward(model, x, input_size, first_head=True):
+    """ResNetMulti.forward(x, input_size) (model/deeplab_multi.py:174-194) on the HIP engine.
+    ``first_head=False``: layer5's head (ASPP + upsample) is skipped, its output None."""
     if not x.is_cuda:
         raise RuntimeError("adaptsegnet_amd DeeplabMulti runs on the HIP engine only; "
                            f"got input on {x.device}")
@@ -654,7 +655,7 @@ def deeplab_multi_forward(model, x, input_size):
     grad = torch.is_grad_enabled() and (need_w or x.requires_grad)
     anchor = model._anchors[need_w]
     out_w, out_h = int(input_size[0]), int(input_size[1])
-    return _DeeplabMultiFn.apply(anchor, x, model, out_h, out_w, grad)
+    return _DeeplabMultiFn.apply(anchor, x, model, out_h, out_w, grad, bool(first_head))
 
 
 # ---------------------------------------------------------------------------------------

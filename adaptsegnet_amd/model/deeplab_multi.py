@@ -227,10 +227,16 @@ class ResNetMulti(nn.Module):
     def arena(self) -> ParamArena:
         return self._arena
 
-    def forward(self, x, input_size=None, warper=None):
+    # (the trainer's single-level step asks for the second head only)
+    second_head_only_ok = True
+
+    def forward(self, x, input_size=None, warper=None, first_head=True):
+        """``first_head=False``: the layer5 head is not computed and its output is None — for
+        callers that discard it (the single-level step's ``_, pred2 = model(...)``,
+        train_gta2cityscapes_multi.py:405 / :421): pred2 is the same bit for bit."""
         if input_size is None:
             input_size = (x.shape[3], x.shape[2])
-        x1_up, x2_up = engine.deeplab_multi_forward(self, x, input_size)
+        x1_up, x2_up = engine.deeplab_multi_forward(self, x, input_size, first_head=first_head)
         if warper is not None:   # :190-192: both upsampled heads warped by the same field
             x1_up, x2_up = engine.grid_warp(warper, x1_up, x2_up)
         return x1_up, x2_up

@@ -90,6 +90,9 @@ class StepConfig:
     # ran (same input, same weights: bit-identical, engine.DiscForward) instead of running D and
     # its softmax again — one D forward per discriminator and step fewer
     d_reuse: bool = True
+    # single-level: DeeplabMulti computes only the head the step uses (the reference's
+    # ``_, pred2 = model(...)`` discards layer5's; ResNetMulti.forward(first_head=False))
+    second_head_only: bool = True
     # data parallel: size of the generator's gradient all-reduce buckets (DeeplabMulti); 0 =
     # one all-reduce of the whole arena after its last backward
     bucket_mb: float = 32.0
@@ -384,6 +387,8 @@ class AdaptSegTrainer:
         caller-side ``interp``."""
         if getattr(self.model, "single_output", False):
             return F.interp(self.model(images), (size[1], size[0]))
+        if self.cfg.second_head_only and getattr(self.model, "second_head_only_ok", False):
+            return self.model(images, size, flow, first_head=False)[1]
         return self.model(images, size, flow)[1]
 
     def _flow(self, images):

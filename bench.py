@@ -56,13 +56,15 @@ CONFIGS = {
 }
 
 
-def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None, nbytes=None, d_reuse=True):
+def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None, nbytes=None, d_reuse=True,
+                   first_head=False):
     """Algorithmic conv FLOPs of one step, keyed by igemm kernel selector.  ``products``
     (a set), when given, also collects every (op, selector, split-K?) the step launches
     (host-side planning only: tests/test_conv_coverage.py runs it without a GPU).  ``nbytes``
     (a dict), when given, receives each selector's algorithmic HBM bytes per step: every
     operand read once and the output written once, fp32 (4 B; bf16 math 2 B) per element.
-    ``d_reuse``: StepConfig.d_reuse — D's own step on the target reuses the adversarial forward."""
+    ``d_reuse``: StepConfig.d_reuse — D's own step on the target reuses the adversarial forward.
+    ``first_head``: single-level with the discarded layer5 head computed (second_head_only off)."""
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd import engine
     inv = {}
@@ -123,7 +125,7 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
         h, w = gs.out_hw(h, w)
         h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
         for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4), 1):
-            if li == 4:
+            if li == 4 and ("l5" in heads_bwd or first_head):   # (single-level: layer5 not computed)
                 g5 = engine.aspp_geom(model.layer5)
                 add(g5, batch, h, w, 0)
                 if backward and "l5" in heads_bwd:
@@ -337,6 +339,8 @@ def main():
     ap.add_argument("--no-d-reuse", action="store_true",
                     help="run D again on the target prediction for its own step instead of reusing "
                          "the adversarial forward (StepConfig.d_reuse off)")
+    ap.add_argument("--both-heads", action="store_true",
+                    help="single-level: compute the discarded first head too (StepConfig.second_head_only off)")
     ap.add_argument("--target-first", action="store_true",
                     help="with the domain overlap, enqueue the target forward before the source "
                          "backward (StepConfig.target_first)")
@@ -378,7 +382,7 @@ def main():
     scfg = StepConfig(level=level, gan=gan, input_size=src_wh, input_size_target=tgt_wh,
                       overlap_domains={"auto": "auto", "on": True, "off": False}[args.overlap],
                       overlap_d=args.overlap_d, target_first=args.target_first,
-                      d_reuse=not args.no_d_reuse)
+                      d_reuse=not args.no_d_reuse, second_head_only=not args.both_heads)
     trainer = AdaptSegTrainer(model, D1, D2, scfg)
     tsize = trainer._target_size()
 
@@ -395,7 +399,8 @@ def main():
     torch.cuda.synchronize()
 
     inv_bytes = {}
-    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes, d_reuse=scfg.d_reuse)
+    inv = conv_inventory(model, D2, level, batch, src_wh, tgt_wh, tsize, nbytes=inv_bytes, d_reuse=scfg.d_reuse,
+                         first_head=not scfg.second_head_only)
     step_flops = sum(inv.values())
     # the roofline kernel: the conv symbol with the most measured kernel time per step (below);
     # without the untimed timing step (--no-roofline) the one with the most algorithmic FLOPs
@@ -481,6 +486,7 @@ def main():
                    "switches": engine.switches(),
                    "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
                    "target_first": bool(scfg.target_first), "d_reuse": bool(scfg.d_reuse),
+                   "second_head_only": bool(scfg.second_head_only),
                    # algorithmic conv FLOPs / step time / (n_gpu x peak)
                    "step_conv_frac_of_peak": step_flops / (ms_per_step / 1e3) / 1e12 / peak,
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across

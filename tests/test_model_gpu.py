@@ -121,6 +121,29 @@ def test_deeplab_input_grad_and_single_head(data):
     assert frob(xd.grad, xr.grad)[0] < 5e-3
 
 
+@pytest.mark.parametrize("train", [False, True])
+def test_second_head_only_is_bit_identical(data, train):
+    """first_head=False (the single-level step, which discards pred1): pred1 is None and pred2,
+    every gradient it produces and the BN running statistics are the same bit for bit."""
+    xs, _, _ = data
+    outs = []
+    for first in (True, False):
+        m = build_g()
+        m.train(train)
+        xd = xs.float().to(DEV).requires_grad_(True)
+        p1, p2 = m(xd, (57, 41), first_head=first)
+        assert (p1 is None) == (not first)
+        (p2 * torch.linspace(-1, 1, p2.numel(), device=DEV).view_as(p2)).sum().backward()
+        torch.cuda.synchronize()
+        outs.append((p2.detach().cpu(), xd.grad.cpu(),
+                     {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                     {k: p.grad.cpu().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    (a2, ax, asd, ag), (b2, bx, bsd, bg) = outs
+    assert torch.equal(a2, b2) and torch.equal(ax, bx)
+    assert asd.keys() == bsd.keys() and all(torch.equal(asd[k], bsd[k]) for k in asd)
+    assert ag.keys() == bg.keys() and all(torch.equal(ag[k], bg[k]) for k in ag)
+
+
 def test_discriminator(data):
     D = R.to_torch(R.det_state(R.d_specs(), 2001), trainable=lambda k: True)
     g = torch.Generator().manual_seed(3)
