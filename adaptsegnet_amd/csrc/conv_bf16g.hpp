@@ -283,8 +283,7 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
 // tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
 // KB, two blocks per CU.  BN 256 (with BM 256): two B images, 8 waves of 64x128, a 3 x 32 KB ring
 // and one block per CU — half the operand bytes per MFMA of 256x128.
-// NS: LDS ring depth, NS - 1 K steps in flight across each barrier (3: 2; the 256x128 tile runs
-// one block per CU under the 256-block split target, so a 6-deep ring, 144 KB, fits too).
+// NS: LDS ring depth, NS - 1 K steps in flight across each barrier (3: two).
 template <int BM, int BN = 128, int NS = kG16Stages>
 __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16g_wgrad_kernel(
     const ConvParams p, const __bf16 *__restrict__ dyb, const __bf16 *__restrict__ xb) {
@@ -296,7 +295,9 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
   constexpr int NB = BN / 128;                // B images
   constexpr int IMG = BKP * 256;              // one [32 k][128] bf16 image
   constexpr int STAGE = (NA + NB) * IMG;
-  static_assert(NS >= 3 && NS * STAGE <= 160 * 1024, "ring depth");
+  // (a 4- / 6-deep ring measured no faster, profiles/r5/g16_wgrad_ring_ab.txt: the K loop is
+  // unrolled over exactly three stages)
+  static_assert(NS == 3 && NS * STAGE <= 160 * 1024, "ring depth");
 
   __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
 
@@ -335,24 +336,54 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
     ci[j] = ncol - tap * p.c;
   }
   const __bf16 *zero = reinterpret_cast<const __bf16 *>(g_bf16g_zero);
+  // x element offset of each B chunk's tap and channel, relative to its pixel's (oh s, ow s)
+  int xo[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) xo[j] = (tdy[j] * p.w + tdx[j]) * p.c + ci[j];
+
+  // This lane's pixel walk: the pixel m = kt BKP + kr it loads, its output row / column and the
+  // element offsets of its dY row (column bm + chs) and of its x pixel, advanced one K step at a
+  // time (issue() sees non-decreasing kt: the re-reads past the last step repeat it) instead of
+  // two divisions and a 64-bit multiply per step.  32-bit offsets: the host plans this kernel
+  // only for operands of < 2^31 elements (g16_wgrad_fits).
+  int w_kt = kt0, w_m = kt0 * BKP + kr, w_ow, w_oh, w_a, w_x;
+  {
+    const uint32_t q = fdiv((uint32_t)w_m, p.fd_ow);
+    w_ow = w_m - (int)q * p.ow;
+    const uint32_t b = fdiv(q, p.fd_oh);
+    w_oh = (int)q - (int)b * p.oh;
+    w_a = w_m * p.k + bm + chs;
+    w_x = (((int)b * p.h + w_oh * p.stride) * p.w + w_ow * p.stride) * p.c;
+  }
+  const int x_col = p.stride * p.c;                              // x offset per output column
+  const int x_row = (p.stride * p.w - p.ow * p.stride) * p.c;     // ... at a row wrap
+  const int x_img = (p.h - p.oh * p.stride) * p.w * p.c;         // ... at an image wrap
 
   auto issue = [&](int kt, int st) {
+    if (kt != w_kt) {   // kt == w_kt + 1
+      w_kt = kt;
+      w_m += BKP;
+      w_a += BKP * p.k;
+      w_ow += BKP;
+      w_x += BKP * x_col;
+      while (w_ow >= p.ow) {
+        w_ow -= p.ow;
+        w_x += x_row;
+        if (++w_oh == p.oh) {
+          w_oh = 0;
+          w_x += x_img;
+        }
+      }
+    }
     const uint32_t As = uni((int)((uint32_t)(uintptr_t)lds + st * STAGE + wave * 1024));
-    const int m = kt * BKP + kr;
-    const bool rv = m < K;
-    const int mm = rv ? m : 0;
-    uint32_t q = fdiv((uint32_t)mm, p.fd_ow);
-    const int ow = mm - (int)q * p.ow;
-    uint32_t b = fdiv(q, p.fd_oh);
-    const int oh = (int)q - (int)b * p.oh;
+    const bool rv = w_m < K;
 #pragma unroll
-    for (int i = 0; i < NA; ++i)
-      glds16((rv & a_col[i]) ? dyb + (size_t)mm * p.k + bm + 128 * i + chs : zero, As + i * IMG);
+    for (int i = 0; i < NA; ++i) glds16((rv & a_col[i]) ? dyb + (w_a + 128 * i) : zero, As + i * IMG);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int iy = oh * p.stride + tdy[j], ix = ow * p.stride + tdx[j];
+      const int iy = w_oh * p.stride + tdy[j], ix = w_ow * p.stride + tdx[j];
       const bool bv = rv & b_col[j] & ((unsigned)iy < (unsigned)p.h) & ((unsigned)ix < (unsigned)p.w);
-      glds16(bv ? xb + (((int)b * p.h + iy) * p.w + ix) * p.c + ci[j] : zero, As + (NA + j) * IMG);
+      glds16(bv ? xb + (w_x + xo[j]) : zero, As + (NA + j) * IMG);
     }
   };
 
@@ -365,22 +396,51 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  auto compute = [&](int st) {
-    const char *Ai = lds + st * STAGE + (wm * WTM / 128) * IMG;   // the A image of this wave's rows
-    const char *Bs = lds + st * STAGE + (NA + (wn * WTN) / 128) * IMG;   // this wave's columns' B image
+  // Every fragment read's per-lane byte offset within a ring stage (mc_frag's two transposed
+  // reads, image base included), computed once: a read adds only the compile-time stage base,
+  // which the DS offset field absorbs (the K loop below is unrolled over the NS stages).
+  constexpr int KS = BKP / 16;
+  uint32_t oa[TM][KS][2], ob[TN][KS][2];
+  {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    auto offs = [&](int img, int c0, int ks, uint32_t (&o)[2]) {
+      const int ch = ((c0 + 16 * (g & 1)) >> 3) + (pp >> 1);
+      const int kb = 16 * ks + 8 * (g >> 1);
+      o[0] = (uint32_t)(img + mc_off(kb + q, ch) + 8 * (pp & 1));
+      o[1] = (uint32_t)(img + mc_off(kb + 4 + q, ch) + 8 * (pp & 1));
+    };
+    const int ia = (wm * WTM / 128) * IMG, ib = (NA + (wn * WTN) / 128) * IMG;   // this wave's A / B image
     const int ar = (wm * WTM) % 128, bc = (wn * WTN) % 128;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) offs(ia, ar + i * 32, ks, oa[i][ks]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) offs(ib, bc + j * 32, ks, ob[j][ks]);
+    }
+  }
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)lds;
+  auto rd = [&](uint32_t base, const uint32_t (&o)[2]) -> bf16x8 {
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(base + o[0]));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4 *)(uintptr_t)(base + o[1]));
+    return __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+
+  auto compute = [&](auto st_c) {
+    constexpr int st = decltype(st_c)::value;
+    const uint32_t sb = lds_u32 + st * STAGE;
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[slot][i] = mc_frag(Ai, ar + i * 32, ks, lane);
+      for (int i = 0; i < TM; ++i) a[slot][i] = rd(sb, oa[i][ks]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[slot][j] = mc_frag(Bs, bc + j * 32, ks, lane);
+      for (int j = 0; j < TN; ++j) b[slot][j] = rd(sb, ob[j][ks]);
     };
     read_frags(0, 0);
 #pragma unroll
-    for (int ks = 0; ks < BKP / 16; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int cb = ks & 1;
-      if (ks + 1 < BKP / 16) read_frags(ks + 1, cb ^ 1);
+      if (ks + 1 < KS) read_frags(ks + 1, cb ^ 1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -395,17 +455,23 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
     const int klast = kt1 - 1;
 #pragma unroll
     for (int i = 0; i < NS - 1; ++i) issue(min(kt0 + i, klast), i);
-    int st = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
+    auto step = [&](auto st_c, int kt) {
+      constexpr int st = decltype(st_c)::value;
       // step kt landed (steps kt+1 .. kt+NS-2 in flight) ...
       wait_vmcnt<(NS - 2) * (NA + NB)>();
       // ... in every wave after the barrier, which also retires every wave's reads of step kt-1's
       // stage, the one step kt+NS-1 overwrites
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");   // no LDS access moves above the barrier
-      issue(min(kt + NS - 1, klast), st == 0 ? NS - 1 : st - 1);
-      compute(st);
-      st = st == NS - 1 ? 0 : st + 1;
+      issue(min(kt + NS - 1, klast), (st + NS - 1) % NS);
+      compute(st_c);
+    };
+    for (int kt = kt0; kt < kt1; kt += 3) {   // (NS == 3: one unrolled pass per ring turn)
+      step(std::integral_constant<int, 0>{}, kt);
+      if (kt + 1 >= kt1) break;
+      step(std::integral_constant<int, 1>{}, kt + 1);
+      if (kt + 2 >= kt1) break;
+      step(std::integral_constant<int, 2>{}, kt + 2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -652,7 +652,10 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     }
     // weight gradients with 16-B channel chunks (Cin % 8 == 0, Cout % 8 == 0) on the LDS-DMA
     // weight-gradient kernel: {128,256}x128 tiles, K steps of 32 output pixels
-    if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 8 == 0 && d->k % 8 == 0) {
+    // (its pixel walk keeps 32-bit element offsets: operands of < 2^31 elements, g16_wgrad_fits)
+    const bool g16_wgrad_fits = ((int64_t)p.n * p.oh * p.ow + 64) * p.k < INT32_MAX &&
+                                ((int64_t)p.n + 1) * p.h * p.w * p.c < INT32_MAX;
+    if (op == ADAPTSEG_CONV_BWD_WEIGHT && d->c % 8 == 0 && d->k % 8 == 0 && g16_wgrad_fits) {
       pl.g16 = true;
       pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
       pl.g16_bn = 128;
