@@ -636,9 +636,15 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // (c5 27.6 vs 27.7 images/s, per-shape within +-5 %): only with ADAPTSEG_MATH_BF16_WIDE
     const bool w256 = conv_math() == ADAPTSEG_MATH_BF16_WIDE;
     pl.bf16_bn = (w256 && op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 256) ? 256 : 128;
-    // forward / stride-1 data gradients with N >= 128 on the LDS-DMA kernel (conv_bf16g.hpp):
-    // 128x256 tiles when N >= 256 (the activation operand is fetched once per tap), else 256x128
-    if (op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= 128) {   // stride-2 data gradients by parity class too
+    // forward / data gradients with N >= 64 on the LDS-DMA kernel (conv_bf16g.hpp): 128x256 tiles
+    // when N >= 256 (the activation operand is fetched once per tap), else 256x128 — at N = 64
+    // (layer1, D.conv2's stride-2 data gradient) with half the column tile idle, still faster than
+    // the register-staged bf16 kernel: l1.conv2 48 -> 40 us, D.conv2 data gradient 204 -> 171,
+    // c5 +0.8 % (profiles/r5/g16_min_n64_ab.txt; 128: the round-4 threshold)
+#ifndef ADAPTSEG_G16_MIN_N
+#define ADAPTSEG_G16_MIN_N 64
+#endif
+    if (op != ADAPTSEG_CONV_BWD_WEIGHT && p.N >= ADAPTSEG_G16_MIN_N) {   // stride-2 data gradients by parity class too
       pl.g16 = true;
       pl.g16_bm = p.N >= 256 ? 128 : 256;
       pl.g16_bn = p.N >= 256 ? 256 : 128;
