@@ -214,3 +214,25 @@ def test_f32x3_forward_term_images_only_for_the_wide_dilated_convs():
         assert not any(engine.x3_forward_terms(g) for g in want)
     finally:
         K.set_conv_math(K.MATH_F32X3)
+
+
+def test_inventory_counts_only_the_forwards_that_run():
+    """bench.conv_inventory books the discriminator forward the D step reuses (StepConfig.d_reuse)
+    and the single-level step's discarded first head (second_head_only) only when they run."""
+    import bench
+    from adaptsegnet_amd import engine
+    from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
+    model, D = DeeplabMulti(num_classes=19), FCDiscriminator(num_classes=19)
+    args = (model, D, "single-level", 4, (1024, 512), (1024, 512), (1024, 512))
+    base = sum(bench.conv_inventory(*args).values())
+    n, h, w = 4, 512, 1024
+    d_fwd = 0.0
+    for conv in D._convs():
+        g = conv.geom()
+        d_fwd += g.flops(n, h, w)
+        h, w = g.out_hw(h, w)
+    assert abs(sum(bench.conv_inventory(*args, d_reuse=False).values()) - base - d_fwd) <= 1e-9 * base
+    head = engine.aspp_geom(model.layer5).flops(4, 64, 128) * 2   # layer5 at 1024x512 (64 x 128), source + target
+    assert abs(sum(bench.conv_inventory(*args, first_head=True).values()) - base - head) <= 1e-9 * base
+    multi = (model, D, "multi-level", 2, (1280, 720), (1024, 512), (1024, 512))
+    assert bench.conv_inventory(*multi, first_head=True) == bench.conv_inventory(*multi)
