@@ -141,12 +141,16 @@ _SIGS = {
     "adaptseg_grid_warp_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
+    "adaptseg_conv_set_x3h": [_I],
+    "adaptseg_conv_get_x3h": [ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_enable_mem": [_I],
     "adaptseg_timing_read_id": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_L)],
     "adaptseg_timing_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(_L)],
+    "adaptseg_timing_enable_stream": [_I],
+    "adaptseg_timing_read_id_stream": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_L)],
 }
 _RESTYPES = {"adaptseg_last_error": ctypes.c_char_p, "adaptseg_version": ctypes.c_char_p}
 

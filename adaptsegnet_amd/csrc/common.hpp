@@ -1,6 +1,7 @@
 // Shared helpers for the adaptseg gfx950 kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string>
@@ -113,6 +114,7 @@ __device__ __forceinline__ float4 join3(uint2 h, uint2 m, uint2 l) {
 }
 
 int conv_math();   // process-wide conv arithmetic (adaptseg_conv_set_math)
+int x3h_mode();    // ADAPTSEG_X3H: products on igemm_x3h_kernel (conv_igemm.hip)
 // Operand copies of the _x entry points are three exact bf16 term images [3][rows][C] under the
 // F32X3 maths (one bf16 RNE image under the BF16 maths)
 inline bool copies_are_terms() {
@@ -132,5 +134,19 @@ enum TimingMemId {
 };
 void timing_begin(int kernel_id, hipStream_t s, double units, int *slot);
 void timing_end(int slot, hipStream_t s);
+// Execution-time form for the conv GEMMs: the slot's events are handed to the next launch_k
+// of this thread, which launches through hipExtLaunchKernel with them, so they time the
+// kernel's own execution (what rocprofv3 reports) rather than its stream time.  With stream
+// timing on (adaptseg_timing_enable_stream) a second event pair brackets the stream time too.
+void timing_begin_exec(int kernel_id, hipStream_t s, double units, int *slot);
+bool timing_take_exec(hipEvent_t &start, hipEvent_t &stop);
+
+// Launch a kernel; a pending execution-timed slot (timing_begin_exec) gets its events.
+template <typename... P, typename... A>
+inline void launch_k(void (*kern)(P...), dim3 grid, dim3 block, hipStream_t s, A... args) {
+  hipEvent_t e0, e1;
+  if (timing_take_exec(e0, e1)) hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, args...);
+  else hipLaunchKernelGGL(kern, grid, block, 0, s, args...);
+}
 
 }  // namespace adaptseg

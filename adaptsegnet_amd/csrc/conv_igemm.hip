@@ -298,13 +298,20 @@ struct TimingState {
   std::mutex mu;
   bool enabled = false;
   bool mem_enabled = false;  // HBM-bound kernels (ids >= kTimingMemBase), adaptseg_timing_enable_mem
+  bool stream_too = false;   // conv GEMMs: also bracket the stream time (adaptseg_timing_enable_stream)
   int selector = -1;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  // per slot: the measured pair (conv GEMMs: the kernel's execution, via hipExtLaunchKernel;
+  // other kernels: stream events around the launch) and, for conv GEMMs under stream_too, a
+  // stream-time pair recorded around the launch
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events, sevents;
   std::vector<double> flops;  // algorithmic FLOPs (conv) or bytes (HBM-bound kernels) per launch
   std::vector<int> ids;
+  std::vector<char> has_stream;
   size_t used = 0;
 };
 static TimingState g_timing;
+// the execution-timed slot waiting for this thread's next launch_k (timing_begin_exec)
+static thread_local int t_exec_slot = -1;
 
 // Process-wide conv math (adaptseg_conv_set_math), default F32X3 (fp32-accurate on the bf16
 // MFMA, conv_x3.hpp); F32 = the fp32-input MFMA kernels, BF16 = bf16 operands (config c5).
@@ -312,30 +319,87 @@ static TimingState g_timing;
 static std::atomic<int> g_conv_math{ADAPTSEG_MATH_F32X3};
 int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 
-void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
-  *slot = -1;
+// ADAPTSEG_X3H (read once): bit 1 / 2 put the F32X3 forward / data-gradient products the x3r tile
+// covers on igemm_x3h_kernel (conv_x3r.hpp) instead of the register-staged 128x128x16 kernel
+#ifndef ADAPTSEG_X3H_DEFAULT
+#define ADAPTSEG_X3H_DEFAULT 0
+#endif
+static std::atomic<int> &x3h_state() {
+  static std::atomic<int> m{[] {
+    const char *e = std::getenv("ADAPTSEG_X3H");
+    return e && *e ? std::atoi(e) : ADAPTSEG_X3H_DEFAULT;
+  }()};
+  return m;
+}
+int x3h_mode() { return x3h_state().load(std::memory_order_relaxed); }
+
+// one more slot (two event pairs), under g_timing.mu
+static bool timing_grow() {
+  hipEvent_t a, b, c, d;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess || hipEventCreate(&c) != hipSuccess ||
+      hipEventCreate(&d) != hipSuccess)
+    return false;
+  g_timing.events.push_back({a, b});
+  g_timing.sevents.push_back({c, d});
+  g_timing.flops.push_back(0.0);
+  g_timing.ids.push_back(0);
+  g_timing.has_stream.push_back(0);
+  return true;
+}
+
+static int timing_slot(int kernel_id, double fl) {
   if (kernel_id >= kTimingMemBase) {
-    if (!g_timing.mem_enabled) return;
+    if (!g_timing.mem_enabled) return -1;
   } else {
-    if (!g_timing.enabled) return;
-    if (g_timing.selector >= 0 && g_timing.selector != kernel_id) return;
+    if (!g_timing.enabled) return -1;
+    if (g_timing.selector >= 0 && g_timing.selector != kernel_id) return -1;
   }
   std::lock_guard<std::mutex> lk(g_timing.mu);
-  if (g_timing.used == g_timing.events.size()) {
-    hipEvent_t a, b;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
-    g_timing.events.push_back({a, b});
-    g_timing.flops.push_back(0.0);
-    g_timing.ids.push_back(0);
+  if (g_timing.used == g_timing.events.size() && !timing_grow()) return -1;
+  const int slot = (int)g_timing.used++;
+  g_timing.flops[slot] = fl;
+  g_timing.ids[slot] = kernel_id;
+  g_timing.has_stream[slot] = 0;
+  return slot;
+}
+
+void timing_begin(int kernel_id, hipStream_t s, double fl, int *slot) {
+  *slot = timing_slot(kernel_id, fl);
+  if (*slot >= 0) (void)hipEventRecord(g_timing.events[*slot].first, s);
+}
+
+void timing_begin_exec(int kernel_id, hipStream_t s, double fl, int *slot) {
+  *slot = timing_slot(kernel_id, fl);
+  if (*slot < 0) return;
+  t_exec_slot = *slot;
+  if (g_timing.stream_too) {
+    g_timing.has_stream[*slot] = 1;
+    (void)hipEventRecord(g_timing.sevents[*slot].first, s);
   }
-  *slot = (int)g_timing.used++;
-  g_timing.flops[*slot] = fl;
-  g_timing.ids[*slot] = kernel_id;
-  (void)hipEventRecord(g_timing.events[*slot].first, s);
+  *slot = -2 - *slot;   // timing_end: an execution-timed slot
+}
+
+bool timing_take_exec(hipEvent_t &start, hipEvent_t &stop) {
+  if (t_exec_slot < 0) return false;
+  start = g_timing.events[t_exec_slot].first;
+  stop = g_timing.events[t_exec_slot].second;
+  t_exec_slot = -1;
+  return true;
 }
 
 void timing_end(int slot, hipStream_t s) {
-  if (slot < 0) return;
+  if (slot == -1) return;
+  if (slot <= -2) {   // execution-timed: the launch recorded the pair
+    const int i = -2 - slot;
+    if (t_exec_slot == i) {   // no launch_k consumed it: nothing was timed
+      t_exec_slot = -1;
+      std::lock_guard<std::mutex> lk(g_timing.mu);
+      g_timing.ids[i] = -1;
+      return;
+    }
+    if (g_timing.has_stream[i]) (void)hipEventRecord(g_timing.sevents[i].second, s);
+    return;
+  }
   (void)hipEventRecord(g_timing.events[slot].second, s);
 }
 
@@ -407,6 +471,7 @@ size_t splitk_slab_bytes(const Plan &pl) {
 int plan_bm(const Plan &pl) {
   if (pl.g16) return pl.g16_bm;
   if (pl.x3r) return pl.mode == MODE_WGRAD ? pl.x3r_bm : 256;
+  if (pl.x3h) return pl.mode == MODE_WGRAD ? pl.x3r_bm : 256;
   return (pl.bf16 || pl.x3) ? 128 : kCfgBM[pl.cfg];
 }
 
@@ -416,6 +481,8 @@ int plan_bm(const Plan &pl) {
 // it is there already; it then skips its per-call copy).  Re-plans the grid.
 static void x3_terms_flags(Plan &pl) {
   pl.x3g = pl.x3r = pl.x3ext = true;
+  pl.x3h = false;
+  if (pl.mode == MODE_WGRAD) pl.x3r_bm = pl.p.M >= 256 ? 256 : 128;   // (make_plan's choice; x3h set 128)
   // weight gradients under the default maths run on the side stream beside the main chain's
   // register-staged blocks: the 128-row tile (96 KB LDS, <= 128 VGPRs) leaves a CU room for one
   // of them, the 256-row one (144 KB) does not — except for Cout >= 1024 (DeeplabVGG's fc6 / fc7,
@@ -439,11 +506,11 @@ static void x3_terms(Plan &pl) {
 // >= 8 K-steps per split.  Depends on the K step of the chosen kernel (pl.bk).
 void set_splits(Plan &pl) {
   ConvParams &p = pl.p;
-  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.x3g = pl.x3r = pl.g16 = false;
+  if (!pl.fast) pl.s2 = pl.bf16 = pl.x3 = pl.x3g = pl.x3r = pl.x3h = pl.g16 = false;
   if (!pl.fast && pl.cfg == 8) pl.cfg = 0;  // cfg 8 is built for vector FAST operands only
   const int bm = plan_bm(pl);
   const int bn = pl.g16 ? pl.g16_bn : pl.bf16 ? pl.bf16_bn : pl.x3 ? x3_bn(pl.mode) : kCfgBN[pl.cfg];
-  pl.bk = pl.g16 ? pl.g16_bk : pl.bf16 ? 64 : pl.x3r ? kX3rBK : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
+  pl.bk = pl.g16 ? pl.g16_bk : pl.bf16 ? 64 : (pl.x3r || pl.x3h) ? kX3rBK : pl.x3 ? kX3BK : pl.fast ? fast_bk(pl.cfg) : BK;
   if (pl.s2) {  // rows of the largest parity class; K of the largest tap subset; no K split
     p.M = p.n * ((p.h + 1) / 2) * ((p.w + 1) / 2);
     p.K = ((p.kh_ + 1) / 2) * ((p.kw_ + 1) / 2) * p.k;
@@ -484,9 +551,9 @@ void set_splits(Plan &pl) {
                      : (pl.mode == MODE_WGRAD && pl.x3)            ? kX3WgradTarget
                                                                    : kSplitTarget;
   // the LDS-DMA bf16 / x3r kernels run one block per CU: split only grids under half the CUs
-  const int split_below = pl.mode == MODE_WGRAD ? target : pl.x3r ? 256 : pl.g16 ? 128 : 257;
+  const int split_below = pl.mode == MODE_WGRAD ? target : (pl.x3r || pl.x3h) ? 256 : pl.g16 ? 128 : 257;
   int splits = 1;
-  if (pl.mode == MODE_WGRAD && pl.x3r) {
+  if (pl.mode == MODE_WGRAD && (pl.x3r || pl.x3h)) {
     // one 8-wave block per CU: the grid takes ceil(tiles * s / 256) rounds of 1/s of the K range,
     // so pick the split count s (<= 256, >= 32 K steps each) with the fewest such units — e.g.
     // layer4.conv2 (144 tiles of 128 rows): s = 1 leaves 112 CUs idle for the whole launch
@@ -505,7 +572,7 @@ void set_splits(Plan &pl) {
       }
     }
   } else if (pl.tiles < split_below && !pl.s2) {
-    splits = std::max(1, ((pl.g16 || pl.x3r) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
+    splits = std::max(1, ((pl.g16 || pl.x3r || pl.x3h) && pl.mode != MODE_WGRAD ? 256 : target) / pl.tiles);
     splits = std::min(splits, std::max(1, nkt / 4));
     splits = std::min(splits, 256);
   }
@@ -607,7 +674,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     else pl.bf16 = true;
   }
   // F32X3 conv math: the vector FAST cases whose 16-deep K tiles stay inside one tap
-  pl.x3 = pl.x3g = pl.x3r = pl.x3r_ok = pl.x3ext = false;
+  pl.x3 = pl.x3g = pl.x3r = pl.x3r_ok = pl.x3ext = pl.x3h = false;
   pl.x3r_bm = 256;
   const bool x3_math = conv_math() == ADAPTSEG_MATH_F32X3 || conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT;
   if (x3_math && pl.fast && !pl.ae && !pl.be) {
@@ -628,6 +695,14 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // images under F32X3 measured slower for the multi-tap weight gradients (c2 -1.4 %,
     // profiles/r3/x3r_wgrad_taps_ab.txt); experiments/r3_rejected.patch keeps that build.
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
+    // F32X3: products on the x3r tiles with the fp32 operands split in-kernel (igemm_x3h_kernel,
+    // igemm_x3hw_kernel), by ADAPTSEG_X3H bit 1 (forward) / 2 (data gradient) / 4 (weight gradient)
+    if (pl.x3 && pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3 &&
+        ((op == ADAPTSEG_CONV_FWD && (x3h_mode() & 1)) || (op == ADAPTSEG_CONV_BWD_DATA && (x3h_mode() & 2)) ||
+         (op == ADAPTSEG_CONV_BWD_WEIGHT && (x3h_mode() & 4)))) {
+      pl.x3h = true;
+      if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = 128;   // igemm_x3hw_kernel<128> (conv_launch_x3.hip)
+    }
   }
   if (pl.x3) pl.cfg = 0;
   if (pl.bf16) {
@@ -683,6 +758,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
 int kernel_id(const Plan &pl, int mode) {
   // 88 / 89: the FAST cfg-8 stride-2 ids, which never occur (cfg 8 has no stride-2 form)
   if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
+  // 86 / 87: the FAST cfg-8 per-element ids, which never occur (cfg 8 takes vector operands only)
+  if (pl.x3h) return 100 * mode + 86 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
@@ -737,12 +814,12 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
     // times the GEMM kernel alone, as rocprof reports it
     e = pl.x3 ? prep_x3(pl, ws, s) : prep_bf16(pl, ws, s);
     if (e == hipSuccess) {
-      timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
+      timing_begin_exec(kernel_id(pl, mode), s, pl.flops, &slot);
       e = pl.x3 ? launch_x3(pl, ws, s) : launch_bf16(pl, ws, s);
       timing_end(slot, s);
     }
   } else {
-    timing_begin(kernel_id(pl, mode), s, pl.flops, &slot);
+    timing_begin_exec(kernel_id(pl, mode), s, pl.flops, &slot);
     if (mode == MODE_FWD) e = launch_fwd(pl, s);
     else if (mode == MODE_DGRAD) e = launch_dgrad(pl, s);
     else e = launch_wgrad(pl, s);
@@ -1371,6 +1448,18 @@ int adaptseg_conv_set_math(int math) {
   return ADAPTSEG_OK;
 }
 
+int adaptseg_conv_set_x3h(int mode) {
+  AS_CHECK_ARG(mode >= 0 && mode <= 7, "conv_set_x3h: mode must be 0..7");
+  x3h_state().store(mode);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_conv_get_x3h(int *mode) {
+  AS_CHECK_ARG(mode, "conv_get_x3h: null");
+  *mode = x3h_mode();
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_conv_get_math(int *math) {
   AS_CHECK_ARG(math, "conv_get_math: null");
   *math = g_conv_math.load();
@@ -1393,15 +1482,37 @@ int adaptseg_timing_reserve(int64_t pairs) {
   AS_CHECK_ARG(pairs >= 0 && pairs <= (1 << 20), "timing_reserve: bad count %lld", (long long)pairs);
   std::lock_guard<std::mutex> lk(g_timing.mu);
   while ((int64_t)g_timing.events.size() < pairs) {
-    hipEvent_t a, b;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    if (!timing_grow()) {
       set_error("timing_reserve: hipEventCreate failed");
       return ADAPTSEG_ERR_HIP;
     }
-    g_timing.events.push_back({a, b});
-    g_timing.flops.push_back(0.0);
-    g_timing.ids.push_back(0);
   }
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_timing_enable_stream(int enable) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  g_timing.stream_too = enable != 0;
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_timing_read_id_stream(int kernel_id, double *total_ms, int64_t *launches) {
+  AS_CHECK_ARG(total_ms && launches, "timing_read_id_stream: null");
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  double ms = 0;
+  int64_t n = 0;
+  for (size_t i = 0; i < g_timing.used; ++i) {
+    if (g_timing.ids[i] != kernel_id || !g_timing.has_stream[i]) continue;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, g_timing.sevents[i].first, g_timing.sevents[i].second) != hipSuccess) {
+      set_error("timing_read_id_stream: event query failed (synchronise first)");
+      return ADAPTSEG_ERR_HIP;
+    }
+    ms += t;
+    ++n;
+  }
+  *total_ms = ms;
+  *launches = n;
   return ADAPTSEG_OK;
 }
 
@@ -1439,7 +1550,7 @@ int adaptseg_timing_read(double *total_ms, double *total_flops, int64_t *launche
   double ms = 0, fl = 0;
   int64_t n = 0;
   for (size_t i = 0; i < g_timing.used; ++i) {
-    if (g_timing.ids[i] >= kTimingMemBase) continue;
+    if (g_timing.ids[i] < 0 || g_timing.ids[i] >= kTimingMemBase) continue;
     ++n;
     float t = 0.f;
     if (hipEventElapsedTime(&t, g_timing.events[i].first, g_timing.events[i].second) != hipSuccess) {

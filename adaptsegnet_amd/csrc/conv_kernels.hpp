@@ -1711,6 +1711,7 @@ struct Plan {
   int x3r_bm;  // its row tile (256; weight gradients with Cout < 256: 128)
   bool x3r_ok; // F32X3 product the x3r kernel covers (a 32-deep step inside one tap, 16-B chunks)
   bool x3ext;  // x3r on the caller's term images (F32X3 maths): no per-call split copies
+  bool x3h;    // ... x3r's 256x128x32 tile with the fp32 activation split in-kernel (igemm_x3h_kernel)
   int bf16_bn; // its tile width: 256 for forward / data-grad products with N >= 256, else 128
   bool g16;    // bf16 LDS-DMA kernel (conv_bf16g.hpp): bf16 activation copy, g16_bm x g16_bn x 64
   int g16_bm, g16_bn, g16_bk;

@@ -185,8 +185,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
                                    : reinterpret_cast<const __bf16 *>(base);
     dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(512);
     if (pl.s2) {   // stride-2 data gradient: parity classes on grid.z, K step 32
-      if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_DGRAD, 128, 256, 32, true><<<grid, block, 0, s>>>(p, act, wb);
-      else igemm_bf16g_kernel<MODE_DGRAD, 256, 128, 32, true><<<grid, block, 0, s>>>(p, act, wb);
+      if (pl.g16_bn == 256) launch_k(igemm_bf16g_kernel<MODE_DGRAD, 128, 256, 32, true>, grid, block, s, p, act, wb);
+      else launch_k(igemm_bf16g_kernel<MODE_DGRAD, 256, 128, 32, true>, grid, block, s, p, act, wb);
       return hipGetLastError();
     }
     if (pl.mode == MODE_WGRAD) {
@@ -195,14 +195,14 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
                                              base + al256(g16_act_elems(pl) * sizeof(__bf16)));
       // (a 6-deep ring for the 256x128 tile, 4-deep for 128x128 — five / three steps in flight
       // instead of two: per shape within +-3 %, c5 -0.6 %, profiles/r5/g16_wgrad_ring_ab.txt)
-      if (pl.g16_bm == 256) igemm_bf16g_wgrad_kernel<256><<<grid, block, 0, s>>>(p, act, act2);
-      else igemm_bf16g_wgrad_kernel<128><<<grid, block, 0, s>>>(p, act, act2);
+      if (pl.g16_bm == 256) launch_k(igemm_bf16g_wgrad_kernel<256>, grid, block, s, p, act, act2);
+      else launch_k(igemm_bf16g_wgrad_kernel<128>, grid, block, s, p, act, act2);
       return hipGetLastError();
     }
 #define G16_LAUNCH(MODE_, BK_)                                                                  \
   do {                                                                                          \
-    if (pl.g16_bn == 256) igemm_bf16g_kernel<MODE_, 128, 256, BK_><<<grid, block, 0, s>>>(p, act, wb); \
-    else igemm_bf16g_kernel<MODE_, 256, 128, BK_><<<grid, block, 0, s>>>(p, act, wb);          \
+    if (pl.g16_bn == 256) launch_k(igemm_bf16g_kernel<MODE_, 128, 256, BK_>, grid, block, s, p, act, wb); \
+    else launch_k(igemm_bf16g_kernel<MODE_, 256, 128, BK_>, grid, block, s, p, act, wb);          \
   } while (0)
     if (pl.mode == MODE_FWD) {
       if (pl.g16_bk == 64) G16_LAUNCH(MODE_FWD, 64);
@@ -218,19 +218,19 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
   dim3 grid(pl.tiles, p.splits, pl.s2 ? 4 : 1), block(bf16_threads(pl.mode));
   if (pl.mode == MODE_FWD && pl.act_ext) {   // the caller's bf16 activation copy (bf16 activation storage)
     const __bf16 *act = reinterpret_cast<const __bf16 *>(pl.act_ext);
-    if (w256) igemm_bf16_kernel<MODE_FWD, false, 256, true><<<grid, block, 0, s>>>(p, wb, act);
-    else igemm_bf16_kernel<MODE_FWD, false, 128, true><<<grid, block, 0, s>>>(p, wb, act);
+    if (w256) launch_k(igemm_bf16_kernel<MODE_FWD, false, 256, true>, grid, block, s, p, wb, act);
+    else launch_k(igemm_bf16_kernel<MODE_FWD, false, 128, true>, grid, block, s, p, wb, act);
   } else if (pl.mode == MODE_FWD) {
-    if (w256) igemm_bf16_kernel<MODE_FWD, false, 256><<<grid, block, 0, s>>>(p, wb);
-    else igemm_bf16_kernel<MODE_FWD, false, 128><<<grid, block, 0, s>>>(p, wb);
+    if (w256) launch_k(igemm_bf16_kernel<MODE_FWD, false, 256>, grid, block, s, p, wb, (const __bf16 *)nullptr);
+    else launch_k(igemm_bf16_kernel<MODE_FWD, false, 128>, grid, block, s, p, wb, (const __bf16 *)nullptr);
   } else if (pl.mode == MODE_DGRAD && pl.s2) {
-    if (w256) igemm_bf16_kernel<MODE_DGRAD, true, 256><<<grid, block, 0, s>>>(p, wb);
-    else igemm_bf16_kernel<MODE_DGRAD, true, 128><<<grid, block, 0, s>>>(p, wb);
+    if (w256) launch_k(igemm_bf16_kernel<MODE_DGRAD, true, 256>, grid, block, s, p, wb, (const __bf16 *)nullptr);
+    else launch_k(igemm_bf16_kernel<MODE_DGRAD, true, 128>, grid, block, s, p, wb, (const __bf16 *)nullptr);
   } else if (pl.mode == MODE_DGRAD) {
-    if (w256) igemm_bf16_kernel<MODE_DGRAD, false, 256><<<grid, block, 0, s>>>(p, wb);
-    else igemm_bf16_kernel<MODE_DGRAD, false, 128><<<grid, block, 0, s>>>(p, wb);
+    if (w256) launch_k(igemm_bf16_kernel<MODE_DGRAD, false, 256>, grid, block, s, p, wb, (const __bf16 *)nullptr);
+    else launch_k(igemm_bf16_kernel<MODE_DGRAD, false, 128>, grid, block, s, p, wb, (const __bf16 *)nullptr);
   } else {
-    igemm_bf16_kernel<MODE_WGRAD, false, 128><<<grid, block, 0, s>>>(p, wb);
+    launch_k(igemm_bf16_kernel<MODE_WGRAD, false, 128>, grid, block, s, p, wb, (const __bf16 *)nullptr);
   }
   return hipGetLastError();
 }

@@ -89,21 +89,30 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
   if (pl.x3r) {
     const char *base = reinterpret_cast<const char *>(wpack) + al256(x3_wpack_bytes(pl));
     const __bf16 *act = pl.act_ext ? reinterpret_cast<const __bf16 *>(pl.act_ext) : reinterpret_cast<const __bf16 *>(base);
-    if (pl.mode == MODE_FWD) igemm_x3r_kernel<MODE_FWD, false><<<grid, 512, 0, s>>>(p, act, wb);
-    else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3r_kernel<MODE_DGRAD, true><<<grid, 512, 0, s>>>(p, act, wb);
-    else if (pl.mode == MODE_DGRAD) igemm_x3r_kernel<MODE_DGRAD, false><<<grid, 512, 0, s>>>(p, act, wb);
+    if (pl.mode == MODE_FWD) launch_k(igemm_x3r_kernel<MODE_FWD, false>, grid, 512, s, p, act, wb);
+    else if (pl.mode == MODE_DGRAD && pl.s2) launch_k(igemm_x3r_kernel<MODE_DGRAD, true>, grid, 512, s, p, act, wb);
+    else if (pl.mode == MODE_DGRAD) launch_k(igemm_x3r_kernel<MODE_DGRAD, false>, grid, 512, s, p, act, wb);
     else {
       const __bf16 *act2 = pl.act_ext2 ? reinterpret_cast<const __bf16 *>(pl.act_ext2)
                                        : reinterpret_cast<const __bf16 *>(base + al256(3 * x3g_act_elems(pl) * sizeof(__bf16)));
-      if (pl.x3r_bm == 256) igemm_x3r_wgrad_kernel<256><<<grid, 512, 0, s>>>(p, act, act2);
-      else igemm_x3r_wgrad_kernel<128><<<grid, 512, 0, s>>>(p, act, act2);
+      if (pl.x3r_bm == 256) launch_k(igemm_x3r_wgrad_kernel<256>, grid, 512, s, p, act, act2);
+      else launch_k(igemm_x3r_wgrad_kernel<128>, grid, 512, s, p, act, act2);
     }
     return hipGetLastError();
   }
-  if (pl.mode == MODE_FWD) igemm_x3_kernel<MODE_FWD, false><<<grid, block, 0, s>>>(p, wb);
-  else if (pl.mode == MODE_DGRAD && pl.s2) igemm_x3_kernel<MODE_DGRAD, true><<<grid, block, 0, s>>>(p, wb);
-  else if (pl.mode == MODE_DGRAD) igemm_x3_kernel<MODE_DGRAD, false><<<grid, block, 0, s>>>(p, wb);
-  else igemm_x3_kernel<MODE_WGRAD, false><<<grid, block, 0, s>>>(p, wb);
+  if (pl.x3h) {
+    // (the 256-row weight-gradient tile needs two register sets of six float4 beside its 128
+    // accumulators: it spills, so the weight gradient runs the 128-row tile)
+    if (pl.mode == MODE_WGRAD) launch_k(igemm_x3hw_kernel<128>, grid, 512, s, p);
+    else if (pl.mode == MODE_FWD) launch_k(igemm_x3h_kernel<MODE_FWD, false>, grid, 512, s, p, wb);
+    else if (pl.s2) launch_k(igemm_x3h_kernel<MODE_DGRAD, true>, grid, 512, s, p, wb);
+    else launch_k(igemm_x3h_kernel<MODE_DGRAD, false>, grid, 512, s, p, wb);
+    return hipGetLastError();
+  }
+  if (pl.mode == MODE_FWD) launch_k(igemm_x3_kernel<MODE_FWD, false>, grid, block, s, p, wb);
+  else if (pl.mode == MODE_DGRAD && pl.s2) launch_k(igemm_x3_kernel<MODE_DGRAD, true>, grid, block, s, p, wb);
+  else if (pl.mode == MODE_DGRAD) launch_k(igemm_x3_kernel<MODE_DGRAD, false>, grid, block, s, p, wb);
+  else launch_k(igemm_x3_kernel<MODE_WGRAD, false>, grid, block, s, p, wb);
   return hipGetLastError();
 }
 

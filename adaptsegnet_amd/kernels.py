@@ -82,6 +82,17 @@ def set_conv_math(math: int) -> None:
     _ops.set_math(math)
 
 
+def set_x3h(mode: int) -> None:
+    """F32X3: forward (bit 1) / data-gradient (bit 2) products on igemm_x3h_kernel (the
+    256x128x32 tile, fp32 activations split in-kernel) instead of the 128x128x16 register-staged
+    kernel (adaptseg_conv_set_x3h; initial value from ADAPTSEG_X3H)."""
+    _ops.set_x3h(mode)
+
+
+def get_x3h() -> int:
+    return _ops.x3h_mode()
+
+
 def get_conv_math() -> int:
     m = ctypes.c_int(0)
     check(_lib.lib().adaptseg_conv_get_math(ctypes.byref(m)), "conv_get_math")
@@ -685,11 +696,25 @@ def timing_enable_mem(enable: bool = True):
 
 
 def timing_read_id(kernel_id: int):
-    """(total_ms, total_units, launches) of the recorded launches of one kernel id."""
+    """(total_ms, total_units, launches) of the recorded launches of one kernel id (conv GEMMs:
+    the kernels' execution time, hipExtLaunchKernel events)."""
     ms, un, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
     check(_lib.lib().adaptseg_timing_read_id(int(kernel_id), ctypes.byref(ms), ctypes.byref(un),
                                              ctypes.byref(n)), "timing_read_id")
     return ms.value, un.value, n.value
+
+
+def timing_enable_stream(enable: bool = True):
+    """Conv GEMMs: record stream-time event pairs beside the execution-time ones."""
+    check(_lib.lib().adaptseg_timing_enable_stream(1 if enable else 0), "timing_enable_stream")
+
+
+def timing_read_id_stream(kernel_id: int):
+    """(total_ms, launches) of the stream-time pairs of one conv kernel id."""
+    ms, n = ctypes.c_double(0), ctypes.c_int64(0)
+    check(_lib.lib().adaptseg_timing_read_id_stream(int(kernel_id), ctypes.byref(ms), ctypes.byref(n)),
+          "timing_read_id_stream")
+    return ms.value, n.value
 
 
 def timing_read():

@@ -118,11 +118,25 @@ def _ws_args(nbytes: int, device):
 # ---------------------------------------------------------------------------------------
 _DESC_CACHE: dict = {}
 _CONV_MATH = [MATH_F32X3]   # the library's default (adaptseg_conv_get_math)
+_X3H = [None]               # adaptseg_conv_get_x3h, read on first use (the library reads ADAPTSEG_X3H)
+
+
+def x3h_mode() -> int:
+    if _X3H[0] is None:
+        m = ctypes.c_int(0)
+        check(_lib.lib().adaptseg_conv_get_x3h(ctypes.byref(m)), "conv_get_x3h")
+        _X3H[0] = m.value
+    return _X3H[0]
+
+
+def set_x3h(mode: int) -> None:
+    check(_lib.lib().adaptseg_conv_set_x3h(int(mode)), "conv_set_x3h")
+    _X3H[0] = int(mode)
 
 
 def conv_desc(n, c, h, w, strides, cout, kh, kw, stride, pads, dils):
     """(ConvDesc, {op: workspace bytes}, oh, ow) of one conv product, cached."""
-    key = (n, c, h, w, strides, cout, kh, kw, stride, pads, dils, _CONV_MATH[0])
+    key = (n, c, h, w, strides, cout, kh, kw, stride, pads, dils, _CONV_MATH[0], x3h_mode())
     d = _DESC_CACHE.get(key)
     if d is None:
         p, dl = pads[0], dils[0]

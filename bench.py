@@ -15,10 +15,11 @@ Conv math: the fp32 configs run F32X3 by default (fp32-accurate convs on the bf1
 exact three-term bf16 operand splits, six bf16 products per fp32 product; conv_x3.hpp),
 ``--conv-math f32`` the fp32-input MFMA kernels; c5 runs bf16 operands.
 
-roofline: the dominant implicit-GEMM conv kernel symbol (the most measured kernel time per
-step, from hipEvents around every conv launch of one untimed step) is bracketed by hipEvents
-inside the library during the timed steps; achieved = its
-algorithmic FLOPs / its summed launch time, against that kernel's MFMA ceiling: the fp32 MFMA
+roofline: the dominant implicit-GEMM conv kernel symbol (the most kernel execution time per
+step, from execution-time events of every conv launch of one untimed step) is launched with
+hipExtLaunchKernel start/stop events inside the library during the timed steps, which time the
+kernel's own execution as rocprofv3 does; achieved = its
+algorithmic FLOPs / its summed execution time, against that kernel's MFMA ceiling: the fp32 MFMA
 peak (157.3 TFLOP/s) for the fp32-input kernels, the bf16 dense peak / 6 (419.4 TFLOP/s of
 fp32 products) for F32X3, the bf16 dense peak (2516.6) for bf16.
 cpu_baseline: the oracle (stock-PyTorch CPU restatement of the reference step, the
@@ -194,7 +195,7 @@ _CFG = {0: (128, 128, 2, 2, 32), 1: (256, 32, 4, 1, 32), 2: (32, 256, 1, 4, 32),
 
 def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
-    if sel % 100 in (88, 89, 95, 96):
+    if sel % 100 in (86, 87, 88, 89, 95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
     if sel % 100 >= 90:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
@@ -205,6 +206,10 @@ def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
     if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
+    if sel % 100 in (86, 87):   # F32X3, the same tiles with the fp32 operands split in-kernel
+        if op == 2:
+            return f"igemm_x3hw_kernel<{256 if var == 6 else 128}>"
+        return f"igemm_x3h_kernel<{op}, {'true' if var == 7 else 'false'}>"
     if sel % 100 in (88, 89):   # F32X3, 256x128x32 tiles on pre-split images (conv_x3r.hpp)
         if op == 2:
             return f"igemm_x3r_wgrad_kernel<{256 if var == 8 else 128}>"
@@ -234,7 +239,7 @@ def pmc_traffic(config, sel):
     (tools/gpu_traffic.sh + tools/traffic_summary.py over this same bench command):
     profiles/rN/pmc/traffic_<config>[_<kernel>].json, newest round first."""
     import glob
-    for rnd in ("r5", "r4", "r3", "r2", "r1"):
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):
         for path in sorted(glob.glob(os.path.join(REPO, "profiles", rnd, "pmc", f"traffic_{config}*.json"))):
             try:
                 d = json.load(open(path))
@@ -415,22 +420,32 @@ def main():
         # of the largest symbols (roofline.by_kernel); the timed region records only `dom`.
         K.timing_enable(-1)
         K.timing_enable_mem(True)
+        K.timing_enable_stream(True)
         trainer.step(args.warmup, batches)
         torch.cuda.synchronize()
+        K.timing_enable_stream(False)
         K.timing_enable_mem(False)
         K.timing_enable(-1, enable=False)
         by_kernel = []
+        # conv GEMMs: execution time (hipExtLaunchKernel events: the kernel's own start to end,
+        # what rocprofv3 reports) ranks them; the stream time of the same launches (events
+        # recorded around the launch in its stream: includes waiting for CU slots beside the
+        # other streams' work) is reported beside it
         live = {sel: K.timing_read_id(sel) for sel in inv}
         live = {sel: t for sel, t in live.items() if t[2]}
         if live:
             dom = max(live, key=lambda sel: live[sel][0])
         for sel in sorted(live, key=lambda sel: live[sel][0], reverse=True)[:6]:
             ms_, _fl, n_ = live[sel]
+            sms_, sn_ = K.timing_read_id_stream(sel)
             pk, fam = kernel_peak(sel)
             a_ = inv[sel] / (ms_ / 1e3) / 1e12   # algorithmic FLOPs of one step / summed launch time
+            sa_ = inv[sel] / (sms_ / 1e3) / 1e12 if sms_ else None
             by_kernel.append({"kernel": selector_symbol(sel), "selector": sel, "achieved": a_, "peak": pk,
                               "unit": "TFLOP/s", "frac": a_ / pk, "kernel_family": fam,
                               "kernel_ms_per_step": ms_, "launches_per_step": n_, "avg_launch_ms": ms_ / n_,
+                              "stream_ms_per_step": sms_, "stream_avg_launch_ms": sms_ / sn_ if sn_ else None,
+                              "stream_frac": sa_ / pk if sa_ else None,
                               "algorithmic_tflop_per_step": inv[sel] / 1e12,
                               "flop_share_of_step": inv[sel] / step_flops})
         for kid, name in K.MEM_KERNELS.items():
@@ -484,6 +499,7 @@ def main():
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
                    "conv_math": conv_math,
                    "switches": engine.switches(),
+                   "x3h_mode": K.get_x3h(),
                    "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
                    "target_first": bool(scfg.target_first), "d_reuse": bool(scfg.d_reuse),
                    "second_head_only": bool(scfg.second_head_only),
@@ -517,14 +533,17 @@ def main():
                            "algorithmic_flop_per_launch": k_flops / k_launches,
                            "launched_flop_per_launch": launched_flops / k_launches,
                            "kernel": selector_symbol(dom), "selector": dom,
-                           "chosen_by": "most measured kernel time per step (by_kernel)",
+                           "chosen_by": "most kernel execution time per step (by_kernel)",
+                           "timing": "kernel execution (hipExtLaunchKernel start/stop events, as rocprofv3 "
+                                     "reports kernel durations); by_kernel adds the stream time",
                            "launches_per_step": k_launches / args.steps,
                            "avg_launch_ms": avg_ms,
                            "flop_share_of_step": inv[dom] / step_flops,
                            # the six conv symbols with the most kernel time, live over the
                            # untimed step before the timed one
                            "by_kernel": by_kernel,
-                           "by_kernel_source": "hipEvents around every conv launch of one untimed step"}
+                           "by_kernel_source": "execution-time events of every conv launch of one untimed step, "
+                                               "stream-time events around the same launches"}
         # north_star: HBM GB/s of the interp / loss kernels (and the BN passes) vs the peak,
         # live hipEvents over one untimed step right before the timed region
         out["hbm_kernels"] = hbm

@@ -92,6 +92,13 @@ enum adaptseg_conv_math {
 };
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);
+/* F32X3 maths: forward (bit 1) / data-gradient (bit 2) products that the 256x128x32 tile covers
+   (a 32-deep K step inside one tap) run on igemm_x3h_kernel — that tile with the fp32 activation
+   split in-kernel, no term images — instead of the register-staged 128x128x16 kernel.  Same
+   arithmetic (bitwise the x3r results).  Process-wide; initial value from the environment
+   variable ADAPTSEG_X3H.  Set before sizing workspaces, like the maths. */
+int adaptseg_conv_set_x3h(int mode);
+int adaptseg_conv_get_x3h(int *mode);
 
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
 /* Kernel selector (see adaptseg_timing_enable) and K-split count the library would use. */
@@ -529,8 +536,10 @@ int adaptseg_add_i64(int64_t *p, int64_t n, int64_t v, adaptseg_stream_t stream)
 
 /* ------------------------------------------------------------------------------------ */
 /* Live kernel timing for the benchmark: when enabled, every launch of the selected          */
-/* implicit-GEMM conv kernel symbol is bracketed by hipEvents on its stream; the summed      */
-/* durations and summed algorithmic FLOPs (2*N*OH*OW*K*C*KH*KW*nseg per launch) are read    */
+/* implicit-GEMM conv kernel symbol is launched through hipExtLaunchKernel with an event     */
+/* pair, which records the kernel's own execution (start to end, as rocprofv3 reports it,   */
+/* not the stream time it spent queued behind other streams' work); the summed durations    */
+/* and summed algorithmic FLOPs (2*N*OH*OW*K*C*KH*KW*nseg per launch) are read              */
 /* back after a device synchronise.  selector = -1: every igemm launch; otherwise           */
 /* selector = 100*op + 10*tile + variant names ONE kernel symbol: op 0 fwd, 1 bwd-data,     */
 /* 2 bwd-weight; tile 0 = 128x128, 1 = 256x32, 2 = 32x256, 3 = 64x256, 4 = 256x64;          */
@@ -552,6 +561,11 @@ int adaptseg_timing_reserve(int64_t pairs);
    ALGORITHMIC bytes (compulsory reads + writes at the op interface) as units. */
 int adaptseg_timing_enable_mem(int enable);
 int adaptseg_timing_read_id(int kernel_id, double *total_ms, double *total_units, int64_t *launches);
+/* Conv GEMMs: also bracket each timed launch with stream events (the time from the launch's
+   position in its stream to its end, which includes waiting for CU slots beside other streams'
+   work); read per kernel id with adaptseg_timing_read_id_stream. */
+int adaptseg_timing_enable_stream(int enable);
+int adaptseg_timing_read_id_stream(int kernel_id, double *total_ms, int64_t *launches);
 
 #ifdef __cplusplus
 }
