@@ -141,8 +141,8 @@ _SIGS = {
     "adaptseg_grid_warp_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "adaptseg_conv_set_math": [_I],
     "adaptseg_conv_get_math": [ctypes.POINTER(_I)],
-    "adaptseg_conv_set_x3h": [_I],
-    "adaptseg_conv_get_x3h": [ctypes.POINTER(_I)],
+    "adaptseg_conv_set_option": [_I, _I],
+    "adaptseg_conv_get_option": [_I, ctypes.POINTER(_I)],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_enable_mem": [_I],
     "adaptseg_timing_read_id": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

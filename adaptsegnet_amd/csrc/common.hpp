@@ -114,7 +114,8 @@ __device__ __forceinline__ float4 join3(uint2 h, uint2 m, uint2 l) {
 }
 
 int conv_math();   // process-wide conv arithmetic (adaptseg_conv_set_math)
-int x3h_mode();    // ADAPTSEG_X3H: products on igemm_x3h_kernel (conv_igemm.hip)
+int x3h_mode();        // ADAPTSEG_OPT_X3H (adaptseg_conv_set_option, conv_igemm.hip)
+int g16_wide_mode();   // ADAPTSEG_OPT_G16_WIDE
 // Operand copies of the _x entry points are three exact bf16 term images [3][rows][C] under the
 // F32X3 maths (one bf16 RNE image under the BF16 maths)
 inline bool copies_are_terms() {

@@ -64,26 +64,35 @@ __device__ __forceinline__ int g16_off(int r, int ch) {
 // 256x256 (BK 32 only: a 3 x 32 KB ring): 8 waves of 64x128, 128 accumulator VGPRs, one block per
 // CU — half the operand bytes per MFMA of the 128x256 tile, for products whose M x N fills the
 // chip with such tiles.
-template <int MODE, int BM, int BN, int BK, bool S2 = false>
-__global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) igemm_bf16g_kernel(const ConvParams p,
+// NST: LDS stages.  3 (the default): two K steps in flight across each barrier.  2 (256x256x64,
+// "wide"): 2 x 64 KB, one step in flight — issued right after the barrier that opens the step
+// before it, so it has that step's MFMAs (16 waves x 16, 2,048 cycles per SIMD) to land; twice
+// the MFMA cycles per SIMD per barrier of the 128x256x64 tile and 2/3 of its operand bytes per
+// MFMA.
+template <int MODE, int BM, int BN, int BK, bool S2 = false, int NST = kG16Stages>
+__global__ void __launch_bounds__(NST == 2 ? 1024 : 512, (BK == 32 && BM * BN < 65536) || NST == 2 ? 4 : 2)
+igemm_bf16g_kernel(const ConvParams p,
                                                                               const __bf16 *__restrict__ ab,
                                                                               const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products only");
   static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
   static_assert(BK == 64 || BK == 32, "K step");
-  constexpr int NT = 512;
-  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;  // 64 x (BN / WAVES_N) wave tiles
-  static_assert(WAVES_M * WAVES_N == 8 && BN % (32 * WAVES_N) == 0, "8 waves");
-  static_assert(BM * BN < 65536 || BK == 32, "256x256 tiles: K step 32 (LDS ring)");
+  static_assert(NST == 3 || NST == 2, "ring depth");
+  // 8 waves; the two-stage 256x256 tile: 16 waves of 64x64 (4 per SIMD, the 64x64 wave code
+  // and its <= 128 registers: 64x128 wave tiles spill at two waves per SIMD)
+  constexpr int NW = NST == 2 ? 16 : 8, NT = 64 * NW;
+  constexpr int WAVES_M = BM / 64, WAVES_N = NW / WAVES_M;  // 64 x (BN / WAVES_N) wave tiles
+  static_assert(WAVES_M * WAVES_N == NW && BN % (32 * WAVES_N) == 0, "wave grid");
+  static_assert(BM * BN < 65536 || BK == 32 || NST == 2, "256x256 tiles: K step 32, or 64 on two stages");
   constexpr int WTM = 64, WTN = BN / WAVES_N, TM = 2, TN = WTN / 32;
   constexpr int LPR = BK / 8;                          // lanes per image row (16 B each)
   constexpr int RPI = 64 / LPR;                        // rows per LDS-DMA instruction
-  constexpr int NA = BM / (8 * RPI), NB = BN / (8 * RPI);  // instructions per wave and K step
+  constexpr int NA = BM / (NW * RPI), NB = BN / (NW * RPI);  // instructions per wave and K step
   constexpr int IMGA = BM * BK * 2;
   constexpr int STAGE = g16_stage_bytes(BM, BN, BK);
   (void)NT;
 
-  __shared__ __attribute__((aligned(16))) char lds[kG16Stages * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[NST * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -116,14 +125,14 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
   const int ca = MODE == MODE_FWD ? p.c : p.k;
 
   // ---- per-lane rows: instruction i of wave w covers image rows 8 RPI i + RPI w .. +RPI-1 ----
-  const int rsub = wave * RPI + lane / LPR;                 // row within an 8 RPI-row group
+  const int rsub = wave * RPI + lane / LPR;                 // row within an NW RPI-row group
   // source chunk (elements) of this lane: the one whose swizzled slot is the lane's (lane % LPR)
   const int chs = (BK == 64 ? ((lane & 7) ^ ((rsub >> 1) & 7)) : ((lane & 3) ^ ((rsub >> 2) & 3))) * 8;
   int a_pix[NA], a_y[NA], a_x[NA];
   bool a_ok[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int m = bm + 8 * RPI * i + rsub;
+    const int m = bm + NW * RPI * i + rsub;
     a_ok[i] = m < M;
     const int mm = min(m, M - 1);
     if constexpr (S2) {   // row = (b, i, j) of the parity class's subgrid
@@ -154,7 +163,7 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
   bool b_ok[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int n = bn + 8 * RPI * j + rsub;
+    const int n = bn + NW * RPI * j + rsub;
     b_ok[j] = n < p.N;
     b_off[j] = min(n, p.N - 1) * ktot + chs;
   }
@@ -199,10 +208,10 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
         v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.h) & ((unsigned)(a_x[i] + dx) < (unsigned)p.w);
       else
         v = a_ok[i] & ((unsigned)(a_y[i] + dy) < (unsigned)p.oh) & ((unsigned)(a_x[i] + dx) < (unsigned)p.ow);
-      glds16(v ? ab + a_pix[i] + soff : zero, As + i * 8 * 1024);
+      glds16(v ? ab + a_pix[i] + soff : zero, As + i * NW * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) glds16(b_ok[j] ? wb + b_off[j] + wk : zero, Bs + j * 8 * 1024);
+    for (int j = 0; j < NB; ++j) glds16(b_ok[j] ? wb + b_off[j] + wk : zero, Bs + j * NW * 1024);
   };
 
   const int wm = wave / WAVES_N, wn = wave - wm * WAVES_N;
@@ -241,7 +250,22 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
     }
   };
 
-  if (kt0 < kt1) {
+  if constexpr (NST == 2) {
+   if (kt0 < kt1) {
+    // two stages, one K step in flight: step kt lives in stage (kt - kt0) & 1
+    issue(kt0, 0);
+    int st = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of step kt landed
+      __builtin_amdgcn_s_barrier();                       // ... everyone's; stage st^1 is free
+      asm volatile("" ::: "memory");
+      if (kt + 1 < kt1) issue(kt + 1, st ^ 1);
+      compute(st);
+      st ^= 1;
+    }
+    __syncthreads();   // the epilogue reuses the LDS
+   }
+  } else if (kt0 < kt1) {
     // Ring of 3 stages, two K steps in flight: step kt lives in stage (kt - kt0) % 3.  The loads
     // past the last step re-read it into a stage nobody reads again, so every wave always has
     // exactly NA + NB instructions per step outstanding and the counted wait stays constant.
@@ -251,7 +275,8 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
     int st = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       // this wave's DMAs of step kt are done (step kt+1's NA + NB stay in flight) ...
-      static_assert(NA + NB == 6 || NA + NB == 4 || NA + NB == 3, "vmcnt below counts 6, 4 or 3 instructions per step");
+      static_assert(NST == 2 || NA + NB == 6 || NA + NB == 4 || NA + NB == 3,
+                    "vmcnt below counts 6, 4 or 3 instructions per step");
       if constexpr (NA + NB == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else if constexpr (NA + NB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
@@ -268,7 +293,7 @@ __global__ void __launch_bounds__(512, (BK == 32 && BM * BN < 65536) ? 4 : 2) ig
     __syncthreads();  // the epilogue reuses the LDS
   }
 
-  static_assert(kG16Stages * STAGE >= WAVES_M * WAVES_N * 32 * 33 * 4, "LDS for the bf16x8 epilogue");
+  static_assert(NST * STAGE >= WAVES_M * WAVES_N * 32 * 33 * 4, "LDS for the bf16x8 epilogue");
   igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 1>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
 }

@@ -319,19 +319,26 @@ static thread_local int t_exec_slot = -1;
 static std::atomic<int> g_conv_math{ADAPTSEG_MATH_F32X3};
 int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 
-// ADAPTSEG_X3H (read once): bit 1 / 2 put the F32X3 forward / data-gradient products the x3r tile
-// covers on igemm_x3h_kernel (conv_x3r.hpp) instead of the register-staged 128x128x16 kernel
+// Kernel-selection options (adaptseg_conv_set_option), initial values from the environment:
+//   ADAPTSEG_OPT_X3H (ADAPTSEG_X3H): bits 1 / 2 / 4 put the F32X3 forward / data-gradient /
+//     weight-gradient products the x3r tiles cover on igemm_x3h_kernel / igemm_x3hw_kernel
+//     (conv_x3r.hpp) instead of the register-staged 128x128x16 kernel;
+//   ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE): 1 = bf16 forward / data-gradient products with
+//     N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile (conv_bf16g.hpp).
 #ifndef ADAPTSEG_X3H_DEFAULT
 #define ADAPTSEG_X3H_DEFAULT 0
 #endif
-static std::atomic<int> &x3h_state() {
-  static std::atomic<int> m{[] {
-    const char *e = std::getenv("ADAPTSEG_X3H");
-    return e && *e ? std::atoi(e) : ADAPTSEG_X3H_DEFAULT;
-  }()};
-  return m;
+#ifndef ADAPTSEG_G16_WIDE_DEFAULT
+#define ADAPTSEG_G16_WIDE_DEFAULT 0
+#endif
+static int env_int(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
 }
-int x3h_mode() { return x3h_state().load(std::memory_order_relaxed); }
+static std::atomic<int> g_opt_x3h{env_int("ADAPTSEG_X3H", ADAPTSEG_X3H_DEFAULT)};
+static std::atomic<int> g_opt_g16_wide{env_int("ADAPTSEG_G16_WIDE", ADAPTSEG_G16_WIDE_DEFAULT)};
+int x3h_mode() { return g_opt_x3h.load(std::memory_order_relaxed); }
+int g16_wide_mode() { return g_opt_g16_wide.load(std::memory_order_relaxed); }
 
 // one more slot (two event pairs), under g_timing.mu
 static bool timing_grow() {
@@ -697,8 +704,14 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
     // F32X3: products on the x3r tiles with the fp32 operands split in-kernel (igemm_x3h_kernel,
     // igemm_x3hw_kernel), by ADAPTSEG_X3H bit 1 (forward) / 2 (data gradient) / 4 (weight gradient)
+    // Forward / data gradient only at K >= 256 (per shape, tools/conv_bench.py: the layer-1 1x1
+    // products with K = 64 / 128 run slower on the 256-row tile — two to four K steps against its
+    // prologue and epilogue) and not on the stride-2 parity classes (D.conv2's data gradient 449 ->
+    // 523 us); the larger products gain 4-12 % (l4.ds forward 854 -> 775 us).
+    const bool x3h_fd = p.K >= 256 && !(op == ADAPTSEG_CONV_BWD_DATA && d->stride == 2);
     if (pl.x3 && pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3 &&
-        ((op == ADAPTSEG_CONV_FWD && (x3h_mode() & 1)) || (op == ADAPTSEG_CONV_BWD_DATA && (x3h_mode() & 2)) ||
+        ((op == ADAPTSEG_CONV_FWD && (x3h_mode() & 1) && x3h_fd) ||
+         (op == ADAPTSEG_CONV_BWD_DATA && (x3h_mode() & 2) && x3h_fd) ||
          (op == ADAPTSEG_CONV_BWD_WEIGHT && (x3h_mode() & 4)))) {
       pl.x3h = true;
       if (op == ADAPTSEG_CONV_BWD_WEIGHT) pl.x3r_bm = 128;   // igemm_x3hw_kernel<128> (conv_launch_x3.hip)
@@ -728,6 +741,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
+      if (g16_wide_mode() && p.N >= 256 && p.K >= 2048 && !pl.s2) pl.g16_bm = 256;   // 256x256x64, two stages
       // (256x256x32 tiles, one block per CU, measured slower: c5 -10 % / -2.4 % with the weight
       // gradients only, profiles/r3/bf16_wide_tiles_ab.txt; experiments/r3_rejected.patch)
     }
@@ -762,6 +776,8 @@ int kernel_id(const Plan &pl, int mode) {
   if (pl.x3h) return 100 * mode + 86 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
   if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
+  // 85: the FAST cfg-8 id with per-element B, which never occurs (cfg 8: vector operands only)
+  if (pl.g16 && pl.g16_bm == 256 && pl.g16_bn == 256) return 100 * mode + 85;
   if (pl.g16) return 100 * mode + (pl.g16_bk == 64 ? (pl.g16_bn == 256 ? 97 : 98) : (pl.g16_bn == 256 ? 94 : 99));
   if (pl.bf16) return 100 * mode + 90 + (pl.s2 ? 1 : 0) + (pl.bf16_bn == 256 ? 2 : 0);
   if (pl.x3) return 100 * mode + 95 + (pl.s2 ? 1 : 0);
@@ -1448,15 +1464,24 @@ int adaptseg_conv_set_math(int math) {
   return ADAPTSEG_OK;
 }
 
-int adaptseg_conv_set_x3h(int mode) {
-  AS_CHECK_ARG(mode >= 0 && mode <= 7, "conv_set_x3h: mode must be 0..7");
-  x3h_state().store(mode);
+int adaptseg_conv_set_option(int option, int value) {
+  if (option == ADAPTSEG_OPT_X3H) {
+    AS_CHECK_ARG(value >= 0 && value <= 7, "conv_set_option: X3H must be 0..7");
+    g_opt_x3h.store(value);
+  } else if (option == ADAPTSEG_OPT_G16_WIDE) {
+    AS_CHECK_ARG(value == 0 || value == 1, "conv_set_option: G16_WIDE must be 0 or 1");
+    g_opt_g16_wide.store(value);
+  } else {
+    AS_CHECK_ARG(false, "conv_set_option: unknown option %d", option);
+  }
   return ADAPTSEG_OK;
 }
 
-int adaptseg_conv_get_x3h(int *mode) {
-  AS_CHECK_ARG(mode, "conv_get_x3h: null");
-  *mode = x3h_mode();
+int adaptseg_conv_get_option(int option, int *value) {
+  AS_CHECK_ARG(value, "conv_get_option: null");
+  if (option == ADAPTSEG_OPT_X3H) *value = x3h_mode();
+  else if (option == ADAPTSEG_OPT_G16_WIDE) *value = g16_wide_mode();
+  else AS_CHECK_ARG(false, "conv_get_option: unknown option %d", option);
   return ADAPTSEG_OK;
 }
 

@@ -201,7 +201,9 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
     }
 #define G16_LAUNCH(MODE_, BK_)                                                                  \
   do {                                                                                          \
-    if (pl.g16_bn == 256) launch_k(igemm_bf16g_kernel<MODE_, 128, 256, BK_>, grid, block, s, p, act, wb); \
+    if (pl.g16_bm == 256 && pl.g16_bn == 256)                                                   \
+      launch_k(igemm_bf16g_kernel<MODE_, 256, 256, 64, false, 2>, grid, dim3(1024), s, p, act, wb); \
+    else if (pl.g16_bn == 256) launch_k(igemm_bf16g_kernel<MODE_, 128, 256, BK_>, grid, block, s, p, act, wb); \
     else launch_k(igemm_bf16g_kernel<MODE_, 256, 128, BK_>, grid, block, s, p, act, wb);          \
   } while (0)
     if (pl.mode == MODE_FWD) {

@@ -83,14 +83,25 @@ def set_conv_math(math: int) -> None:
 
 
 def set_x3h(mode: int) -> None:
-    """F32X3: forward (bit 1) / data-gradient (bit 2) products on igemm_x3h_kernel (the
-    256x128x32 tile, fp32 activations split in-kernel) instead of the 128x128x16 register-staged
-    kernel (adaptseg_conv_set_x3h; initial value from ADAPTSEG_X3H)."""
-    _ops.set_x3h(mode)
+    """F32X3: forward (bit 1) / data-gradient (bit 2) / weight-gradient (bit 4) products on the
+    256x128x32 tiles with the fp32 operands split in-kernel (igemm_x3h_kernel, igemm_x3hw_kernel)
+    instead of the 128x128x16 register-staged kernel (ADAPTSEG_OPT_X3H; initial value from
+    ADAPTSEG_X3H)."""
+    _ops.set_option(_ops.OPT_X3H, mode)
 
 
 def get_x3h() -> int:
-    return _ops.x3h_mode()
+    return _ops.get_option(_ops.OPT_X3H)
+
+
+def set_g16_wide(on: bool) -> None:
+    """BF16: forward / data-gradient products with N >= 256 and K >= 2048 on the 256x256x64
+    two-stage LDS-DMA tile (ADAPTSEG_OPT_G16_WIDE; initial value from ADAPTSEG_G16_WIDE)."""
+    _ops.set_option(_ops.OPT_G16_WIDE, 1 if on else 0)
+
+
+def get_g16_wide() -> int:
+    return _ops.get_option(_ops.OPT_G16_WIDE)
 
 
 def get_conv_math() -> int:
@@ -331,13 +342,20 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
     if res is not None:
         flags |= EPI_RESIDUAL
     if aux is not None and not flags & EPI_RELU_GRAD:   # the same gating rule in both storages
+        # (no caller passes aux to the bf16-storage path; the kernel would apply LeakyReLU' there)
+        assert not low, "conv_dgrad: aux with bf16 gradient storage is not a supported combination"
         flags |= EPI_LEAKY_GRAD
     outb = None if low else _bf16_like(out, bf16_out)
     dx, dxb = (None, out) if low else (out, outb)
     wp = _wpack(g, n, h, w, nhwc_strides(n, h, w, g.cin), weights, CONV_BWD_DATA)
     ret = out if (low or not bf16_out) else (out, outb)
     nt = 0
-    if bnsum is not None and aux is None:
+    # the launch-time conditions of the fused sums (adaptseg_conv2d_bwd_data_bnsum): 16-B aligned
+    # operands (an unaligned dY or weight downgrades the plan; the BN vectors and its fp32 x are read
+    # as float4) and C % 4 == 0 — otherwise the unfused call, and bn_bwd runs its own reduction
+    if (bnsum is not None and aux is None and g.cin % 4 == 0 and _aligned16(dy, *weights) and
+            _aligned16(bnsum.mean, bnsum.invstd, bnsum.weight, bnsum.bias) and
+            (bnsum.x is None or bnsum.x.dtype != torch.float32 or _aligned16(bnsum.x))):
         nt = conv_bnsum_tiles(g, n, h, w, with_copy=dyb is not None and _aligned16(dyb))
     if nt == 0:
         _OP.conv2d_bwd_data(dy, dyb, list(weights), wp, res, resbits, aux, dx, dxb, (n, g.cin, h, w), _wshape(g),

@@ -118,25 +118,27 @@ def _ws_args(nbytes: int, device):
 # ---------------------------------------------------------------------------------------
 _DESC_CACHE: dict = {}
 _CONV_MATH = [MATH_F32X3]   # the library's default (adaptseg_conv_get_math)
-_X3H = [None]               # adaptseg_conv_get_x3h, read on first use (the library reads ADAPTSEG_X3H)
+OPT_X3H, OPT_G16_WIDE = 1, 2   # adaptseg_conv_option
+_OPTS: dict = {}               # adaptseg_conv_get_option, read on first use (the library reads the environment)
 
 
-def x3h_mode() -> int:
-    if _X3H[0] is None:
+def get_option(opt: int) -> int:
+    if opt not in _OPTS:
         m = ctypes.c_int(0)
-        check(_lib.lib().adaptseg_conv_get_x3h(ctypes.byref(m)), "conv_get_x3h")
-        _X3H[0] = m.value
-    return _X3H[0]
+        check(_lib.lib().adaptseg_conv_get_option(int(opt), ctypes.byref(m)), "conv_get_option")
+        _OPTS[opt] = m.value
+    return _OPTS[opt]
 
 
-def set_x3h(mode: int) -> None:
-    check(_lib.lib().adaptseg_conv_set_x3h(int(mode)), "conv_set_x3h")
-    _X3H[0] = int(mode)
+def set_option(opt: int, value: int) -> None:
+    check(_lib.lib().adaptseg_conv_set_option(int(opt), int(value)), "conv_set_option")
+    _OPTS[opt] = int(value)
 
 
 def conv_desc(n, c, h, w, strides, cout, kh, kw, stride, pads, dils):
     """(ConvDesc, {op: workspace bytes}, oh, ow) of one conv product, cached."""
-    key = (n, c, h, w, strides, cout, kh, kw, stride, pads, dils, _CONV_MATH[0], x3h_mode())
+    key = (n, c, h, w, strides, cout, kh, kw, stride, pads, dils, _CONV_MATH[0], get_option(OPT_X3H),
+           get_option(OPT_G16_WIDE))
     d = _DESC_CACHE.get(key)
     if d is None:
         p, dl = pads[0], dils[0]

@@ -197,7 +197,7 @@ def kernel_peak(sel):
     """(MFMA ceiling in TFLOP/s of algorithmic products, family) of a kernel selector."""
     if sel % 100 in (86, 87, 88, 89, 95, 96):
         return BF16_MFMA_PEAK_TFLOPS / 6, "f32x3 (6 bf16 MFMA products per fp32 product)"
-    if sel % 100 >= 90:
+    if sel % 100 >= 90 or sel % 100 == 85:
         return BF16_MFMA_PEAK_TFLOPS, "bf16"
     return FP32_MFMA_PEAK_TFLOPS, "fp32-input MFMA"
 
@@ -206,6 +206,8 @@ def selector_symbol(sel):
     op, cfg, var = sel // 100, sel // 10 % 10, sel % 10
     if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
+    if sel % 100 == 85:   # bf16 LDS-DMA 256x256x64, two stages
+        return f"igemm_bf16g_kernel<{op}, 256, 256, 64, false, 2>"
     if sel % 100 in (86, 87):   # F32X3, the same tiles with the fp32 operands split in-kernel
         if op == 2:
             return f"igemm_x3hw_kernel<{256 if var == 6 else 128}>"
@@ -499,7 +501,7 @@ def main():
                    "step_conv_tflops_achieved": step_flops / (ms_per_step / 1e3) / 1e12,
                    "conv_math": conv_math,
                    "switches": engine.switches(),
-                   "x3h_mode": K.get_x3h(),
+                   "x3h_mode": K.get_x3h(), "g16_wide": K.get_g16_wide(),
                    "overlap_domains": trainer._overlap_domains(), "overlap_d": bool(scfg.overlap_d),
                    "target_first": bool(scfg.target_first), "d_reuse": bool(scfg.d_reuse),
                    "second_head_only": bool(scfg.second_head_only),
@@ -508,7 +510,10 @@ def main():
                    # the same against a fixed denominator (the fp32 MFMA peak), comparable across
                    # conv maths and rounds (the line above divides by the dominant family's peak)
                    "step_conv_frac_of_fp32_peak": step_flops / (ms_per_step / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                   "losses_last_step": losses},
+                   "losses_last_step": losses,
+                   # caching-allocator peak over the whole run (d_reuse keeps D's target-forward
+                   # activations until D's own step: ADVICE r5; --no-d-reuse is the low-memory arm)
+                   "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 1e9},
     }
     if not args.no_roofline and k_launches:
         avg_ms = k_ms / k_launches

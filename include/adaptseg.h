@@ -92,13 +92,18 @@ enum adaptseg_conv_math {
 };
 int adaptseg_conv_set_math(int math);
 int adaptseg_conv_get_math(int *math);
-/* F32X3 maths: forward (bit 1) / data-gradient (bit 2) products that the 256x128x32 tile covers
-   (a 32-deep K step inside one tap) run on igemm_x3h_kernel — that tile with the fp32 activation
-   split in-kernel, no term images — instead of the register-staged 128x128x16 kernel.  Same
-   arithmetic (bitwise the x3r results).  Process-wide; initial value from the environment
-   variable ADAPTSEG_X3H.  Set before sizing workspaces, like the maths. */
-int adaptseg_conv_set_x3h(int mode);
-int adaptseg_conv_get_x3h(int *mode);
+/* Kernel-selection options, process-wide (set before sizing workspaces, like the maths); the
+   initial values come from the environment variables named below.
+     ADAPTSEG_OPT_X3H (ADAPTSEG_X3H, default 0): F32X3 maths, bit 1 / 2 / 4 = forward / data-gradient
+       / weight-gradient products that the 256x128x32 term-image tiles cover (a 32-deep K step inside
+       one tap) run on igemm_x3h_kernel / igemm_x3hw_kernel<128> — those tiles with the fp32 operands
+       split in-kernel, no term images — instead of the register-staged 128x128x16 kernel.  Same
+       arithmetic (bitwise the term-image kernels' results on the same plan).
+     ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE, default 0): BF16 maths, 1 = forward / data-gradient
+       products with N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile. */
+enum adaptseg_conv_option { ADAPTSEG_OPT_X3H = 1, ADAPTSEG_OPT_G16_WIDE = 2 };
+int adaptseg_conv_set_option(int option, int value);
+int adaptseg_conv_get_option(int option, int *value);
 
 int adaptseg_conv2d_workspace_size(const adaptseg_conv_desc *d, int op, size_t *bytes);
 /* Kernel selector (see adaptseg_timing_enable) and K-split count the library would use. */

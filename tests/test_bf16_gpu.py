@@ -325,3 +325,49 @@ def test_aspp_tap_gemm_reads_the_bf16_copy_bitwise(bf16_math):
     k.conv_wgrad(geom, gy, x, n, h, w, dw1, accumulate=False, xb=xb)
     for a, b in zip(dw0, dw1):
         assert torch.equal(a, b)
+
+
+# (n, cin, h, w, cout, k, stride, pad, dil): products with N >= 256 and K >= 2048 (the wide tile)
+WIDE_SHAPES = [
+    (2, 256, 24, 40, 256, 3, 1, 2, 2),     # layer3 conv2 (K 2304): one 256-wide column tile
+    (1, 512, 20, 24, 512, 3, 1, 4, 4),     # layer4 conv2 (K 4608), split-K grid
+    (2, 256, 96, 96, 256, 3, 1, 2, 2),     # >= 256 tiles of 256x256: unsplit, in-kernel epilogue
+    (2, 2048, 17, 29, 704, 1, 1, 0, 1),    # the ASPP tap-GEMM's inner 1x1 (N 704: a ragged tile)
+]
+
+
+@pytest.mark.parametrize("shape", WIDE_SHAPES, ids=[f"w{i}" for i in range(len(WIDE_SHAPES))])
+def test_bf16_wide_tile_matches_default_and_oracle(bf16_math, shape):
+    """ADAPTSEG_OPT_G16_WIDE: forward / data-gradient products with N >= 256 and K >= 2048 on the
+    256x256x64 two-stage LDS-DMA tile (selector 100*op + 85): the same k order per output as the
+    128x256 tile, so bitwise its result on an unsplit plan, and the bf16-rounded fp64 oracle
+    within 2e-5 (model/deeplab_multi.py:70-71, 139-140: the c5 atrous products)."""
+    k = bf16_math
+    n, cin, h, w, cout, ks, stride, pad, dil = shape
+    geom = k.ConvGeom(cin, cout, ks, ks, stride, (pad,), (dil,))
+    oh, ow = geom.out_hw(h, w)
+    g = torch.Generator().manual_seed(500 + WIDE_SHAPES.index(shape))
+    x = torch.randn(n, cin, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, ks, ks, generator=g, dtype=torch.float64) / (cin * ks * ks) ** 0.5
+    gy = torch.randn(n, cout, oh, ow, generator=g, dtype=torch.float64)
+    xd, gyd, wd = nhwc(x), nhwc(gy), [wt.permute(0, 2, 3, 1).contiguous().float().to(DEV)]
+    base = [k.conv_kernel_id(geom, n, h, w, op) for op in (0, 1)]
+    y0, dx0 = k.conv_fwd(geom, xd, n, h, w, wd), k.conv_dgrad(geom, gyd, n, h, w, wd)
+    k.set_g16_wide(True)
+    try:
+        wide = [k.conv_kernel_id(geom, n, h, w, op) for op in (0, 1)]
+        y1, dx1 = k.conv_fwd(geom, xd, n, h, w, wd), k.conv_dgrad(geom, gyd, n, h, w, wd)
+    finally:
+        k.set_g16_wide(False)
+    for op, (sel, sp) in enumerate(wide):
+        if (cout if op == 0 else cin) >= 256:
+            assert sel == 100 * op + 85, (op, sel)
+    ref = F.conv2d(bf(x), bf(wt), None, stride, pad, dil)
+    assert rel(nchw(y1), ref) < 2e-5
+    xr = bf(x).requires_grad_(True)
+    F.conv2d(xr, bf(wt), None, stride, pad, dil).backward(bf(gy))
+    assert rel(nchw(dx1), xr.grad) < 2e-5
+    if base[0][1] == 1 and wide[0][1] == 1:
+        assert torch.equal(y0, y1)
+    if base[1][1] == 1 and wide[1][1] == 1:
+        assert torch.equal(dx0, dx1)
