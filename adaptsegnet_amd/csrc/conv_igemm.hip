@@ -326,10 +326,10 @@ int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 //   ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE): 1 = bf16 forward / data-gradient products with
 //     N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile (conv_bf16g.hpp).
 #ifndef ADAPTSEG_X3H_DEFAULT
-#define ADAPTSEG_X3H_DEFAULT 0
+#define ADAPTSEG_X3H_DEFAULT 3
 #endif
 #ifndef ADAPTSEG_G16_WIDE_DEFAULT
-#define ADAPTSEG_G16_WIDE_DEFAULT 0
+#define ADAPTSEG_G16_WIDE_DEFAULT 1
 #endif
 static int env_int(const char *name, int dflt) {
   const char *e = std::getenv(name);

@@ -37,9 +37,19 @@ def test_default_conv_math_selects_f32x3():
     from adaptsegnet_amd import kernels as K
     assert K.get_conv_math() == K.MATH_F32X3
     g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
-    assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [95, 195, 295]
+    # the default ADAPTSEG_OPT_X3H 3: forward / data gradients with K >= 256 on the 256x128x32
+    # tile splitting fp32 rows in-kernel (100*op + 86), weight gradients on the staged kernel
+    assert K.get_x3h() == 3
+    assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [86, 186, 295]
+    c1 = K.ConvGeom(64, 256, 1, 1, 1, (0,), (1,))   # K 64: the staged kernel
+    assert [K.conv_kernel_id(c1, 4, 128, 256, op)[0] for op in (0, 2)] == [95, 295]
     s2 = K.ConvGeom(256, 128, 1, 1, 2, (0,), (1,))
-    assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 196
+    assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 196   # stride-2 parity classes: staged
+    K.set_x3h(0)
+    try:
+        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [95, 195, 295]
+    finally:
+        K.set_x3h(3)
     stem = K.ConvGeom(3, 64, 7, 7, 2, (3,), (1,))
     assert K.conv_kernel_id(stem, 4, 512, 1024, 0, (3 * 512 * 1024, 512 * 1024, 1024, 1))[0] % 100 < 90
     d5 = K.ConvGeom(512, 1, 4, 4, 2, (1,), (1,))
@@ -147,7 +157,11 @@ def test_bf16_operand_abi_checks_on_host():
     K.set_conv_math(K.MATH_BF16)
     try:
         g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
+        # K 2304, N 256: the 256x256x64 two-stage tile (ADAPTSEG_OPT_G16_WIDE, default on)
+        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 298]
+        K.set_g16_wide(False)
         assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
+        K.set_g16_wide(True)
         s2 = K.ConvGeom(256, 128, 1, 1, 2, (0,), (1,))
         assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 192    # stride-2 parity classes, LDS-DMA
         # weight gradient without the fp32 operands needs both copies (and no bias gradient)

@@ -101,7 +101,7 @@ def test_copy_operand_only_matches_the_lds_dma_selectors():
         seen = set()
         for g, n, h, w, op, st in geoms:
             kid, _ = K.conv_kernel_id(g, n, h, w, op, st)
-            lds_dma = kid % 100 in (94, 97, 98, 99) or (op == 1 and kid % 100 in (92, 93))
+            lds_dma = kid % 100 in (85, 94, 97, 98, 99) or (op == 1 and kid % 100 in (92, 93))
             # the register-staged bf16 forward (90-93) reads the contiguous bf16 copy too
             lds_dma = lds_dma or (op == 0 and kid % 100 in (90, 91, 92, 93))
             if g.cout <= 32:   # tap-GEMM (ASPP heads): the selector is the inner GEMM's, whose

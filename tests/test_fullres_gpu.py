@@ -271,6 +271,32 @@ def test_c1_forward_crossentropy2d_vs_oracle():
         assert abs(loss - l_ref) <= 1e-3 * abs(l_ref)
 
 
+# one oracle step per (geometry, BN mode, GAN, storage, batch) per session: the full-size CPU
+# steps dominate this module's time, and test_fullres_fused_bn_sums_match_unfused repeats
+# test_fullres_step_vs_oracle[trainBN-c2]'s
+_ORACLE_CACHE: dict = {}
+
+
+def _oracle_step(geom, bn_train, gan, act_bf16, batch):
+    key = (geom, bn_train, gan, act_bf16, batch)
+    if key not in _ORACLE_CACHE:
+        level, src, tgt = GEOMS[geom]
+        xs, lab, xt = _batch(src, tgt, batch)
+        cfg = dict(level=level, gan=gan, input_size=src, input_size_target=tgt)
+        # oracle, fp32 on the host cores
+        G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
+        D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=torch.float32, trainable=lambda k: True)
+        D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
+        opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
+        if act_bf16:
+            with R.bf16_activation_storage():
+                ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
+        else:
+            ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
+        _ORACLE_CACHE[key] = (ref, G, D1, D2)
+    return _ORACLE_CACHE[key]
+
+
 def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16=False, batch=1):
     """act_bf16: the oracle stores the Bottleneck activations in bf16 as the engine's bf16
     program does (R.bf16_activation_storage).  batch: images per domain (the bench's own batch
@@ -278,17 +304,7 @@ def _step_vs_oracle(geom, bn_train, gan, tol, trunk=True, d_bound=None, act_bf16
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     level, src, tgt = GEOMS[geom]
     xs, lab, xt = _batch(src, tgt, batch)
-    cfg = dict(level=level, gan=gan, input_size=src, input_size_target=tgt)
-    # oracle, fp32 on the host cores
-    G = R.to_torch(R.det_state(R.g_specs(), 1338), dtype=torch.float32, trainable=R.g_trainable)
-    D1 = R.to_torch(R.det_state(R.d_specs(), 2001), dtype=torch.float32, trainable=lambda k: True)
-    D2 = R.to_torch(R.det_state(R.d_specs(), 2002), dtype=torch.float32, trainable=lambda k: True)
-    opts = R.make_optimizers(G, D1 if level == "multi-level" else None, D2, R.DEFAULT_CFG | cfg)
-    if act_bf16:
-        with R.bf16_activation_storage():
-            ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
-    else:
-        ref = R.oracle_step(G, D1, D2, opts, cfg, 0, [(xs, lab, xt)], bn_train=bn_train)
+    ref, G, D1, D2 = _oracle_step(geom, bn_train, gan, act_bf16, batch)
     # HIP engine
     tr, m, d1, d2 = _hip_trainer(level, src, tgt, bn_train, gan=gan)
     got = tr.step(0, [(xs.to(DEV), lab.to(DEV), xt.to(DEV))]).values()

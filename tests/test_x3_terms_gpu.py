@@ -142,8 +142,9 @@ def test_conv_on_terms_matches_staged_kernel_and_fp64(shape):
     for op in (0, 1, 2):
         sel_t, sp_t = k.conv_kernel_id(geom, n, h, w, op, copies=True)
         sel_s, sp_s = k.conv_kernel_id(geom, n, h, w, op)
-        # without copies: the register-staged kernel
-        assert sel_t % 100 in (88, 89) and sel_s % 100 in (95, 96), (op, sel_t, sel_s)
+        # without copies: the register-staged kernel, or (ADAPTSEG_OPT_X3H, K >= 256) the same
+        # 256x128x32 tile splitting fp32 rows in-kernel
+        assert sel_t % 100 in (88, 89) and sel_s % 100 in (86, 87, 95, 96), (op, sel_t, sel_s)
     # forward
     ref = F.conv2d(x, wt, None, stride, pad, dil)
     y_s = k.conv_fwd(geom, xd, n, h, w, [wd])
