@@ -308,13 +308,19 @@ igemm_bf16g_kernel(const ConvParams p,
 // tile instead of twice; 8 waves of 64x32 (BM 128) or 64x64 (BM 256); 3-stage ring of 16 / 24
 // KB, two blocks per CU.  BN 256 (with BM 256): two B images, 8 waves of 64x128, a 3 x 32 KB ring
 // and one block per CU — half the operand bytes per MFMA of 256x128.
-// NS: LDS ring depth, NS - 1 K steps in flight across each barrier (3: two).
+// NS: LDS ring depth, NS - 1 K steps in flight across each barrier (3: two).  NS 2 with 256x256
+// ("wide", ADAPTSEG_OPT_G16_WIDE): 16 waves of 64x64 and K steps of 64 pixels (each wave DMAs four
+// k-rows of every image), two 64 KB stages, one step in flight — 16 MFMAs per wave and 2,048
+// MFMA cycles per SIMD between barriers (the 256x128 tile: 8 and 512) and half its operand bytes
+// per MFMA.
+constexpr int g16w_waves(int bm, int bn, int ns) { return (bm == 256 && bn == 256 && ns == 2) ? 16 : 8; }
 template <int BM, int BN = 128, int NS = kG16Stages>
-__global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16g_wgrad_kernel(
-    const ConvParams p, const __bf16 *__restrict__ dyb, const __bf16 *__restrict__ xb) {
-  constexpr int BKP = 32;
+__global__ void __launch_bounds__(64 * g16w_waves(BM, BN, NS), g16w_waves(BM, BN, NS) == 16 ? 4 : (BN == 256 || NS > 4) ? 1 : 2)
+igemm_bf16g_wgrad_kernel(const ConvParams p, const __bf16 *__restrict__ dyb, const __bf16 *__restrict__ xb) {
+  constexpr int NW = g16w_waves(BM, BN, NS);
+  constexpr int BKP = 4 * NW;                 // pixels per K step: four k-rows per wave
   static_assert(BN == 128 || (BN == 256 && BM == 256), "wgrad tiles 128x128, 256x128, 256x256");
-  constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  constexpr int WAVES_M = BM / 64, WAVES_N = NW / WAVES_M;
   constexpr int WTM = 64, WTN = BN / WAVES_N, TM = 2, TN = WTN / 32;
   constexpr int NA = BM / 128;                // A images / instructions per wave and K step
   constexpr int NB = BN / 128;                // B images
@@ -322,7 +328,7 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
   constexpr int STAGE = (NA + NB) * IMG;
   // (a 4- / 6-deep ring measured no faster, profiles/r5/g16_wgrad_ring_ab.txt: the K loop is
   // unrolled over exactly three stages)
-  static_assert(NS == 3 && NS * STAGE <= 160 * 1024, "ring depth");
+  static_assert((NS == 3 || (NS == 2 && NW == 16)) && NS * STAGE <= 160 * 1024, "ring depth");
 
   __shared__ __attribute__((aligned(16))) char lds[NS * STAGE];
 
@@ -423,9 +429,11 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
 
   // Every fragment read's per-lane byte offset within a ring stage (mc_frag's two transposed
   // reads, image base included), computed once: a read adds only the compile-time stage base,
-  // which the DS offset field absorbs (the K loop below is unrolled over the NS stages).
+  // which the DS offset field absorbs (the K loop below is unrolled over the NS stages).  Sub-step
+  // ks + 1 is 16 k-rows (4 KB) further with the same swizzle (mc_off: k-row bits 0-3): only the
+  // ks = 0 offsets are kept.
   constexpr int KS = BKP / 16;
-  uint32_t oa[TM][KS][2], ob[TN][KS][2];
+  uint32_t oa[TM][1][2], ob[TN][1][2];
   {
     const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
     auto offs = [&](int img, int c0, int ks, uint32_t (&o)[2]) {
@@ -437,12 +445,9 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
     const int ia = (wm * WTM / 128) * IMG, ib = (NA + (wn * WTN) / 128) * IMG;   // this wave's A / B image
     const int ar = (wm * WTM) % 128, bc = (wn * WTN) % 128;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int i = 0; i < TM; ++i) offs(ia, ar + i * 32, 0, oa[i][0]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) offs(ia, ar + i * 32, ks, oa[i][ks]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) offs(ib, bc + j * 32, ks, ob[j][ks]);
-    }
+    for (int j = 0; j < TN; ++j) offs(ib, bc + j * 32, 0, ob[j][0]);
   }
   const uint32_t lds_u32 = (uint32_t)(uintptr_t)lds;
   auto rd = [&](uint32_t base, const uint32_t (&o)[2]) -> bf16x8 {
@@ -457,9 +462,9 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
     bf16x8 a[2][TM], b[2][TN];
     auto read_frags = [&](int ks, int slot) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[slot][i] = rd(sb, oa[i][ks]);
+      for (int i = 0; i < TM; ++i) a[slot][i] = rd(sb + 4096 * ks, oa[i][0]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[slot][j] = rd(sb, ob[j][ks]);
+      for (int j = 0; j < TN; ++j) b[slot][j] = rd(sb + 4096 * ks, ob[j][0]);
     };
     read_frags(0, 0);
 #pragma unroll
@@ -474,7 +479,25 @@ __global__ void __launch_bounds__(512, (BN == 256 || NS > 4) ? 1 : 2) igemm_bf16
     }
   };
 
-  if (kt0 < kt1) {
+  if constexpr (NS == 2) {
+    if (kt0 < kt1) {   // two stages, one step in flight (issued after the barrier opening the step before)
+      issue(kt0, 0);
+      for (int kt = kt0; kt < kt1; kt += 2) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < kt1) issue(kt + 1, 1);
+        compute(std::integral_constant<int, 0>{});
+        if (kt + 1 >= kt1) break;
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 2 < kt1) issue(kt + 2, 0);
+        compute(std::integral_constant<int, 1>{});
+      }
+      __syncthreads();
+    }
+  } else if (kt0 < kt1) {
     // step kt lives in stage (kt - kt0) % NS; steps past the last re-read it into stages nobody
     // reads again, so every wave always has NS - 2 steps' NA + NB instructions outstanding
     const int klast = kt1 - 1;

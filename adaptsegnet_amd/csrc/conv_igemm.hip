@@ -548,7 +548,8 @@ void set_splits(Plan &pl) {
 #ifndef ADAPTSEG_X3_WGRAD_TARGET
 #define ADAPTSEG_X3_WGRAD_TARGET 384   // (a compile-time knob of experiment builds, EXTRA=-D...)
 #endif
-  constexpr int kX3WgradTarget = ADAPTSEG_X3_WGRAD_TARGET;
+  // (the environment variable ADAPTSEG_X3_WGRAD_TARGET overrides it, for A/B runs)
+  static const int kX3WgradTarget = env_int("ADAPTSEG_X3_WGRAD_TARGET", ADAPTSEG_X3_WGRAD_TARGET);
   // The LDS-DMA bf16 weight gradient (side stream) to ~256 blocks: half the split-K slab
   // traffic of 512, c5 +1.8 % same box (37.30 / 37.30 / 37.29 vs 36.64 / 36.65 / 36.62,
   // tools/dbg/ab_lib.sh).
@@ -741,7 +742,12 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
-      if (g16_wide_mode() && p.N >= 256 && p.K >= 2048 && !pl.s2) pl.g16_bm = 256;   // 256x256x64, two stages
+      // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs)
+      static const int wide_min_k = env_int("ADAPTSEG_G16_WIDE_MIN_K", 2048);
+      if (g16_wide_mode() && p.N >= 256 && p.K >= wide_min_k && !pl.s2) {
+        pl.g16_bm = 256;
+        pl.g16_bk = 64;
+      }
       // (256x256x32 tiles, one block per CU, measured slower: c5 -10 % / -2.4 % with the weight
       // gradients only, profiles/r3/bf16_wide_tiles_ab.txt; experiments/r3_rejected.patch)
     }
@@ -755,6 +761,11 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16_bm = d->k >= 256 ? 256 : 128;   // 256 rows: dY read once per column tile
       pl.g16_bn = 128;
       pl.g16_bk = 32;
+      // 256x256 with 64-pixel K steps (16 waves, two stages: ADAPTSEG_OPT_G16_WIDE)
+      if (g16_wide_mode() && d->k >= 256 && p.N >= 256) {
+        pl.g16_bn = 256;
+        pl.g16_bk = 64;
+      }
     }
   }
   // cfg 8 (occupancy-3 BK-16 tile) exists for vector FAST fwd / weight-grad products only
@@ -774,7 +785,7 @@ int kernel_id(const Plan &pl, int mode) {
   if (pl.x3r) return 100 * mode + 88 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
   // 86 / 87: the FAST cfg-8 per-element ids, which never occur (cfg 8 takes vector operands only)
   if (pl.x3h) return 100 * mode + 86 + ((mode == MODE_WGRAD ? pl.x3r_bm == 128 : pl.s2) ? 1 : 0);
-  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bm == 256 ? 98 : 99);
+  if (pl.g16 && mode == MODE_WGRAD) return 100 * mode + (pl.g16_bn == 256 ? 85 : pl.g16_bm == 256 ? 98 : 99);
   if (pl.g16 && pl.s2) return 100 * mode + (pl.g16_bn == 256 ? 92 : 93);
   // 85: the FAST cfg-8 id with per-element B, which never occurs (cfg 8: vector operands only)
   if (pl.g16 && pl.g16_bm == 256 && pl.g16_bn == 256) return 100 * mode + 85;

@@ -195,7 +195,8 @@ hipError_t launch_bf16(const Plan &pl, void *wpack, hipStream_t s) {
                                              base + al256(g16_act_elems(pl) * sizeof(__bf16)));
       // (a 6-deep ring for the 256x128 tile, 4-deep for 128x128 — five / three steps in flight
       // instead of two: per shape within +-3 %, c5 -0.6 %, profiles/r5/g16_wgrad_ring_ab.txt)
-      if (pl.g16_bm == 256) launch_k(igemm_bf16g_wgrad_kernel<256>, grid, block, s, p, act, act2);
+      if (pl.g16_bn == 256) launch_k(igemm_bf16g_wgrad_kernel<256, 256, 2>, grid, dim3(1024), s, p, act, act2);
+      else if (pl.g16_bm == 256) launch_k(igemm_bf16g_wgrad_kernel<256>, grid, block, s, p, act, act2);
       else launch_k(igemm_bf16g_wgrad_kernel<128>, grid, block, s, p, act, act2);
       return hipGetLastError();
     }

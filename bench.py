@@ -207,6 +207,8 @@ def selector_symbol(sel):
     if sel % 100 in (95, 96):
         return f"igemm_x3_kernel<{op}, {'true' if var == 6 else 'false'}>"
     if sel % 100 == 85:   # bf16 LDS-DMA 256x256x64, two stages
+        if op == 2:
+            return "igemm_bf16g_wgrad_kernel<256, 256, 2>"
         return f"igemm_bf16g_kernel<{op}, 256, 256, 64, false, 2>"
     if sel % 100 in (86, 87):   # F32X3, the same tiles with the fp32 operands split in-kernel
         if op == 2:

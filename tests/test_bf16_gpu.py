@@ -373,3 +373,21 @@ def test_bf16_wide_tile_matches_default_and_oracle(bf16_math, shape):
         assert torch.equal(y0, y1)
     if base[1][1] == 1 and wide[1][1] == 1:
         assert torch.equal(dx0, dx1)
+    # weight gradient: 256x256 tiles, 64-pixel K steps (selector 285) when Cout and N >= 256
+    wr = bf(wt).requires_grad_(True)
+    F.conv2d(bf(x), wr, None, stride, pad, dil).backward(bf(gy))
+    dws = []
+    for on in (False, True):
+        k.set_g16_wide(on)
+        try:
+            sel, sp = k.conv_kernel_id(geom, n, h, w, 2)
+            dw = torch.zeros_like(wd[0])
+            k.conv_wgrad(geom, gyd, xd, n, h, w, [dw], accumulate=False)
+        finally:
+            k.set_g16_wide(w0)
+        if on and cout >= 256 and ks * ks * cin >= 256:
+            assert sel == 285, sel
+        assert rel(dw.permute(0, 3, 1, 2).cpu(), wr.grad) < 2e-5
+        dws.append((dw, sp))
+    if dws[0][1] == 1 and dws[1][1] == 1:
+        assert torch.equal(dws[0][0], dws[1][0])

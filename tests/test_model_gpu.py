@@ -28,17 +28,26 @@ def _sd_torch(sd):
             for k, v in sd.items()}
 
 
+_SD_CACHE: dict = {}   # deterministic state dicts by (model, seed): the PCG64 draw of 44 M values once
+
+
+def _det_sd(kind, seed):
+    if (kind, seed) not in _SD_CACHE:
+        _SD_CACHE[(kind, seed)] = _sd_torch(R.det_state(R.g_specs() if kind == "g" else R.d_specs(), seed))
+    return _SD_CACHE[(kind, seed)]
+
+
 def build_g(seed=1338):
     from adaptsegnet_amd.model import DeeplabMulti
     m = DeeplabMulti(num_classes=19)
-    m.load_state_dict(_sd_torch(R.det_state(R.g_specs(), seed)))
+    m.load_state_dict(_det_sd("g", seed))
     return m.to(DEV)
 
 
 def build_d(seed):
     from adaptsegnet_amd.model import FCDiscriminator
     d = FCDiscriminator(num_classes=19)
-    d.load_state_dict(_sd_torch(R.det_state(R.d_specs(), seed)))
+    d.load_state_dict(_det_sd("d", seed))
     return d.to(DEV)
 
 

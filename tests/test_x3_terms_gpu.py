@@ -179,7 +179,9 @@ def test_fused_bn_statistics_on_terms():
     xd, wd = nhwc(x), w_cl(wt)
     y0, t0 = k.conv_fwd_bnstats(geom, xd, n, h, w, [wd])
     y1, t1 = k.conv_fwd_bnstats(geom, None, n, h, w, [wd], xb=terms(xd))
-    assert t0 is not None and t1 is not None and t1[1] * 2 == t0[1]
+    # 128-row tiles on the register-staged kernel, 256 on the x3h one (the default here, K 2304)
+    rows0 = 256 if k.conv_kernel_id(geom, n, h, w, 0)[0] % 100 == 86 else 128
+    assert t0 is not None and t1 is not None and t1[1] * 256 // rows0 == t0[1]
     assert torch.equal(y0, y1)   # neither splits K: bitwise the staged kernel
     bw, bb = torch.ones(cout, device=DEV), torch.zeros(cout, device=DEV)
     _, m0, i0 = k.bn_fwd_train_tiles(y0, t0, bw, bb, None, None, 0.1, 1e-5)
