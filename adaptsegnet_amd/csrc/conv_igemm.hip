@@ -323,8 +323,10 @@ int conv_math() { return g_conv_math.load(std::memory_order_relaxed); }
 //   ADAPTSEG_OPT_X3H (ADAPTSEG_X3H): bits 1 / 2 / 4 put the F32X3 forward / data-gradient /
 //     weight-gradient products the x3r tiles cover on igemm_x3h_kernel / igemm_x3hw_kernel
 //     (conv_x3r.hpp) instead of the register-staged 128x128x16 kernel;
-//   ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE): 1 = bf16 forward / data-gradient products with
-//     N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile (conv_bf16g.hpp).
+//   ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE): bit 1 = bf16 forward / data-gradient products with
+//     N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile, bit 2 = weight gradients
+//     with Cout and N >= 256 on the 256x256 / 64-pixel tile (conv_bf16g.hpp).  Default 1: c5 +1.9 %
+//     (profiles/r6/g16_wide_ab.txt); the weight-gradient tile measured -2.8 % on top of it.
 #ifndef ADAPTSEG_X3H_DEFAULT
 #define ADAPTSEG_X3H_DEFAULT 3
 #endif
@@ -744,7 +746,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
       // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs)
       static const int wide_min_k = env_int("ADAPTSEG_G16_WIDE_MIN_K", 2048);
-      if (g16_wide_mode() && p.N >= 256 && p.K >= wide_min_k && !pl.s2) {
+      if ((g16_wide_mode() & 1) && p.N >= 256 && p.K >= wide_min_k && !pl.s2) {
         pl.g16_bm = 256;
         pl.g16_bk = 64;
       }
@@ -762,7 +764,7 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16_bn = 128;
       pl.g16_bk = 32;
       // 256x256 with 64-pixel K steps (16 waves, two stages: ADAPTSEG_OPT_G16_WIDE)
-      if (g16_wide_mode() && d->k >= 256 && p.N >= 256) {
+      if ((g16_wide_mode() & 2) && d->k >= 256 && p.N >= 256) {
         pl.g16_bn = 256;
         pl.g16_bk = 64;
       }
@@ -1480,7 +1482,7 @@ int adaptseg_conv_set_option(int option, int value) {
     AS_CHECK_ARG(value >= 0 && value <= 7, "conv_set_option: X3H must be 0..7");
     g_opt_x3h.store(value);
   } else if (option == ADAPTSEG_OPT_G16_WIDE) {
-    AS_CHECK_ARG(value == 0 || value == 1, "conv_set_option: G16_WIDE must be 0 or 1");
+    AS_CHECK_ARG(value >= 0 && value <= 3, "conv_set_option: G16_WIDE must be 0..3");
     g_opt_g16_wide.store(value);
   } else {
     AS_CHECK_ARG(false, "conv_set_option: unknown option %d", option);

@@ -94,10 +94,11 @@ def get_x3h() -> int:
     return _ops.get_option(_ops.OPT_X3H)
 
 
-def set_g16_wide(on: bool) -> None:
-    """BF16: forward / data-gradient products with N >= 256 and K >= 2048 on the 256x256x64
-    two-stage LDS-DMA tile (ADAPTSEG_OPT_G16_WIDE; initial value from ADAPTSEG_G16_WIDE)."""
-    _ops.set_option(_ops.OPT_G16_WIDE, 1 if on else 0)
+def set_g16_wide(mode) -> None:
+    """BF16: bit 1 = forward / data-gradient products with N >= 256 and K >= 2048 on the
+    256x256x64 two-stage LDS-DMA tile, bit 2 = weight gradients on the 256x256 tile
+    (ADAPTSEG_OPT_G16_WIDE; initial value from ADAPTSEG_G16_WIDE, default 1).  True = 3."""
+    _ops.set_option(_ops.OPT_G16_WIDE, 3 if mode is True else int(mode))
 
 
 def get_g16_wide() -> int:

@@ -99,8 +99,10 @@ int adaptseg_conv_get_math(int *math);
        one tap) run on igemm_x3h_kernel / igemm_x3hw_kernel<128> — those tiles with the fp32 operands
        split in-kernel, no term images — instead of the register-staged 128x128x16 kernel.  Same
        arithmetic (bitwise the term-image kernels' results on the same plan).
-     ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE, default 0): BF16 maths, 1 = forward / data-gradient
-       products with N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA tile. */
+     ADAPTSEG_OPT_G16_WIDE (ADAPTSEG_G16_WIDE, default 1): BF16 maths, bit 1 = forward /
+       data-gradient products with N >= 256 and K >= 2048 on the 256x256x64 two-stage LDS-DMA
+       tile, bit 2 = weight gradients with Cout >= 256 and N >= 256 on the 256x256 tile with
+       64-pixel K steps. */
 enum adaptseg_conv_option { ADAPTSEG_OPT_X3H = 1, ADAPTSEG_OPT_G16_WIDE = 2 };
 int adaptseg_conv_set_option(int option, int value);
 int adaptseg_conv_get_option(int option, int *value);
