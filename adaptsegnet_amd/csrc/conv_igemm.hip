@@ -561,7 +561,9 @@ void set_splits(Plan &pl) {
                      : (pl.mode == MODE_WGRAD && pl.x3)            ? kX3WgradTarget
                                                                    : kSplitTarget;
   // the LDS-DMA bf16 / x3r kernels run one block per CU: split only grids under half the CUs
-  const int split_below = pl.mode == MODE_WGRAD ? target : (pl.x3r || pl.x3h) ? 256 : pl.g16 ? 128 : 257;
+  // (the 256x256 bf16 tile, one block per CU: split under 256 tiles, like x3r)
+  const bool g16w = pl.g16 && pl.g16_bm == 256 && pl.g16_bn == 256;
+  const int split_below = pl.mode == MODE_WGRAD ? target : (pl.x3r || pl.x3h || g16w) ? 256 : pl.g16 ? 128 : 257;
   int splits = 1;
   if (pl.mode == MODE_WGRAD && (pl.x3r || pl.x3h)) {
     // one 8-wave block per CU: the grid takes ceil(tiles * s / 256) rounds of 1/s of the K range,
@@ -746,7 +748,11 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
       // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs)
       static const int wide_min_k = env_int("ADAPTSEG_G16_WIDE_MIN_K", 2048);
-      if ((g16_wide_mode() & 1) && p.N >= 256 && p.K >= wide_min_k && !pl.s2) {
+      // ... and only where its grid fills the chip (>= 256 tiles): per shape l4.conv2 899 -> 1068
+      // TF/s on it, but l3.conv2 (128 wide tiles at the c2 geometry) 712 -> 551 (half the CUs idle)
+      static const int wide_min_tiles = env_int("ADAPTSEG_G16_WIDE_MIN_TILES", 256);   // (under 256: split-K to 256 blocks)
+      const int64_t wide_tiles = ceil_div(p.M, 256) * ceil_div(p.N, 256);
+      if ((g16_wide_mode() & 1) && p.N >= 256 && p.K >= wide_min_k && !pl.s2 && wide_tiles >= wide_min_tiles) {
         pl.g16_bm = 256;
         pl.g16_bk = 64;
       }

@@ -73,7 +73,8 @@ BF16_CASES = [
     (1, 128, 12, 14, 384, 3, 1, (1,), (1,), False),      # dgrad 256x128 / K step 64; wgrad 256-row tile, half-empty
     (2, 128, 19, 25, 128, 3, 2, (1,), (1,), False),      # stride-2 3x3 data gradient, LDS-DMA parity classes 256x128
     (2, 256, 16, 20, 128, 4, 2, (1,), (1,), True),       # D-style 4x4/2 (bias), parity classes on 128x256
-    (1, 256, 128, 256, 256, 3, 1, (2,), (2,), False),    # 256x256x64 two-stage tile (N 256, K 2304), 128 tiles: unsplit
+    (1, 2048, 86, 256, 768, 1, 1, (0,), (1,), False),    # 256x256x64 two-stage tile, forward (K 2048, 258 tiles)
+    (1, 768, 86, 256, 2048, 1, 1, (0,), (1,), False),    # ... data gradient (N 768, K 2048, 258 tiles)
 ]
 
 

@@ -159,12 +159,15 @@ def test_bf16_operand_abi_checks_on_host():
         g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
         # K 2304, N 256: the 256x256x64 two-stage tile (ADAPTSEG_OPT_G16_WIDE bit 1, the default);
         # bit 2 also puts the weight gradient on the 256x256 tile
+        # when its grid has >= 256 tiles (4 x 128 x 128 rows: 256 tiles; 4 x 64 x 128: 128, the
+        # 128x256 tile)
         assert K.get_g16_wide() == 1
-        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 298]
-        K.set_g16_wide(0)
         assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
+        assert [K.conv_kernel_id(g, 4, 128, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 298]
+        K.set_g16_wide(0)
+        assert [K.conv_kernel_id(g, 4, 128, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
         K.set_g16_wide(3)
-        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 285]
+        assert [K.conv_kernel_id(g, 4, 128, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 285]
         K.set_g16_wide(1)
         s2 = K.ConvGeom(256, 128, 1, 1, 2, (0,), (1,))
         assert K.conv_kernel_id(s2, 4, 128, 256, 1)[0] == 192    # stride-2 parity classes, LDS-DMA
