@@ -748,9 +748,11 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
       // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs)
       static const int wide_min_k = env_int("ADAPTSEG_G16_WIDE_MIN_K", 2048);
-      // ... and only where its grid fills the chip (>= 256 tiles): per shape l4.conv2 899 -> 1068
-      // TF/s on it, but l3.conv2 (128 wide tiles at the c2 geometry) 712 -> 551 (half the CUs idle)
-      static const int wide_min_tiles = env_int("ADAPTSEG_G16_WIDE_MIN_TILES", 256);   // (under 256: split-K to 256 blocks)
+      // ... and only where its grid holds >= 128 tiles (grids of 128-255 tiles split K to ~256
+      // blocks, set_splits): per shape l4.conv2 899 -> 1068 TF/s on it, l3.conv2 at c5's source
+      // geometry (225 tiles) 691 -> 893, at the c2 geometry (128 tiles) unsplit 712 -> 551
+      // (profiles/r6/g16_wide_ab.txt); the c5 step is within +-0.3 % of a 256-tile threshold
+      static const int wide_min_tiles = env_int("ADAPTSEG_G16_WIDE_MIN_TILES", 128);   // (under 256: split-K to 256 blocks)
       const int64_t wide_tiles = ceil_div(p.M, 256) * ceil_div(p.N, 256);
       if ((g16_wide_mode() & 1) && p.N >= 256 && p.K >= wide_min_k && !pl.s2 && wide_tiles >= wide_min_tiles) {
         pl.g16_bm = 256;

@@ -75,6 +75,8 @@ BF16_CASES = [
     (2, 256, 16, 20, 128, 4, 2, (1,), (1,), True),       # D-style 4x4/2 (bias), parity classes on 128x256
     (1, 2048, 86, 256, 768, 1, 1, (0,), (1,), False),    # 256x256x64 two-stage tile, forward (K 2048, 258 tiles)
     (1, 768, 86, 256, 2048, 1, 1, (0,), (1,), False),    # ... data gradient (N 768, K 2048, 258 tiles)
+    (1, 2048, 64, 256, 512, 1, 1, (0,), (1,), False),    # ... forward, 128 tiles: split K to 256 blocks
+    (1, 512, 64, 256, 2048, 1, 1, (0,), (1,), False),    # ... data gradient, 128 tiles: split K
 ]
 
 

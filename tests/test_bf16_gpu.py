@@ -328,9 +328,10 @@ def test_aspp_tap_gemm_reads_the_bf16_copy_bitwise(bf16_math):
 
 
 # (n, cin, h, w, cout, k, stride, pad, dil): the wide tile takes products with N >= 256, K >= 2048
-# and >= 256 tiles of 256x256 (a full chip); smaller grids keep the 128x256 tile
+# and >= 128 tiles of 256x256 (128-255: K split to ~256 blocks); smaller grids keep the 128x256 tile
 WIDE_SHAPES = [
     (2, 256, 24, 40, 256, 3, 1, 2, 2),     # layer3 conv2 class, 8 wide tiles: stays on 128x256
+    (1, 256, 64, 256, 512, 3, 1, 2, 2),    # forward on the wide tile, 128 tiles: split K
     (1, 256, 86, 256, 768, 3, 1, 2, 2),    # forward on the wide tile (K 2304, 258 tiles)
     (1, 768, 86, 256, 256, 3, 1, 2, 2),    # data gradient on the wide tile (N = Cin 768)
     (1, 2048, 96, 256, 704, 1, 1, 0, 1),   # the ASPP tap-GEMM's inner 1x1 (N 704: a ragged tile)
@@ -339,13 +340,14 @@ WIDE_SHAPES = [
 
 def _wide(n, cin, h, w, cout, ks, op):
     m, nn, kk = n * h * w, (cout if op == 0 else cin), ks * ks * (cin if op == 0 else cout)
-    return nn >= 256 and kk >= 2048 and -(-m // 256) * -(-nn // 256) >= 256
+    return nn >= 256 and kk >= 2048 and -(-m // 256) * -(-nn // 256) >= 128
 
 
 @pytest.mark.parametrize("shape", WIDE_SHAPES, ids=[f"w{i}" for i in range(len(WIDE_SHAPES))])
 def test_bf16_wide_tile_matches_default_and_oracle(bf16_math, shape):
     """ADAPTSEG_OPT_G16_WIDE: forward / data-gradient products with N >= 256, K >= 2048 and >= 256
-    tiles on the 256x256x64 two-stage LDS-DMA tile (selector 100*op + 85): the same k order per output as the
+    tiles on the 256x256x64 two-stage LDS-DMA tile (selector 100*op + 85; with 128-255 tiles, split K):
+    the same k order per output as the
     128x256 tile, so bitwise its result on an unsplit plan, and the bf16-rounded fp64 oracle
     within 2e-5 (model/deeplab_multi.py:70-71, 139-140: the c5 atrous products)."""
     k = bf16_math

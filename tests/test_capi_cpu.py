@@ -159,10 +159,11 @@ def test_bf16_operand_abi_checks_on_host():
         g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
         # K 2304, N 256: the 256x256x64 two-stage tile (ADAPTSEG_OPT_G16_WIDE bit 1, the default);
         # bit 2 also puts the weight gradient on the 256x256 tile
-        # when its grid has >= 256 tiles (4 x 128 x 128 rows: 256 tiles; 4 x 64 x 128: 128, the
-        # 128x256 tile)
+        # when its grid has >= 128 tiles (4 x 128 x 128 rows: 256 tiles; 4 x 64 x 128: 128, split K;
+        # 4 x 32 x 128: 64, the 128x256 tile)
         assert K.get_g16_wide() == 1
-        assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
+        assert [K.conv_kernel_id(g, 4, 32, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
+        assert [K.conv_kernel_id(g, 4, 64, 128, op) for op in (0, 1)] == [(85, 2), (185, 2)]
         assert [K.conv_kernel_id(g, 4, 128, 128, op)[0] for op in (0, 1, 2)] == [85, 185, 298]
         K.set_g16_wide(0)
         assert [K.conv_kernel_id(g, 4, 128, 128, op)[0] for op in (0, 1, 2)] == [97, 197, 298]
