@@ -746,7 +746,9 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
       // (tools/conv_bench.py, kernel time): l3.conv2 (K 2304) 706 vs 675 TF/s, l4.conv3 forward
       // (K 512) 483 vs 625, l4.conv1 data gradient (K 512) 488 vs 631
       pl.g16_bk = (p.K >= 2048 && !pl.s2) ? 64 : 32;   // parity classes: short K, step 32
-      // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs)
+      // 256x256x64, two stages (ADAPTSEG_G16_WIDE_MIN_K: the smallest K, for A/B runs; 512 / 256
+      // speed the 1x1 products up alone, -1.3 % conv time, but cost the c5 step 0.3 %:
+      // profiles/r6/g16_wide_min_k_ab.txt)
       static const int wide_min_k = env_int("ADAPTSEG_G16_WIDE_MIN_K", 2048);
       // ... and only where its grid holds >= 128 tiles (grids of 128-255 tiles split K to ~256
       // blocks, set_splits): per shape l4.conv2 899 -> 1068 TF/s on it, l3.conv2 at c5's source
