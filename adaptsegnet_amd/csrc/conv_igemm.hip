@@ -24,6 +24,7 @@
 #include "conv_thin.hpp"
 #include <cstdlib>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 namespace adaptseg {
@@ -831,7 +832,47 @@ static bool splitk_vec(const ConvParams &q, const float *slab, const float *fina
   return vec;
 }
 
-int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
+// The split-K sum of one product (q.out: the final output; slab: its splits' partial outputs)
+static int splitk_sum(const ConvParams &q, const float *slab, int mode, hipStream_t s) {
+  const size_t total = (size_t)q.M * q.N;
+  const bool vec = splitk_vec(q, slab, q.out, mode);
+  int slot;  // the slabs + read-modify-write operands in, the output out
+  const int extra = (q.flags & ADAPTSEG_EPI_ACCUMULATE ? 1 : 0) +
+                    (mode != MODE_WGRAD && (q.flags & ADAPTSEG_EPI_RESIDUAL) ? 1 : 0) +
+                    (mode != MODE_WGRAD && (q.flags & kEpiActGrad) ? 1 : 0);
+  timing_begin(kTSplitkReduce, s, 4.0 * (double)total * (q.splits + 1 + extra), &slot);
+  if (vec) {
+    const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
+    const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
+    // grid cap: 512 / 1024 / 8192 measured within +-0.2 %
+    const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
+    if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
+    else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
+    else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
+  } else {
+    int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
+  }
+  timing_end(slot, s);
+  AS_CHECK_LAUNCH("splitk_reduce");
+  return ADAPTSEG_OK;
+}
+
+// Deferred split-K sums (adaptseg_splitk_flush): per stream, in launch order.  A weight
+// gradient's sum only feeds the optimiser, so its launch can wait until the backward has
+// queued every weight-gradient GEMM.  Removing the sums outright is worth c2 +8 %, c5 +3 %
+// (profiles/r6/sol_diag.txt, about twice their kernel time); deferring them to the end of the
+// backward measured c2 -1.0 %, c5 -1.3 % (profiles/r6/splitk_defer_ab.txt: the work stays on
+// the weight-gradient stream, now at its tail), so the engine keeps it off (ADAPTSEG_DEFER_SPLITK).
+struct PendingSum {
+  ConvParams q;
+  const float *slab;
+  int mode;
+};
+static std::mutex g_pending_mu;
+static std::unordered_map<hipStream_t, std::vector<PendingSum>> g_pending;
+
+int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s, bool defer) {
   float *final_out = pl.p.out;
   if (!ws || ws_bytes < pl.slab_bytes) {
     if (pl.slab_bytes) {
@@ -871,27 +912,12 @@ int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s) {
   if (pl.p.splits > 1) {
     ConvParams q = pl.p;
     q.out = final_out;
-    const size_t total = (size_t)q.M * q.N;
-    const bool vec = splitk_vec(q, slab, final_out, mode);
-    int slot;  // the slabs + read-modify-write operands in, the output out
-    const int extra = (q.flags & ADAPTSEG_EPI_ACCUMULATE ? 1 : 0) +
-                      (mode != MODE_WGRAD && (q.flags & ADAPTSEG_EPI_RESIDUAL) ? 1 : 0) +
-                      (mode != MODE_WGRAD && (q.flags & kEpiActGrad) ? 1 : 0);
-    timing_begin(kTSplitkReduce, s, 4.0 * (double)total * (q.splits + 1 + extra), &slot);
-    if (vec) {
-      const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
-      const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
-      // grid cap: 512 / 1024 / 8192 measured within +-0.2 %
-      const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
-      if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
-      else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
-      else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
-    } else {
-      int blocks = (int)std::min<size_t>(ceil_div(total, 256), 4096);
-      splitk_reduce_kernel<<<blocks, 256, 0, s>>>(q, slab, mode);
+    if (defer && mode == MODE_WGRAD) {   // the sum runs at adaptseg_splitk_flush(s)
+      std::lock_guard<std::mutex> lk(g_pending_mu);
+      g_pending[s].push_back(PendingSum{q, slab, mode});
+      return ADAPTSEG_OK;
     }
-    timing_end(slot, s);
-    AS_CHECK_LAUNCH("splitk_reduce");
+    return splitk_sum(q, slab, mode, s);
   }
   return ADAPTSEG_OK;
 }
@@ -1447,7 +1473,11 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
     AS_CHECK_ARG((dy && x) || ((pl.g16 || pl.x3ext) && pl.act_ext),
                  "conv bwd_weight: dy / x is NULL but the plan (after the alignment checks) needs the fp32 operands");
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
-    st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s);
+    // a deferred sum keeps its slabs in ws until the flush: not with a bias gradient, whose
+    // partial sums reuse the start of ws right after this GEMM
+    bool any_db = false;
+    for (int g = 0; db && g < d->nseg; ++g) any_db |= db[g] != nullptr;
+    st = run_plan(pl, MODE_WGRAD, ws, ws_bytes, s, (flags & ADAPTSEG_WGRAD_DEFER_SUM) && !any_db);
   }
   if (st) return st;
   if (db) {
@@ -1505,6 +1535,29 @@ int adaptseg_conv_get_option(int option, int *value) {
   if (option == ADAPTSEG_OPT_X3H) *value = x3h_mode();
   else if (option == ADAPTSEG_OPT_G16_WIDE) *value = g16_wide_mode();
   else AS_CHECK_ARG(false, "conv_get_option: unknown option %d", option);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_splitk_flush(adaptseg_stream_t stream) {
+  const hipStream_t s = as_stream(stream);
+  std::vector<PendingSum> v;
+  {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    auto it = g_pending.find(s);
+    if (it != g_pending.end()) v.swap(it->second);
+  }
+  for (const PendingSum &e : v) {
+    const int st = splitk_sum(e.q, e.slab, e.mode, s);
+    if (st) return st;
+  }
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_splitk_pending(adaptseg_stream_t stream, int *count) {
+  AS_CHECK_ARG(count, "splitk_pending: null");
+  std::lock_guard<std::mutex> lk(g_pending_mu);
+  auto it = g_pending.find(as_stream(stream));
+  *count = it == g_pending.end() ? 0 : (int)it->second.size();
   return ADAPTSEG_OK;
 }
 

@@ -1743,7 +1743,9 @@ double conv_flops(const adaptseg_conv_desc *d);
 void set_splits(Plan &pl);
 int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl);
 int kernel_id(const Plan &pl, int mode);
-int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s);
+// defer: a weight gradient whose plan splits K leaves its sum pending on stream s
+// (adaptseg_splitk_flush) instead of launching it
+int run_plan(Plan &pl, int mode, void *ws, size_t ws_bytes, hipStream_t s, bool defer = false);
 
 // Tap-GEMM path for stride-1 'same' convs with Cout <= 32 (ASPP): conv_tapgemm.hip.
 bool tapgemm_eligible(const adaptseg_conv_desc *d);

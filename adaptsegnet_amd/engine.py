@@ -62,8 +62,16 @@ class WgradStream:
             t.record_stream(self.side)
         self.used = True
 
+    def flush(self):
+        """Launch the split-K sums the weight gradients left pending on the side stream
+        (DEFER_SPLITK): before anything reads the gradients they write."""
+        if self.used and DEFER_SPLITK:
+            with torch.cuda.stream(self.side):
+                K.splitk_flush()
+
     def join(self):
         if self.used:
+            self.flush()
             self.main.wait_stream(self.side)
             self.used = False
 
@@ -124,6 +132,14 @@ def switches() -> dict:
 
 # (A/B switch) bf16 gradient storage under the BF16 maths
 BF16_GRADS = _switch("ADAPTSEG_BF16_GRADS", 1, (0, 1))
+
+# (A/B switch) the weight gradients' split-K sums deferred to the end of each backward
+# (WgradStream.flush, adaptseg.h ADAPTSEG_WGRAD_DEFER_SUM): the same sums, bitwise, launched
+# back to back once every weight-gradient GEMM is queued instead of one after each GEMM.
+# Measured slower (c2 -1.0 %, c3 -1.4 %, c5 -1.3 %, profiles/r6/splitk_defer_ab.txt): the sums
+# still run on the weight-gradient stream, now all at its tail, on slabs that went cold —
+# off by default
+DEFER_SPLITK = _switch("ADAPTSEG_DEFER_SPLITK", 0, (0, 1))
 
 
 def lowp_grads() -> bool:
@@ -349,7 +365,8 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None, dyb=None, xb=None
     """Weight gradient of one conv: on the side stream when ``ws`` is given.  dyb / xb: bf16
     copies of both operands (bf16 conv math)."""
     def run():
-        K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides, dyb=dyb, xb=xb)
+        K.conv_wgrad(g, dy, x, n, h, w, dws, dbs, strides=strides, dyb=dyb, xb=xb,
+                     defer=ws is not None and DEFER_SPLITK == 1)
     if ws is None:
         run()
     else:
@@ -585,7 +602,9 @@ class _DeeplabMultiFn(torch.autograd.Function):
         def done(ordinal):
             # a backward unit's weight gradients are queued (on the side stream): the
             # data-parallel hook may start all-reducing the gradient buckets now complete
+            # (their deferred split-K sums first)
             if hook is not None:
+                ws.flush()
                 hook(ordinal, ws.side)
 
         # unit ordinals follow DeeplabMulti._bwd_units

@@ -371,13 +371,25 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, n: int, h: int, w: int, weights, o
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, n: int, h: int, w: int, dws,
-               dbs=None, strides=None, accumulate: bool = True, dyb=None, xb=None) -> None:
+               dbs=None, strides=None, accumulate: bool = True, dyb=None, xb=None, defer: bool = False) -> None:
     """dw_seg (+)= sum dy (x) x_gathered ; db_seg (+)= sum dy.  dyb / xb: bf16 copies of the
     operands (bf16 conv math): the LDS-DMA weight-gradient kernel uses them together; the
-    tap-GEMM (ASPP) path uses xb alone (its dY operand is its own scattered buffer)."""
+    tap-GEMM (ASPP) path uses xb alone (its dY operand is its own scattered buffer).
+    defer: a split-K sum into dw is left pending on the current stream until splitk_flush()
+    (adaptseg.h ADAPTSEG_WGRAD_DEFER_SUM); dw must not be read before it."""
     strides = strides or nhwc_strides(n, h, w, g.cin)
+    flags = (EPI_ACCUMULATE if accumulate else 0) | (_ops.WGRAD_DEFER_SUM if defer else 0)
     _OP.conv2d_bwd_weight(dy, dyb, x, xb, list(dws), list(dbs) if dbs is not None else [], (n, g.cin, h, w), strides,
-                          _wshape(g), g.stride, g.pads, g.dils, EPI_ACCUMULATE if accumulate else 0)
+                          _wshape(g), g.stride, g.pads, g.dils, flags)
+
+
+def splitk_flush() -> None:
+    """Launch the split-K sums deferred on the current stream (conv_wgrad(..., defer=True))."""
+    _ops.splitk_flush()
+
+
+def splitk_pending() -> int:
+    return _ops.splitk_pending()
 
 
 # ---------------------------------------------------------------------------------------

@@ -303,12 +303,41 @@ def _conv2d_bwd_data_bnsum(dy, dyb, weight, wpack, res, resbits, dx, dxb, in_sha
      "int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, int flags) -> ()")
 def _conv2d_bwd_weight(dy, dyb, x, xb, dw, db, in_shape, in_stride, w_shape, stride, pad, dil, flags):
     d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
-    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dw[0].device)
+    if flags & WGRAD_DEFER_SUM:
+        # a deferred split-K sum reads this call's partial outputs at the flush: a workspace of
+        # its own, kept until splitk_flush (allocated on the current stream, where the flush runs)
+        nb = ws[CONV_BWD_WEIGHT]
+        w = torch.empty(nb, dtype=torch.uint8, device=dw[0].device) if nb else None
+        if w is not None:
+            _DEFERRED_WS.setdefault(torch.cuda.current_stream(dw[0].device).cuda_stream, []).append(w)
+        wp, wsz = (ctypes.c_void_p(w.data_ptr()) if w is not None else None), ctypes.c_size_t(nb)
+    else:
+        wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dw[0].device)
     nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
     check(_lib.lib().adaptseg_conv2d_bwd_weight_x(
         ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_weight dy"), _pc(dyb, ny, "conv2d_bwd_weight dyb"),
         _pf(x, nx, "conv2d_bwd_weight x"), _pc(xb, nx, "conv2d_bwd_weight xb"), _ptrs(dw),
         _ptrs(db) if len(db) else None, flags, wp, wsz, _stream()), "conv2d_bwd_weight")
+
+
+WGRAD_DEFER_SUM = 64   # adaptseg.h ADAPTSEG_WGRAD_DEFER_SUM
+_DEFERRED_WS: dict = {}   # stream handle -> workspaces of the weight gradients whose sums are pending
+
+
+def splitk_flush(device=None) -> None:
+    """adaptseg_splitk_flush on the current stream: launch the split-K sums the weight gradients
+    issued with WGRAD_DEFER_SUM left pending on it, then release their workspaces (freed in
+    stream order: the caching allocator reuses them only after the sums on this stream)."""
+    s = torch.cuda.current_stream(device)
+    check(_lib.lib().adaptseg_splitk_flush(ctypes.c_void_p(s.cuda_stream)), "splitk_flush")
+    _DEFERRED_WS.pop(s.cuda_stream, None)
+
+
+def splitk_pending(device=None) -> int:
+    n = ctypes.c_int(0)
+    s = torch.cuda.current_stream(device)
+    check(_lib.lib().adaptseg_splitk_pending(ctypes.c_void_p(s.cuda_stream), ctypes.byref(n)), "splitk_pending")
+    return n.value
 
 
 # ---- batch norm (x as [rows, C]: the NHWC buffer) ------------------------------------------

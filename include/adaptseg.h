@@ -68,7 +68,8 @@ enum adaptseg_conv_flags {
   ADAPTSEG_EPI_LEAKY_GRAD = 4, /* bwd_data: dx *= (aux > 0 ? 1 : 0.2)                      */
   ADAPTSEG_EPI_RESIDUAL = 8,   /* out = result + res (same NHWC shape as out)              */
   ADAPTSEG_EPI_RELU = 16,      /* fwd: y = relu(y)  (deeplab_vgg.py:34-43 conv + ReLU)     */
-  ADAPTSEG_EPI_RELU_GRAD = 32  /* bwd_data: dx *= (aux > 0 ? 1 : 0)                        */
+  ADAPTSEG_EPI_RELU_GRAD = 32, /* bwd_data: dx *= (aux > 0 ? 1 : 0)                        */
+  ADAPTSEG_WGRAD_DEFER_SUM = 64 /* bwd_weight: leave a split-K sum pending (adaptseg_splitk_flush) */
 };
 
 /* Conv arithmetic, process-wide (set before sizing workspaces; every conv entry point and
@@ -256,10 +257,25 @@ int adaptseg_conv2d_bwd_data(const adaptseg_conv_desc *d, const float *dy, const
                              size_t ws_bytes, adaptseg_stream_t stream);
 
 /* dw[seg][k,kh,kw,c] (+)= sum_{n,oh,ow} dy * x_gathered; db[seg][k] (+)= sum dy.
-   db may be NULL.  Only ADAPTSEG_EPI_ACCUMULATE is honoured. */
+   db may be NULL.  Only ADAPTSEG_EPI_ACCUMULATE and ADAPTSEG_WGRAD_DEFER_SUM are honoured. */
 int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, const float *x,
                                float *const *dw, float *const *db, int flags, void *ws,
                                size_t ws_bytes, adaptseg_stream_t stream);
+
+/* Deferred split-K sums of weight gradients (round 6).  With ADAPTSEG_WGRAD_DEFER_SUM in
+   `flags`, a weight gradient whose plan splits K writes its partial outputs into `ws` and
+   returns with their sum into dw pending on `stream` (a call that also computes a bias gradient
+   db sums immediately: its bias partials reuse the workspace);
+   adaptseg_splitk_flush(stream) launches every pending sum of that stream on it, in the order
+   the products were issued, and clears the list — bitwise the same dw as the immediate sum.
+   Until the flush the caller keeps each deferred call's workspace alive and unshared (the
+   partial outputs live there) and reads no deferred dw.  A product that does not split K
+   writes dw in its GEMM as usual.  The PyTorch binding: ops.splitk_flush(); the engine's weight
+   gradient stream flushes when it joins (engine.WgradStream, ADAPTSEG_DEFER_SPLITK).
+   Replaces nothing in the reference (its weight gradients are cuDNN's, inside autograd). */
+int adaptseg_splitk_flush(adaptseg_stream_t stream);
+/* number of sums pending on `stream` */
+int adaptseg_splitk_pending(adaptseg_stream_t stream, int *count);
 
 /* ------------------------------------------------------------------------------------ */
 /* BatchNorm2d, train mode (batch statistics) with fused residual add and ReLU.          */
