@@ -145,6 +145,8 @@ _SIGS = {
     "adaptseg_conv_get_option": [_I, ctypes.POINTER(_I)],
     "adaptseg_splitk_flush": [_P],
     "adaptseg_splitk_pending": [_P, ctypes.POINTER(_I)],
+    "adaptseg_stream_create_cu_mask": [_I, _I, ctypes.POINTER(_P)],
+    "adaptseg_stream_destroy": [_P],
     "adaptseg_timing_enable": [_I, _I],
     "adaptseg_timing_enable_mem": [_I],
     "adaptseg_timing_read_id": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

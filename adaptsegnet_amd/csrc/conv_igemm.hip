@@ -1591,6 +1591,37 @@ int adaptseg_timing_reserve(int64_t pairs) {
   return ADAPTSEG_OK;
 }
 
+int adaptseg_stream_create_cu_mask(int k, int d, adaptseg_stream_t *stream) {
+  AS_CHECK_ARG(stream && d > 0 && k > 0 && k <= d, "stream_create_cu_mask: bad arguments (k=%d d=%d)", k, d);
+  int dev = 0, ncu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) {
+    set_error("stream_create_cu_mask: %s", hipGetErrorString(e));
+    return ADAPTSEG_ERR_HIP;
+  }
+  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i)
+    if (i % d < k) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) {
+    set_error("hipExtStreamCreateWithCUMask: %s", hipGetErrorString(e));
+    return ADAPTSEG_ERR_HIP;
+  }
+  *stream = reinterpret_cast<adaptseg_stream_t>(s);
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_stream_destroy(adaptseg_stream_t stream) {
+  hipError_t e = hipStreamDestroy(as_stream(stream));
+  if (e != hipSuccess) {
+    set_error("hipStreamDestroy: %s", hipGetErrorString(e));
+    return ADAPTSEG_ERR_HIP;
+  }
+  return ADAPTSEG_OK;
+}
+
 int adaptseg_timing_enable_stream(int enable) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.stream_too = enable != 0;

@@ -50,9 +50,20 @@ class WgradStream:
         self.main = torch.cuda.current_stream(device)
         side = WgradStream._streams.get(device.index)
         if side is None:
-            side = WgradStream._streams[device.index] = torch.cuda.Stream(device)
+            side = WgradStream._streams[device.index] = WgradStream._new_stream(device)
         self.side = side
         self.used = False
+
+    @staticmethod
+    def _new_stream(device):
+        """The side stream; ADAPTSEG_WGRAD_CU_MASK="k/d" restricts it to the CUs i with
+        i % d < k (adaptseg_stream_create_cu_mask), leaving the rest to the main chain."""
+        spec = _os.environ.get("ADAPTSEG_WGRAD_CU_MASK", "")
+        if not spec:
+            return torch.cuda.Stream(device)
+        k, d = (int(v) for v in spec.split("/"))
+        with torch.cuda.device(device):
+            return torch.cuda.ExternalStream(K.stream_create_cu_mask(k, d), device=device)
 
     def launch(self, fn, *tensors):
         self.side.wait_stream(self.main)
@@ -140,6 +151,9 @@ BF16_GRADS = _switch("ADAPTSEG_BF16_GRADS", 1, (0, 1))
 # still run on the weight-gradient stream, now all at its tail, on slabs that went cold —
 # off by default
 DEFER_SPLITK = _switch("ADAPTSEG_DEFER_SPLITK", 0, (0, 1))
+
+# (A/B switch) weight gradients on the side stream (WgradStream; 0: inline on the main stream)
+WGRAD_STREAM = _switch("ADAPTSEG_WGRAD_STREAM", 1, (0, 1))
 
 
 def lowp_grads() -> bool:
@@ -596,7 +610,7 @@ class _DeeplabMultiFn(torch.autograd.Function):
             if g1_up is not None:
                 idx += model._pidx["layer5"]
             model._arena.claim(idx)
-        ws = WgradStream(ctx.x.device) if need_w else None
+        ws = WgradStream(ctx.x.device) if need_w and WGRAD_STREAM else None
         hook = model._grad_hook if need_w else None
 
         def done(ordinal):
@@ -604,8 +618,9 @@ class _DeeplabMultiFn(torch.autograd.Function):
             # data-parallel hook may start all-reducing the gradient buckets now complete
             # (their deferred split-K sums first)
             if hook is not None:
-                ws.flush()
-                hook(ordinal, ws.side)
+                if ws is not None:
+                    ws.flush()
+                hook(ordinal, ws.side if ws is not None else None)
 
         # unit ordinals follow DeeplabMulti._bwd_units
         n4 = len(model.layer4)
@@ -710,7 +725,7 @@ def _disc_backward(model, acts, actsb, dims, n, gout, need_w, need_dx):
     g = K.nhwc_view(gout)
     if not g.is_contiguous():
         g = g.contiguous()
-    ws = WgradStream(g.device) if need_w else None
+    ws = WgradStream(g.device) if need_w and WGRAD_STREAM else None
     dx, gb = None, None
     for i in reversed(range(len(convs))):
         conv = convs[i]
@@ -903,7 +918,7 @@ class _DeeplabVGGFn(torch.autograd.Function):
         gc = _branches_geom(branches)
         a, ch, cw = ctx.cls_in
         ctx.cls_in = None
-        ws = WgradStream(g.device) if need_w else None
+        ws = WgradStream(g.device) if need_w and WGRAD_STREAM else None
         if need_w and branches[0].weight.grad is not None:
             _wgrad(ws, gc, g, a, n, ch, cw, [b.weight.grad for b in branches],
                    [b.bias.grad for b in branches])
@@ -1066,7 +1081,7 @@ class _WarperFn(torch.autograd.Function):
         g = K.nhwc_view(gflow)
         if not g.is_contiguous():
             g = g.contiguous()
-        ws = WgradStream(g.device) if need_w else None
+        ws = WgradStream(g.device) if need_w and WGRAD_STREAM else None
 
         def wgrad(conv, dy, xin, hh, ww, strides=None):
             if need_w and conv.weight.grad is not None:

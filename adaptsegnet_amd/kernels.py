@@ -392,6 +392,14 @@ def splitk_pending() -> int:
     return _ops.splitk_pending()
 
 
+def stream_create_cu_mask(k: int, d: int) -> int:
+    """A HIP stream on the CUs i with i % d < k (adaptseg_stream_create_cu_mask); returns the
+    handle (wrap it with torch.cuda.ExternalStream)."""
+    h = ctypes.c_void_p(0)
+    _lib.check(_lib.lib().adaptseg_stream_create_cu_mask(int(k), int(d), ctypes.byref(h)), "stream_create_cu_mask")
+    return h.value
+
+
 # ---------------------------------------------------------------------------------------
 # BatchNorm (x as [rows, C])
 # ---------------------------------------------------------------------------------------

@@ -590,6 +590,14 @@ int adaptseg_timing_read_id(int kernel_id, double *total_ms, double *total_units
 int adaptseg_timing_enable_stream(int enable);
 int adaptseg_timing_read_id_stream(int kernel_id, double *total_ms, int64_t *launches);
 
+/* A stream restricted to a subset of the device's compute units (hipExtStreamCreateWithCUMask):
+   CU i is enabled when i % d < k (a stride pattern, so every XCD keeps k / d of its CUs whatever
+   the logical CU numbering).  For the engine's weight-gradient stream (ADAPTSEG_WGRAD_CU_MASK):
+   its GEMM blocks then occupy only those CUs, and the main chain's one-block-per-CU tiles keep
+   the rest.  The stream lives until adaptseg_stream_destroy. */
+int adaptseg_stream_create_cu_mask(int k, int d, adaptseg_stream_t *stream);
+int adaptseg_stream_destroy(adaptseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
