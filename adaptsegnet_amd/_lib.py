@@ -43,6 +43,12 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class OperandBN(ctypes.Structure):
+    """adaptseg_operand_bn (include/adaptseg.h)."""
+    _fields_ = [("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+                ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p)]
+
+
 class BnSumDesc(ctypes.Structure):
     """adaptseg_bnsum_desc (include/adaptseg.h)."""
     _fields_ = [
@@ -70,6 +76,11 @@ _SIGS = {
     "adaptseg_conv2d_kernel_id": [_DESC, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
     "adaptseg_conv2d_kernel_id_x": [_DESC, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
     "adaptseg_conv2d_copy_operand_only": [_DESC, _I, ctypes.POINTER(_I)],
+    "adaptseg_conv2d_operand_bn_ok": [_DESC, _I, ctypes.POINTER(_I)],
+    "adaptseg_conv2d_fwd_bnstats_abn": [_DESC, _P, ctypes.POINTER(OperandBN), _PP, _P, _P, _P, _SZ,
+                                        ctypes.POINTER(ctypes.c_int), _P, _SZ, _P],
+    "adaptseg_conv2d_bwd_weight_abn": [_DESC, _P, _P, ctypes.POINTER(OperandBN), _PP, _I, _P, _SZ, _P],
+    "adaptseg_bn_fwd_train_tiles_stats": [_L, _I, _P, _I, _P, _P, _F, _F, _P, _P, _P],
     "adaptseg_conv2d_fwd": [_DESC, _P, _PP, _PP, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_data": [_DESC, _P, _PP, _P, _P, _P, _I, _P, _SZ, _P],
     "adaptseg_conv2d_bwd_weight": [_DESC, _P, _P, _PP, _PP, _I, _P, _SZ, _P],

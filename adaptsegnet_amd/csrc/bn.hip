@@ -18,10 +18,8 @@
 namespace adaptseg {
 
 // ReLU mask without reading y: y > 0  <=>  (x - mean)*invstd*w + b > 0, evaluated with the
-// same expression bn_apply2d_kernel uses (valid for BNs without a residual input).
-__device__ __forceinline__ float bn_affine(float v, float m, float is, float w, float b) {
-  return (v - m) * is * w + b;
-}
+// same expression bn_apply2d_kernel uses (bn_affine, common.hpp; valid for BNs without a
+// residual input).
 __device__ __forceinline__ float4 relu_mask_from_x(float4 g, float4 v, float4 m, float4 is, float4 w, float4 b) {
   g.x = bn_affine(v.x, m.x, is.x, w.x, b.x) > 0.f ? g.x : 0.f;
   g.y = bn_affine(v.y, m.y, is.y, w.y, b.y) > 0.f ? g.y : 0.f;
@@ -994,6 +992,18 @@ int adaptseg_bn_fwd_train_tiles_xm(int64_t rows, int c, const float *stats, int 
                relu_bits);
   timing_end(slot, s);
   AS_CHECK_LAUNCH("bn_apply");
+  return ADAPTSEG_OK;
+}
+
+int adaptseg_bn_fwd_train_tiles_stats(int64_t rows, int c, const float *stats, int ntiles, float *running_mean,
+                                      float *running_var, float momentum, float eps, float *save_mean,
+                                      float *save_invstd, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(rows > 1 && c > 0 && c % 4 == 0, "bn_fwd_train_tiles_stats: rows>1, C%%4==0 required (C=%d)", c);
+  AS_CHECK_ARG(stats && ntiles > 0 && save_mean && save_invstd, "bn_fwd_train_tiles_stats: null pointer");
+  hipStream_t s = as_stream(stream);
+  bn_tiles_final_kernel<<<(unsigned)ceil_div(c, 4), 256, 0, s>>>(c, ntiles, stats, save_mean, save_invstd,
+                                                                   running_mean, running_var, momentum, eps);
+  AS_CHECK_LAUNCH("bn_tiles_final");
   return ADAPTSEG_OK;
 }
 

@@ -69,6 +69,17 @@ __device__ __forceinline__ float epi_act_grad(float v, float a, int flags) {
 }
 constexpr int kEpiActGrad = ADAPTSEG_EPI_LEAKY_GRAD | ADAPTSEG_EPI_RELU_GRAD;
 
+// The train-mode BatchNorm affine, (x - mean) * invstd * w + b: one expression for every kernel
+// that evaluates it (bn.hip's apply passes and mask recomputation, the conv kernels' operand-BN
+// gathers), so their results agree bit for bit
+__device__ __forceinline__ float bn_affine(float v, float m, float is, float w, float b) {
+  return (v - m) * is * w + b;
+}
+// bn_apply2d_kernel's BN + ReLU output of one element (no residual): fwd_act(affine + 0, ReLU)
+__device__ __forceinline__ float bn_relu(float v, float m, float is, float w, float b) {
+  return fmaxf(bn_affine(v, m, is, w, b) + 0.f, 0.f);
+}
+
 // F32X3 operand split: v = hi + mid + lo EXACTLY, each term the RNE bf16 of what is left
 // (3 x 8 significant bits cover fp32's 24; bf16 has fp32's exponent range).  The conv kernels
 // split their staged operands with it and the BatchNorm passes write the term images the

@@ -1081,6 +1081,34 @@ int adaptseg_conv2d_kernel_id_x(const adaptseg_conv_desc *d, int op, int with_co
   return ADAPTSEG_OK;
 }
 
+// The products with an operand-BN kernel (adaptseg_operand_bn): the x3h forward (selector 86)
+// and the register-staged F32X3 weight gradient (295), on a BN of at most kAbnMaxC channels
+static bool abn_plan_ok(const Plan &pl, const adaptseg_conv_desc *d, int op) {
+  if (d->c > kAbnMaxC || d->c % 4 || d->nseg != 1 || use_thin(d, op) || tapgemm_eligible(d)) return false;
+  const int kid = ::adaptseg::kernel_id(pl, op);
+  return (op == ADAPTSEG_CONV_FWD && kid == 86) || (op == ADAPTSEG_CONV_BWD_WEIGHT && kid == 295);
+}
+
+int adaptseg_conv2d_operand_bn_ok(const adaptseg_conv_desc *d, int op, int *ok) {
+  AS_CHECK_ARG(ok, "conv2d_operand_bn_ok: null");
+  *ok = 0;
+  Plan pl;
+  int st = make_plan(d, op, pl);
+  if (st) return st;
+  if (op != ADAPTSEG_CONV_FWD && op != ADAPTSEG_CONV_BWD_WEIGHT) return ADAPTSEG_OK;
+  set_splits(pl);
+  x3_terms(pl);
+  *ok = abn_plan_ok(pl, d, op) ? 1 : 0;
+  return ADAPTSEG_OK;
+}
+
+static void set_abn(ConvParams &p, const adaptseg_operand_bn *abn) {
+  p.abn_m = abn->mean;
+  p.abn_is = abn->invstd;
+  p.abn_w = abn->weight;
+  p.abn_b = abn->bias;
+}
+
 int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *only) {
   AS_CHECK_ARG(only, "conv2d_copy_operand_only: null");
   *only = 0;
@@ -1226,10 +1254,32 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
                                        stream);
 }
 
+static int fwd_bnstats_impl(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                            const float *const *w, const void *w_pack, float *y, uint16_t *y_bf16, float *stats,
+                            size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream,
+                            const adaptseg_operand_bn *abn);
+
 int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
                                   const float *const *w, const void *w_pack, float *y, uint16_t *y_bf16,
                                   float *stats, size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
                                   adaptseg_stream_t stream) {
+  return fwd_bnstats_impl(d, x, x_bf16, w, w_pack, y, y_bf16, stats, stats_bytes, ntiles, ws, ws_bytes, stream,
+                          nullptr);
+}
+
+int adaptseg_conv2d_fwd_bnstats_abn(const adaptseg_conv_desc *d, const float *x_pre, const adaptseg_operand_bn *abn,
+                                    const float *const *w, const void *w_pack, float *y, float *stats,
+                                    size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                    adaptseg_stream_t stream) {
+  AS_CHECK_ARG(abn && abn->mean && abn->invstd && x_pre, "conv fwd_bnstats_abn: null operand BN / input");
+  return fwd_bnstats_impl(d, x_pre, nullptr, w, w_pack, y, nullptr, stats, stats_bytes, ntiles, ws, ws_bytes, stream,
+                          abn);
+}
+
+static int fwd_bnstats_impl(const adaptseg_conv_desc *d, const float *x, const uint16_t *x_bf16,
+                            const float *const *w, const void *w_pack, float *y, uint16_t *y_bf16, float *stats,
+                            size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes, adaptseg_stream_t stream,
+                            const adaptseg_operand_bn *abn) {
   AS_CHECK_ARG(ntiles && stats, "conv fwd_bnstats: null stats / ntiles");
   *ntiles = 0;
   Plan pl;
@@ -1240,6 +1290,7 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   AS_CHECK_ARG(x || copy_only(pl, d, ADAPTSEG_CONV_FWD),
                "conv fwd_bnstats: this product needs the fp32 input (no bf16-operand kernel for it)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(w[s], "conv fwd_bnstats: null weight %d", s);
+  AS_CHECK_ARG(!abn || !tapgemm_eligible(d), "conv fwd_bnstats_abn: no operand-BN kernel for this product");
   if (tapgemm_eligible(d))  // the tap-GEMM path has no fused statistics: plain forward
     return adaptseg_conv2d_fwd_x(d, x, x_bf16, w, nullptr, nullptr, nullptr, y, y_bf16, 0, ws, ws_bytes, stream);
   ConvParams &p = pl.p;
@@ -1254,6 +1305,11 @@ int adaptseg_conv2d_fwd_bnstats_x(const adaptseg_conv_desc *d, const float *x, c
   x3_terms(pl);
   AS_CHECK_ARG(x || (copy_only(pl, d, ADAPTSEG_CONV_FWD) && pl.act_ext),
                "conv fwd_bnstats: x is NULL but the plan (after the alignment checks) needs the fp32 input");
+  if (abn) {
+    AS_CHECK_ARG(abn_plan_ok(pl, d, ADAPTSEG_CONV_FWD),
+                 "conv fwd_bnstats_abn: no operand-BN kernel for this product (adaptseg_conv2d_operand_bn_ok)");
+    set_abn(p, abn);
+  }
   const bool terms = copies_are_terms();
   AS_CHECK_ARG(y || !terms, "conv fwd_bnstats: under the F32X3 maths the output is fp32");
   const int64_t nyb = (int64_t)d->n * d->oh * d->ow * d->k;
@@ -1436,9 +1492,26 @@ int adaptseg_conv2d_bwd_weight(const adaptseg_conv_desc *d, const float *dy, con
   return adaptseg_conv2d_bwd_weight_x(d, dy, nullptr, x, nullptr, dw, db, flags, ws, ws_bytes, stream);
 }
 
+static int bwd_weight_impl(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16, const float *x,
+                           const uint16_t *x_bf16, float *const *dw, float *const *db, int flags, void *ws,
+                           size_t ws_bytes, adaptseg_stream_t stream, const adaptseg_operand_bn *abn);
+
 int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16,
                                  const float *x, const uint16_t *x_bf16, float *const *dw, float *const *db,
                                  int flags, void *ws, size_t ws_bytes, adaptseg_stream_t stream) {
+  return bwd_weight_impl(d, dy, dy_bf16, x, x_bf16, dw, db, flags, ws, ws_bytes, stream, nullptr);
+}
+
+int adaptseg_conv2d_bwd_weight_abn(const adaptseg_conv_desc *d, const float *dy, const float *x_pre,
+                                   const adaptseg_operand_bn *abn, float *const *dw, int flags, void *ws,
+                                   size_t ws_bytes, adaptseg_stream_t stream) {
+  AS_CHECK_ARG(abn && abn->mean && abn->invstd && x_pre && dy, "conv bwd_weight_abn: null operand BN / operand");
+  return bwd_weight_impl(d, dy, nullptr, x_pre, nullptr, dw, nullptr, flags, ws, ws_bytes, stream, abn);
+}
+
+static int bwd_weight_impl(const adaptseg_conv_desc *d, const float *dy, const uint16_t *dy_bf16, const float *x,
+                           const uint16_t *x_bf16, float *const *dw, float *const *db, int flags, void *ws,
+                           size_t ws_bytes, adaptseg_stream_t stream, const adaptseg_operand_bn *abn) {
   Plan pl;
   int st = make_plan(d, ADAPTSEG_CONV_BWD_WEIGHT, pl);
   if (st) return st;
@@ -1448,6 +1521,8 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
                "conv bwd_weight: this product needs the fp32 operands (no bf16-operand kernel / bias gradient)");
   for (int s = 0; s < d->nseg; ++s) AS_CHECK_ARG(dw[s], "conv bwd_weight: null dw %d", s);
   hipStream_t s = as_stream(stream);
+  AS_CHECK_ARG(!abn || !(use_thin(d, ADAPTSEG_CONV_BWD_WEIGHT) || tapgemm_eligible(d)),
+               "conv bwd_weight_abn: no operand-BN kernel for this product");
   int thin_st = ADAPTSEG_ERR_ARG;
   if (use_thin(d, ADAPTSEG_CONV_BWD_WEIGHT)) {
     thin_st = thin_wgrad(d, dy, x, dw[0], flags, ws, ws_bytes, s);
@@ -1472,6 +1547,11 @@ int adaptseg_conv2d_bwd_weight_x(const adaptseg_conv_desc *d, const float *dy, c
     x3_terms(pl);
     AS_CHECK_ARG((dy && x) || ((pl.g16 || pl.x3ext) && pl.act_ext),
                  "conv bwd_weight: dy / x is NULL but the plan (after the alignment checks) needs the fp32 operands");
+    if (abn) {
+      AS_CHECK_ARG(abn_plan_ok(pl, d, ADAPTSEG_CONV_BWD_WEIGHT),
+                   "conv bwd_weight_abn: no operand-BN kernel for this product (adaptseg_conv2d_operand_bn_ok)");
+      set_abn(p, abn);
+    }
     p.flags = flags & ADAPTSEG_EPI_ACCUMULATE;
     // a deferred sum keeps its slabs in ws until the flush: not with a bias gradient, whose
     // partial sums reuse the start of ws right after this GEMM

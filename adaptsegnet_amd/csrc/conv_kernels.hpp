@@ -79,7 +79,12 @@ struct ConvParams {
   const uint32_t *bs_bits;
   int bs_mask, bs_ntiles;
   short tap_dy[kMaxTaps], tap_dx[kMaxTaps];
+  // operand BatchNorm + ReLU (adaptseg_operand_bn): the activation operand x is a train-mode BN's
+  // input and the conv reads relu((x - mean) * invstd * w + b) — the forward's A operand on
+  // igemm_x3h_kernel, the weight gradient's x operand on igemm_x3_kernel (NULL abn_m: none)
+  const float *abn_m, *abn_is, *abn_w, *abn_b;
 };
+constexpr int kAbnMaxC = 512;   // channels of an operand BN (staged in LDS)
 
 // The epilogue's read-modify-write operands under either storage: the accumulate target (the
 // fp32 output, or — bf16 gradient storage, p.out NULL — its bf16 image) and the residual (fp32,

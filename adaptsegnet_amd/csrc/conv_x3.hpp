@@ -64,8 +64,13 @@ static __device__ __attribute__((aligned(16))) float g_x3_zero4[4];
 // the exact three-term split (rne2 / split3_2 / split3) lives in common.hpp: the BatchNorm
 // passes that write F32X3 term images use the same arithmetic
 
-template <int MODE, bool S2>
+// ABN (the weight gradient only): its x operand is a train-mode BN's input and the product reads
+// relu(bn_affine(x)) (common.hpp bn_relu: bn_apply2d_kernel's expression, so bitwise the unfused
+// weight gradient on the BN pass's output); pixels outside the image / past K read 0.  The BN's
+// channel parameters (Cin <= kAbnMaxC) are staged in LDS at the start.
+template <int MODE, bool S2, bool ABN>
 __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  static_assert(!ABN || MODE == MODE_WGRAD, "operand BN: the weight gradient's x operand");
   constexpr bool MC = MODE == MODE_WGRAD;   // both operands M/N-contiguous (k = output pixel)
   constexpr int BM = 128, BN = 128, BK = kX3BK, NT = x3_threads(MODE);
   constexpr int WAVES_M = 2, WAVES_N = NT / 128;        // 2x2 (WGRAD) or 2x4 waves
@@ -75,8 +80,9 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
   constexpr int IMGB = BN * kX3BK * 2;      // B term image
   constexpr int BPT = IMGB / NT;            // packed-B bytes per thread and term (16 or 8)
   constexpr int STAGE = 3 * IMG + 3 * IMGB; // A hi/mid/lo, B hi/mid/lo
+  constexpr int ABN_BYTES = ABN ? 4 * kAbnMaxC * 4 : 0;
 
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + ABN_BYTES];
 
   const int tid = threadIdx.x;
   const int ntn = (p.N + BN - 1) / BN;
@@ -163,6 +169,7 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
 
   float4 ra[NQ];           // A: one float4 per slot
   float4 rbf[MC ? NQ : 1]; // MC: B float4 per slot
+  bool rbv = false;        // ABN: rbf[0] is a real pixel (else the zero fill)
   BChunk rbh[MC ? 1 : 3];  // K-contiguous B: this thread's BPT bytes of each packed term image
   const float *zero4 = g_x3_zero4;
 
@@ -255,6 +262,7 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
       const int ix = (w_pos & 0xffff) * p.stride + (int)(short)(w_tap & 0xffff);
       const bool v = b_ok[0] && rv && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
       rbf[0] = ld4(v ? p.x + w_x : zero4);
+      rbv = v;
     }
   };
 
@@ -348,10 +356,27 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
   // step's staged registers into LDS buffer cur^1 in the same basic block, and the scheduler
   // interleaves that vector / LDS work between the MFMAs (one MFMA, three VALU, one LDS store)
   // instead of running it after them.
+  // ABN: the staged x float4 (loaded one step earlier) through the operand BN, in place, before
+  // this step's fragments are live (inside the MFMA-interleaved split below it spilled)
+  auto abn_x = [&]() {
+    if constexpr (ABN) {
+      const float *L = reinterpret_cast<const float *>(lds + 2 * STAGE) + b_off[0];
+      const float4 bm4 = *reinterpret_cast<const float4 *>(L);
+      const float4 bi4 = *reinterpret_cast<const float4 *>(L + kAbnMaxC);
+      const float4 bw4 = *reinterpret_cast<const float4 *>(L + 2 * kAbnMaxC);
+      const float4 bb4 = *reinterpret_cast<const float4 *>(L + 3 * kAbnMaxC);
+      float4 &xv = rbf[0];
+      xv.x = rbv ? bn_relu(xv.x, bm4.x, bi4.x, bw4.x, bb4.x) : 0.f;
+      xv.y = rbv ? bn_relu(xv.y, bm4.y, bi4.y, bw4.y, bb4.y) : 0.f;
+      xv.z = rbv ? bn_relu(xv.z, bm4.z, bi4.z, bw4.z, bb4.z) : 0.f;
+      xv.w = rbv ? bn_relu(xv.w, bm4.w, bi4.w, bw4.w, bb4.w) : 0.f;
+    }
+  };
   auto compute = [&](auto cur_c) {
     constexpr int cur = decltype(cur_c)::value;
     const char *As = lds + cur * STAGE;
     const char *Bs = As + 3 * IMG;
+    abn_x();
     bf16x8 a[3][TM], b[3][TN];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
@@ -388,11 +413,22 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if constexpr (ABN) {   // the operand BN's channel parameters (weight / bias NULL: 1 / 0)
+    float *L = reinterpret_cast<float *>(lds + 2 * STAGE);
+    for (int c = tid; c < p.c; c += NT) {
+      L[c] = p.abn_m[c];
+      L[kAbnMaxC + c] = p.abn_is[c];
+      L[2 * kAbnMaxC + c] = p.abn_w ? p.abn_w[c] : 1.f;
+      L[3 * kAbnMaxC + c] = p.abn_b ? p.abn_b[c] : 0.f;
+    }
+    __syncthreads();
+  }
   if (kt0 < kt1) {
     // T14 order with unconditional staging (past the last step it re-reads step kt1-1 into
     // the LDS buffer nobody reads again): registers hold step kt+1 while step kt computes
     const int klast = kt1 - 1;
     load_tile(kt0);
+    abn_x();
     store_tile(std::integral_constant<int, 0>{});
     load_tile(min(kt0 + 1, klast));
     __syncthreads();

@@ -387,17 +387,24 @@ __device__ __forceinline__ void x3h_wait(f32x4v (&r)[4]) {
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : : "memory");
 }
 
-template <int MODE, bool S2>
+// ABN (operand BatchNorm, the forward only): the activation operand is a BN's input x_pre and
+// the conv reads relu(bn_affine(x_pre)) — bn_apply2d_kernel's expression (common.hpp bn_relu), so
+// the products equal the unfused conv's on the BN pass's output bit for bit, and taps outside the
+// image read 0 as before.  The BN's per-channel mean / invstd / weight / bias (C <= kAbnMaxC) are
+// staged in LDS at the start; the split of each gathered float4 applies them first.
+template <int MODE, bool S2, bool ABN>
 __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products");
   static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
+  static_assert(!ABN || MODE == MODE_FWD, "operand BN: the forward's activation operand");
   constexpr int BM = 256, BN = 128, BK = kX3rBK;
   constexpr int WAVES_M = 4, WAVES_N = 2, WTM = 64, WTN = 64, TM = 2, TN = 2;
   constexpr int IMGA = BM * BK * 2;                // one A term image [256 rows][32 k]: 16 KB
   constexpr int IMGB = BN * 16 * 2;                // one B term image of one 16-deep sub-step: 4 KB
   constexpr int BOFF = 3 * IMGA;
   constexpr int STAGE = x3r_stage_bytes(BM);
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  constexpr int ABN_BYTES = ABN ? 4 * kAbnMaxC * 4 : 0;   // [mean | invstd | weight | bias][kAbnMaxC]
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + ABN_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (p.N + BN - 1) / BN;
@@ -471,6 +478,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
 
   // per K step: A source offset / tap shift, B pack step
+  int cbase = 0;   // FWD: the input channel of the step's first k (the operand BN's channel)
   auto geom = [&](int kt, int &soff, int &dy, int &dx, int &wkt) {
     const int kbase = kt * BK;
     if constexpr (MODE == MODE_FWD) {
@@ -479,7 +487,8 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
       seg_geom(p, sr, tap, seg, t, dy, dx);
       dy = uni(dy);
       dx = uni(dx);
-      soff = uni(dy * p.sxh + dx * p.sxw + kbase - tap * p.c);
+      cbase = uni(kbase - tap * p.c);
+      soff = uni(dy * p.sxh + dx * p.sxw + cbase);
       wkt = 2 * kt;
     } else if constexpr (S2) {
       const int tap = uni((int)fdiv((uint32_t)kbase, p.fd_k));
@@ -500,16 +509,20 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
       wkt = 2 * kt;
     }
   };
-  auto load_a = [&](int kt, f32x4v (&r)[4]) {
+  // load_a's `meta` (ABN): (channel of the thread's float4 << 4) | the four rows' tap-valid bits
+  auto load_a = [&](int kt, f32x4v (&r)[4], int &meta) {
     int soff, dy, dx, wkt;
     geom(kt, soff, dy, dx, wkt);
     const int hh = MODE == MODE_FWD ? p.h : p.oh, ww = MODE == MODE_FWD ? p.w : p.ow;
+    int vb = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool v = a_ok[i] & ((unsigned)((a_yx[i] >> 16) + dy) < (unsigned)hh) &
                      ((unsigned)((a_yx[i] & 0xffff) + dx) < (unsigned)ww);
+      vb |= (int)v << i;
       r[i] = x3h_ld16(v ? src + a_pix[i] + soff : zero4);
     }
+    meta = ABN ? ((cbase + 4 * q) << 4) | vb : 0;
   };
   auto issue_b = [&](int kt, int st) {
     int soff, dy, dx, wkt;
@@ -519,13 +532,29 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
 #pragma unroll
     for (int j = 0; j < 3; ++j) glds16(bsrc + j * 8 * 1024, bdst + j * 8 * 1024);
   };
-  auto store_a = [&](const f32x4v (&r)[4], auto st_c) {
+  auto store_a = [&](const f32x4v (&r)[4], int meta, auto st_c) {
     constexpr int st = decltype(st_c)::value;
     char *As = lds + st * STAGE + a_st;
+    float4 bm4, bi4, bw4, bb4;
+    if constexpr (ABN) {
+      const float *L = reinterpret_cast<const float *>(lds + 2 * STAGE) + (meta >> 4);
+      bm4 = *reinterpret_cast<const float4 *>(L);
+      bi4 = *reinterpret_cast<const float4 *>(L + kAbnMaxC);
+      bw4 = *reinterpret_cast<const float4 *>(L + 2 * kAbnMaxC);
+      bb4 = *reinterpret_cast<const float4 *>(L + 3 * kAbnMaxC);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       uint2 h, m, l;
-      split3(make_float4(r[i].x, r[i].y, r[i].z, r[i].w), h, m, l);
+      float4 v = make_float4(r[i].x, r[i].y, r[i].z, r[i].w);
+      if constexpr (ABN) {
+        const bool ok = (meta >> i) & 1;
+        v.x = ok ? bn_relu(v.x, bm4.x, bi4.x, bw4.x, bb4.x) : 0.f;
+        v.y = ok ? bn_relu(v.y, bm4.y, bi4.y, bw4.y, bb4.y) : 0.f;
+        v.z = ok ? bn_relu(v.z, bm4.z, bi4.z, bw4.z, bb4.z) : 0.f;
+        v.w = ok ? bn_relu(v.w, bm4.w, bi4.w, bw4.w, bb4.w) : 0.f;
+      }
+      split3(v, h, m, l);
       *reinterpret_cast<uint2 *>(As + i * 64 * 64) = h;
       *reinterpret_cast<uint2 *>(As + IMGA + i * 64 * 64) = m;
       *reinterpret_cast<uint2 *>(As + 2 * IMGA + i * 64 * 64) = l;
@@ -542,7 +571,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
       for (int r = 0; r < 16; ++r) acc[i][j][r] = accs[i][j][r] = 0.f;
 
   // the MFMAs of stage st with the split + store of `r` (the next step's A) into stage st^1
-  auto compute = [&](auto st_c, const f32x4v (&r)[4]) {
+  auto compute = [&](auto st_c, const f32x4v (&r)[4], int meta) {
     constexpr int st = decltype(st_c)::value;
     const char *S = lds + st * STAGE;
     __builtin_amdgcn_s_setprio(1);
@@ -560,7 +589,7 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
       }
       x3_products(a, b, acc, accs);
     }
-    store_a(r, std::integral_constant<int, st ^ 1>{});
+    store_a(r, meta, std::integral_constant<int, st ^ 1>{});
     // 48 MFMAs; ~100 VALU and 12 ds_write_b64 of the split: two VALU after each MFMA, one
     // store after every fourth
 #pragma unroll
@@ -584,25 +613,36 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
     asm volatile("" ::: "memory");
   };
 
+  if constexpr (ABN) {   // the operand BN's channel parameters (weight / bias NULL: 1 / 0)
+    float *L = reinterpret_cast<float *>(lds + 2 * STAGE);
+    for (int c = tid; c < p.c; c += 512) {
+      L[c] = p.abn_m[c];
+      L[kAbnMaxC + c] = p.abn_is[c];
+      L[2 * kAbnMaxC + c] = p.abn_w ? p.abn_w[c] : 1.f;
+      L[3 * kAbnMaxC + c] = p.abn_b ? p.abn_b[c] : 0.f;
+    }
+    __syncthreads();
+  }
   if (kt0 < kt1) {
     // past the last step the loads re-read step kt1-1 into the stage nobody reads again
     const int klast = kt1 - 1;
     f32x4v ra[4], rb[4];
-    load_a(kt0, ra);
+    int ma, mb;
+    load_a(kt0, ra, ma);
     x3h_wait(ra);
-    store_a(ra, std::integral_constant<int, 0>{});
+    store_a(ra, ma, std::integral_constant<int, 0>{});
     issue_b(kt0, 0);
-    load_a(min(kt0 + 1, klast), rb);
+    load_a(min(kt0 + 1, klast), rb, mb);
     for (int kt = kt0; kt < kt1; kt += 2) {
       step_open(rb);                    // stage 0 holds step kt; rb = A(kt+1)
       issue_b(min(kt + 1, klast), 1);
-      load_a(min(kt + 2, klast), ra);
-      compute(std::integral_constant<int, 0>{}, rb);
+      load_a(min(kt + 2, klast), ra, ma);
+      compute(std::integral_constant<int, 0>{}, rb, mb);
       if (kt + 1 >= kt1) break;
       step_open(ra);                    // stage 1 holds step kt+1; ra = A(kt+2)
       issue_b(min(kt + 2, klast), 0);
-      load_a(min(kt + 3, klast), rb);
-      compute(std::integral_constant<int, 1>{}, ra);
+      load_a(min(kt + 3, klast), rb, mb);
+      compute(std::integral_constant<int, 1>{}, ra, ma);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMAs / gathers past the last step
     __syncthreads();                                     // the epilogue reuses the LDS

@@ -155,6 +155,27 @@ DEFER_SPLITK = _switch("ADAPTSEG_DEFER_SPLITK", 0, (0, 1))
 # (A/B switch) weight gradients on the side stream (WgradStream; 0: inline on the main stream)
 WGRAD_STREAM = _switch("ADAPTSEG_WGRAD_STREAM", 1, (0, 1))
 
+# (A/B switch) BN2 + ReLU folded into conv3 (K.OperandBN): where conv3's forward runs on the x3h
+# tile and its weight gradient on the register-staged F32X3 kernel (layers 3-4 under the F32X3
+# maths), BN2's apply pass is not run — its statistics are finalised alone, conv3's forward and
+# weight gradient read BN2's input c2 and apply the BN in their operand gathers (bitwise the
+# unfused results) and BN2's backward recomputes its ReLU mask from c2 as before.  Measured slower
+# (c2 -1.1 %, c3 -1.1 %, profiles/r6/bn_fold_ab.txt: the x3h forward and the staged weight
+# gradient lose more to the in-gather BN than the apply pass cost) — off by default
+BN_FOLD = _switch("ADAPTSEG_BN_FOLD", 0, (0, 1))
+_FOLD_OK: dict = {}
+
+
+def _fold_ok(g, n, h, w) -> bool:
+    """conv ``g`` on an n x h x w input can take its operand BN in the forward (with fused
+    output statistics) and the weight gradient."""
+    key = (g, n, h, w, K.get_conv_math(), K.get_x3h())
+    v = _FOLD_OK.get(key)
+    if v is None:
+        v = _FOLD_OK[key] = (K.operand_bn_ok(g, n, h, w, 0) and K.operand_bn_ok(g, n, h, w, 2) and
+                             K.conv_bnstats_tiles(g, n, h, w, K.nhwc_strides(n, h, w, g.cin)) > 0)
+    return v
+
 
 def lowp_grads() -> bool:
     """bf16 GRADIENT storage (the BF16 maths, config c5, with lowp_storage): a Bottleneck's data
@@ -260,7 +281,7 @@ def bn_sums_spec(bn, x, st, which=3):
 
 class BlockRec:
     __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
-                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3")
+                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3", "abn2")
 
 
 # (A/B switch) the Bottleneck's output ReLU mask as a bitmap (1 bit per element) instead of the
@@ -341,8 +362,19 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     # conv3's backward on term images (X3_BWD_TERMS 3): BN2 also writes y2's terms for its weight
     # gradient (the forward still reads the fp32 y2)
     terms3 = not sh and save and X3_BWD_TERMS >= 3 and x3_forward_terms(g2) and g3.cin % 32 == 0
-    y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh or terms3, fp32=not thin2)
-    c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
+    abn2 = None
+    if (BN_FOLD and training and not sh and not terms3 and t2 is not None and _fold_ok(g3, n, oh, ow)
+            and c2.is_contiguous()):
+        # BN2 folded into conv3 (BN_FOLD): statistics only, y2 never written
+        bn2 = blk.bn2
+        mean2, is2 = K.bn_fwd_train_tiles_stats(c2, t2, bn2.running_mean, bn2.running_var, bn2.momentum, bn2.eps)
+        s2 = (mean2, is2, True)
+        abn2 = K.OperandBN(mean2, is2, bn2.weight, bn2.bias)
+        y2 = y2b = None
+        c3, t3 = K.conv_fwd_bnstats_abn(g3, c2, abn2, n, oh, ow, [blk.conv3.weight])
+    else:
+        y2, s2, y2b = bn_forward_b(blk.bn2, c2, None, True, training, t2, bf16=sh or terms3, fp32=not thin2)
+        c3, t3 = conv(g3, y2, n, oh, ow, blk.conv3.weight, xb=y2b, bf16_only=lp)
     cd = sd = None
     if blk.downsample is not None:
         dconv, dbn = blk.downsample[0], blk.downsample[1]
@@ -364,6 +396,7 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec = BlockRec()
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, (None if bits3 is not None else out), cd, sd
+        rec.abn2 = abn2
         rec.bits3 = bits3
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
@@ -385,6 +418,17 @@ def _wgrad(ws, g, dy, x, n, h, w, dws, dbs=None, strides=None, dyb=None, xb=None
         run()
     else:
         ws.launch(run, *[t for t in (dy, x, dyb, xb) if t is not None])
+
+
+def _wgrad_abn(ws, g, dy, x_pre, abn, n, h, w, dws):
+    """Weight gradient whose x operand is relu(bn(x_pre)) (K.OperandBN), on the side stream when
+    ``ws`` is given."""
+    def run():
+        K.conv_wgrad_abn(g, dy, x_pre, abn, n, h, w, dws)
+    if ws is None:
+        run()
+    else:
+        ws.launch(run, *[t for t in (dy, x_pre, abn.mean, abn.invstd) if t is not None])
 
 
 # ---------------------------------------------------------------------------------------
@@ -449,7 +493,10 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     r = K.conv_dgrad(g3, dc3, n, oh, ow, [blk.conv3.weight], dyb=dc3b, bf16_only=lg, bnsum=bs2)
     dy2, sums2 = r if bs2 is not None else (r, None)
     if need_w and blk.conv3.weight.grad is not None:
-        _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
+        if rec.abn2 is not None:   # BN2 folded into conv3: its weight gradient reads c2 through BN2
+            _wgrad_abn(ws, g3, dc3, rec.c2, rec.abn2, n, oh, ow, [blk.conv3.weight.grad])
+        else:
+            _wgrad(ws, g3, dc3, rec.y2, n, oh, ow, [blk.conv3.weight.grad], dyb=dc3b, xb=rec.y2b)
     del dc3, dc3b
     # (the saved y is the mask source in eval mode: bf16 like x under bf16 storage)
     # F32X3 (default maths) with y1's term images saved: BN2's backward also writes dY2's terms,

@@ -300,6 +300,47 @@ def _aligned16(*ts) -> bool:
     return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
 
 
+@dataclass
+class OperandBN:
+    """A train-mode BatchNorm + ReLU folded into its consumer conv's operand gather
+    (adaptseg_operand_bn): the conv reads relu((x_pre - mean) * invstd * weight + bias), bitwise
+    the BN apply pass's output, which is never written."""
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    weight: torch.Tensor | None
+    bias: torch.Tensor | None
+
+
+def operand_bn_ok(g: ConvGeom, n: int, h: int, w: int, op: int) -> bool:
+    """Product ``op`` of this conv (contiguous NHWC input) has an operand-BN kernel (the x3h
+    forward, the register-staged F32X3 weight gradient; BN of <= 512 channels)."""
+    return _ops.operand_bn_ok((n, g.cin, h, w), nhwc_strides(n, h, w, g.cin), _wshape(g), g.stride, g.pads, g.dils,
+                              op)
+
+
+def conv_fwd_bnstats_abn(g: ConvGeom, x_pre: torch.Tensor, abn: OperandBN, n: int, h: int, w: int, weights):
+    """conv_fwd_bnstats of relu(bn(x_pre)) with the BN folded into the gather: (y, (stats, ntiles))."""
+    strides = nhwc_strides(n, h, w, g.cin)
+    nt = conv_bnstats_tiles(g, n, h, w, strides)
+    if nt == 0 or not _aligned16(x_pre, *weights):
+        raise RuntimeError("conv_fwd_bnstats_abn: no fused-statistics plan for this product / unaligned operand")
+    oh, ow = g.out_hw(h, w)
+    out = torch.empty((n, oh, ow, g.cout), device=x_pre.device, dtype=torch.float32)
+    stats = torch.empty(nt * (1 + 2 * g.cout), device=x_pre.device, dtype=torch.float32)
+    wp = _wpack(g, n, h, w, strides, weights, CONV_FWD)
+    _OP.conv2d_fwd_bnstats_abn(x_pre, abn.mean, abn.invstd, abn.weight, abn.bias, list(weights), wp, out, stats,
+                               (n, g.cin, h, w), strides, _wshape(g), g.stride, g.pads, g.dils, nt)
+    return out, (stats, nt)
+
+
+def conv_wgrad_abn(g: ConvGeom, dy: torch.Tensor, x_pre: torch.Tensor, abn: OperandBN, n: int, h: int, w: int, dws,
+                   accumulate: bool = True) -> None:
+    """conv_wgrad with the x operand relu(bn(x_pre)) (no bias gradient)."""
+    _OP.conv2d_bwd_weight_abn(dy, x_pre, abn.mean, abn.invstd, abn.weight, abn.bias, list(dws), (n, g.cin, h, w),
+                              nhwc_strides(n, h, w, g.cin), _wshape(g), g.stride, g.pads, g.dils,
+                              EPI_ACCUMULATE if accumulate else 0)
+
+
 def conv_bnsum_tiles(g: ConvGeom, n: int, h: int, w: int, with_copy: bool = False) -> int:
     """Row tiles of the fused BN backward sums of this data gradient (0: its plan cannot fuse them)."""
     d = _desc(g, n, h, w, nhwc_strides(n, h, w, g.cin))[0]
@@ -458,6 +499,18 @@ def bn_fwd_train_tiles(x, tiles, weight, bias, running_mean, running_var, moment
     _OP.bn_fwd_train_tiles(x, stats, int(ntiles), weight, bias, running_mean, running_var, res, y, yb, ybits, mean,
                            invstd, float(momentum), float(eps), int(relu))
     return (y, mean, invstd, yb) if bf16_out else (y, mean, invstd)
+
+
+def bn_fwd_train_tiles_stats(x, tiles, running_mean, running_var, momentum, eps):
+    """The statistics half of bn_fwd_train_tiles alone (x: the BN input, for its shape): returns
+    (mean, invstd); for a BN folded into its consumer conv (OperandBN)."""
+    stats, ntiles = tiles
+    c = x.shape[-1]
+    mean = torch.empty(c, device=x.device, dtype=torch.float32)
+    invstd = torch.empty(c, device=x.device, dtype=torch.float32)
+    _OP.bn_fwd_train_tiles_stats(stats, int(ntiles), x.numel() // c, c, running_mean, running_var, mean, invstd,
+                                 float(momentum), float(eps))
+    return mean, invstd
 
 
 def bn_fwd_infer(x, weight, bias, running_mean, running_var, eps, res=None, relu=True, out=None,

@@ -248,6 +248,71 @@ def _conv2d_fwd_bnstats(x, xb, weight, wpack, out, outb, stats, in_shape, in_str
                            f"{nt.value} (unaligned operand?)")
 
 
+def _abn(mean, invstd, bnw, bnb):
+    return _lib.OperandBN(mean.data_ptr(), invstd.data_ptr(), None if bnw is None else bnw.data_ptr(),
+                          None if bnb is None else bnb.data_ptr())
+
+
+_ABN_OK: dict = {}
+
+
+def operand_bn_ok(in_shape, in_stride, w_shape, stride, pad, dil, op) -> bool:
+    """adaptseg_conv2d_operand_bn_ok, cached per product (host planning, no GPU)."""
+    key = (tuple(in_shape), tuple(in_stride), tuple(w_shape), stride, tuple(pad), tuple(dil), op, _CONV_MATH[0],
+           get_option(OPT_X3H), get_option(OPT_G16_WIDE))
+    v = _ABN_OK.get(key)
+    if v is None:
+        d = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)[0]
+        ok = ctypes.c_int(0)
+        check(_lib.lib().adaptseg_conv2d_operand_bn_ok(ctypes.byref(d), int(op), ctypes.byref(ok)), "operand_bn_ok")
+        v = _ABN_OK[key] = bool(ok.value)
+    return v
+
+
+@_op("conv2d_fwd_bnstats_abn(Tensor x_pre, Tensor mean, Tensor invstd, Tensor? bnw, Tensor? bnb, Tensor[] weight, "
+     "Tensor? wpack, Tensor(a!) out, Tensor(b!) stats, int[] in_shape, int[] in_stride, int[] w_shape, int stride, "
+     "int[] pad, int[] dil, int ntiles) -> ()")
+def _conv2d_fwd_bnstats_abn(x_pre, mean, invstd, bnw, bnb, weight, wpack, out, stats, in_shape, in_stride, w_shape,
+                            stride, pad, dil, ntiles):
+    """conv2d_fwd_bnstats on relu(bn(x_pre)) — the operand BN folded into the gather
+    (adaptseg_conv2d_fwd_bnstats_abn)."""
+    d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_FWD], stats.device)
+    nt = ctypes.c_int(0)
+    nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
+    a = _abn(mean, invstd, bnw, bnb)
+    check(_lib.lib().adaptseg_conv2d_fwd_bnstats_abn(
+        ctypes.byref(d), _pf(x_pre, nx, "conv2d_fwd_bnstats_abn x_pre"), ctypes.byref(a), _ptrs(weight), _p(wpack),
+        _pf(out, ny, "conv2d_fwd_bnstats_abn out"), _p(stats), ctypes.c_size_t(stats.numel() * 4), ctypes.byref(nt),
+        wp, wsz, _stream()), "conv2d_fwd_bnstats_abn")
+    if nt.value != ntiles:
+        raise RuntimeError(f"conv2d_fwd_bnstats_abn: planned {ntiles} statistics tiles, the launch produced "
+                           f"{nt.value} (unaligned operand?)")
+
+
+@_op("conv2d_bwd_weight_abn(Tensor dy, Tensor x_pre, Tensor mean, Tensor invstd, Tensor? bnw, Tensor? bnb, "
+     "Tensor(a!)[] dw, int[] in_shape, int[] in_stride, int[] w_shape, int stride, int[] pad, int[] dil, "
+     "int flags) -> ()")
+def _conv2d_bwd_weight_abn(dy, x_pre, mean, invstd, bnw, bnb, dw, in_shape, in_stride, w_shape, stride, pad, dil,
+                           flags):
+    """conv2d_bwd_weight with the x operand relu(bn(x_pre)) (adaptseg_conv2d_bwd_weight_abn)."""
+    d, ws, oh, ow = _wdesc(in_shape, in_stride, w_shape, stride, pad, dil)
+    wp, wsz = _ws_args(ws[CONV_BWD_WEIGHT], dw[0].device)
+    nx, ny = _prod(in_shape), in_shape[0] * oh * ow * w_shape[0]
+    a = _abn(mean, invstd, bnw, bnb)
+    check(_lib.lib().adaptseg_conv2d_bwd_weight_abn(
+        ctypes.byref(d), _pf(dy, ny, "conv2d_bwd_weight_abn dy"), _pf(x_pre, nx, "conv2d_bwd_weight_abn x_pre"),
+        ctypes.byref(a), _ptrs(dw), flags, wp, wsz, _stream()), "conv2d_bwd_weight_abn")
+
+
+@_op("bn_fwd_train_tiles_stats(Tensor stats, int ntiles, int rows, int c, Tensor(a!)? running_mean, "
+     "Tensor(b!)? running_var, Tensor(d!) mean, Tensor(e!) invstd, float momentum, float eps) -> ()")
+def _bn_fwd_train_tiles_stats(stats, ntiles, rows, c, running_mean, running_var, mean, invstd, momentum, eps):
+    check(_lib.lib().adaptseg_bn_fwd_train_tiles_stats(
+        int(rows), int(c), _p(stats), int(ntiles), _p(running_mean), _p(running_var), float(momentum), float(eps),
+        _p(mean), _p(invstd), _stream()), "bn_fwd_train_tiles_stats")
+
+
 @_op("conv2d_bwd_data(Tensor? dy, Tensor? dyb, Tensor[] weight, Tensor? wpack, Tensor? res, Tensor? resbits, "
      "Tensor? aux, Tensor(a!)? dx, Tensor(b!)? dxb, int[] in_shape, int[] w_shape, int stride, int[] pad, "
      "int[] dil, int flags) -> ()")

@@ -167,6 +167,32 @@ int adaptseg_conv2d_fwd_bnstats(const adaptseg_conv_desc *d, const float *x, con
    per-element and register-staged fp32 kernels, the tap-GEMM data gradient read fp32).  Host-side planning, no GPU.  The same plan
    the _x entry points check against. */
 int adaptseg_conv2d_copy_operand_only(const adaptseg_conv_desc *d, int op, int *only);
+
+/* Operand BatchNorm (round 6): a train-mode BatchNorm + ReLU folded into the consuming conv's
+   operand gather, so the BN's output is never written.  The conv reads x_pre, the BN's INPUT
+   (fp32 NHWC, contiguous), and uses relu((x_pre - mean) * invstd * weight + bias) per element —
+   the expression of the BN apply pass (adaptseg_bn_fwd_train*: bitwise the conv of that pass's
+   output); positions outside the image read 0.  Two products have such a kernel (F32X3 maths):
+   the forward on the 256x128x32 x3h tile and the register-staged weight gradient, for a BN of at
+   most 512 channels; adaptseg_conv2d_operand_bn_ok reports whether product `op` of `d` runs on
+   one (host-side planning, 16-byte aligned operands), and the _abn entry points return
+   ADAPTSEG_ERR_ARG otherwise.  The reference's pair is model/deeplab_multi.py:92-95
+   (out = relu(bn2(conv2(..))); out = conv3(out)). */
+typedef struct {
+  const float *mean, *invstd;   /* the BN's batch statistics (adaptseg_bn_fwd_train_tiles_stats) */
+  const float *weight, *bias;   /* its affine parameters (NULL: 1 / 0) */
+} adaptseg_operand_bn;
+int adaptseg_conv2d_operand_bn_ok(const adaptseg_conv_desc *d, int op, int *ok);
+/* adaptseg_conv2d_fwd_bnstats_x with the operand BN on x_pre (fp32 output, the row-tile
+   statistics of y as there) */
+int adaptseg_conv2d_fwd_bnstats_abn(const adaptseg_conv_desc *d, const float *x_pre, const adaptseg_operand_bn *abn,
+                                    const float *const *w, const void *w_pack, float *y, float *stats,
+                                    size_t stats_bytes, int *ntiles, void *ws, size_t ws_bytes,
+                                    adaptseg_stream_t stream);
+/* adaptseg_conv2d_bwd_weight with the operand BN on x_pre (no bias gradient) */
+int adaptseg_conv2d_bwd_weight_abn(const adaptseg_conv_desc *d, const float *dy, const float *x_pre,
+                                   const adaptseg_operand_bn *abn, float *const *dw, int flags, void *ws,
+                                   size_t ws_bytes, adaptseg_stream_t stream);
 /* Caller-owned weight packs.  The F32X3 and bf16 kernels read the weights of the forward and
    data-gradient products as a pack (the exact three-term bf16 split, or bf16 rows, laid out in
    the kernels' tile order) which the entry points otherwise build per call
@@ -312,6 +338,12 @@ int adaptseg_bn_fwd_train_x(int64_t rows, int c, const float *x, const uint16_t 
                             float *save_mean, float *save_invstd, const float *res, const uint16_t *res_bf16,
                             float *y, uint16_t *y_bf16, int relu, void *ws, size_t ws_bytes,
                             adaptseg_stream_t stream);
+/* The statistics half of adaptseg_bn_fwd_train_tiles alone (batch mean / invstd from the
+   producing conv's row tiles, running statistics updated): for a BN whose apply is folded into
+   its consumer conv (adaptseg_operand_bn), so y is never written. */
+int adaptseg_bn_fwd_train_tiles_stats(int64_t rows, int c, const float *stats, int ntiles, float *running_mean,
+                                      float *running_var, float momentum, float eps, float *save_mean,
+                                      float *save_invstd, adaptseg_stream_t stream);
 int adaptseg_bn_fwd_train_tiles_x(int64_t rows, int c, const float *stats, int ntiles, const float *x,
                                   const uint16_t *x_bf16, const float *weight, const float *bias,
                                   float *running_mean, float *running_var, float momentum, float eps,
