@@ -306,7 +306,12 @@ def x3_forward_terms(g) -> bool:
     footprint costs nothing there (it does in the backward, §3.2).  Same box: c2 26.95 / 26.91
     -> 27.33 / 27.25 images/s, c3 17.35 / 17.36 -> 17.66 / 17.66; extending it to Cin 128 / 64
     (layers 1-2) measured no further gain (profiles/r3/x3r_forward_ab.txt)."""
-    return K.get_conv_math() == K.MATH_F32X3 and g.kh * g.kw > 1 and g.cin >= 256 and g.cin % 32 == 0
+    return (X3_FWD_TERMS == 1 and K.get_conv_math() == K.MATH_F32X3 and g.kh * g.kw > 1 and g.cin >= 256
+            and g.cin % 32 == 0)
+
+
+# (A/B switch) 0: layers 3-4 conv2 forward on the fp32 y1 (the x3h tile) instead of y1's term images
+X3_FWD_TERMS = _switch("ADAPTSEG_X3_FWD_TERMS", 1, (0, 1))
 
 
 # (A/B switch) 0: conv2 backward on fp32 operands; 1: its weight gradient on term images (y1's
