@@ -104,17 +104,17 @@ hipError_t launch_x3(const Plan &pl, void *wpack, hipStream_t s) {
     // (the 256-row weight-gradient tile needs two register sets of six float4 beside its 128
     // accumulators: it spills, so the weight gradient runs the 128-row tile)
     if (pl.mode == MODE_WGRAD) launch_k(igemm_x3hw_kernel<128>, grid, 512, s, p);
-    else if (pl.mode == MODE_FWD && p.abn_m) launch_k(igemm_x3h_kernel<MODE_FWD, false, true>, grid, 512, s, p, wb);
-    else if (pl.mode == MODE_FWD) launch_k(igemm_x3h_kernel<MODE_FWD, false, false>, grid, 512, s, p, wb);
-    else if (pl.s2) launch_k(igemm_x3h_kernel<MODE_DGRAD, true, false>, grid, 512, s, p, wb);
-    else launch_k(igemm_x3h_kernel<MODE_DGRAD, false, false>, grid, 512, s, p, wb);
+    else if (pl.mode == MODE_FWD && p.abn_m) launch_k(igemm_x3h_abn_kernel, grid, 512, s, p, wb);
+    else if (pl.mode == MODE_FWD) launch_k(igemm_x3h_kernel<MODE_FWD, false>, grid, 512, s, p, wb);
+    else if (pl.s2) launch_k(igemm_x3h_kernel<MODE_DGRAD, true>, grid, 512, s, p, wb);
+    else launch_k(igemm_x3h_kernel<MODE_DGRAD, false>, grid, 512, s, p, wb);
     return hipGetLastError();
   }
-  if (pl.mode == MODE_FWD) launch_k(igemm_x3_kernel<MODE_FWD, false, false>, grid, block, s, p, wb);
-  else if (pl.mode == MODE_DGRAD && pl.s2) launch_k(igemm_x3_kernel<MODE_DGRAD, true, false>, grid, block, s, p, wb);
-  else if (pl.mode == MODE_DGRAD) launch_k(igemm_x3_kernel<MODE_DGRAD, false, false>, grid, block, s, p, wb);
-  else if (p.abn_m) launch_k(igemm_x3_kernel<MODE_WGRAD, false, true>, grid, block, s, p, wb);
-  else launch_k(igemm_x3_kernel<MODE_WGRAD, false, false>, grid, block, s, p, wb);
+  if (pl.mode == MODE_FWD) launch_k(igemm_x3_kernel<MODE_FWD, false>, grid, block, s, p, wb);
+  else if (pl.mode == MODE_DGRAD && pl.s2) launch_k(igemm_x3_kernel<MODE_DGRAD, true>, grid, block, s, p, wb);
+  else if (pl.mode == MODE_DGRAD) launch_k(igemm_x3_kernel<MODE_DGRAD, false>, grid, block, s, p, wb);
+  else if (p.abn_m) launch_k(igemm_x3_abn_kernel, grid, block, s, p, wb);
+  else launch_k(igemm_x3_kernel<MODE_WGRAD, false>, grid, block, s, p, wb);
   return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ static __device__ __attribute__((aligned(16))) float g_x3_zero4[4];
 // weight gradient on the BN pass's output); pixels outside the image / past K read 0.  The BN's
 // channel parameters (Cin <= kAbnMaxC) are staged in LDS at the start.
 template <int MODE, bool S2, bool ABN>
-__global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+__device__ __forceinline__ void x3_body(const ConvParams &p, const __bf16 *__restrict__ wb) {
   static_assert(!ABN || MODE == MODE_WGRAD, "operand BN: the weight gradient's x operand");
   constexpr bool MC = MODE == MODE_WGRAD;   // both operands M/N-contiguous (k = output pixel)
   constexpr int BM = 128, BN = 128, BK = kX3BK, NT = x3_threads(MODE);
@@ -450,6 +450,16 @@ __global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const Con
   static_assert(sizeof(lds) >= WAVES_M * WAVES_N * 32 * 36 * 4, "LDS for the f32x4 epilogue");
   igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
+}
+
+template <int MODE, bool S2>
+__global__ void __launch_bounds__(x3_threads(MODE), 4) igemm_x3_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  x3_body<MODE, S2, false>(p, wb);
+}
+// the weight gradient with the operand BN on x (ConvParams::abn_*)
+__global__ void __launch_bounds__(x3_threads(MODE_WGRAD), 4) igemm_x3_abn_kernel(const ConvParams p,
+                                                                               const __bf16 *__restrict__ wb) {
+  x3_body<MODE_WGRAD, false, true>(p, wb);
 }
 
 // Weight pack: the three bf16 terms of every weight of the GEMM's B operand (FWD: row n = Cout,

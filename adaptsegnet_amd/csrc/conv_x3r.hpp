@@ -393,7 +393,7 @@ __device__ __forceinline__ void x3h_wait(f32x4v (&r)[4]) {
 // image read 0 as before.  The BN's per-channel mean / invstd / weight / bias (C <= kAbnMaxC) are
 // staged in LDS at the start; the split of each gathered float4 applies them first.
 template <int MODE, bool S2, bool ABN>
-__global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+__device__ __forceinline__ void x3h_body(const ConvParams &p, const __bf16 *__restrict__ wb) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "K-contiguous products");
   static_assert(!S2 || MODE == MODE_DGRAD, "parity classes: data gradient only");
   static_assert(!ABN || MODE == MODE_FWD, "operand BN: the forward's activation operand");
@@ -654,6 +654,15 @@ __global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, c
   static_assert(sizeof(lds) >= WAVES_M * WAVES_N * 32 * 36 * 4, "LDS for the f32x4 epilogue");
   igemm_epilogue<MODE, BM, BN, WAVES_M, WAVES_N, S2, 2>(p, acc, bm, bn, tm, tn, split, M, Hc, Wc, py, px,
                                                       reinterpret_cast<float *>(lds));
+}
+
+template <int MODE, bool S2>
+__global__ void __launch_bounds__(512, 1) igemm_x3h_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  x3h_body<MODE, S2, false>(p, wb);
+}
+// the forward with the operand BN (ConvParams::abn_*)
+__global__ void __launch_bounds__(512, 1) igemm_x3h_abn_kernel(const ConvParams p, const __bf16 *__restrict__ wb) {
+  x3h_body<MODE_FWD, false, true>(p, wb);
 }
 
 // Weight gradient on the x3r_wgrad tiles ({256,128} x 128, K step = 32 output pixels, mc layout),

@@ -299,7 +299,8 @@ def _conv_plain(g, x, n, h, w, weight, strides=None, xb=None, bf16_only=False):
 
 
 def x3_forward_terms(g) -> bool:
-    """F32X3 (default maths, no operand copies): run this conv's forward on the term-image
+    """(X3_FWD_TERMS 1; off by default since round 6, the x3h tile reads the fp32 y1 instead)
+    F32X3 (default maths, no operand copies): run this conv's forward on the term-image
     kernel (conv_x3r.hpp, 256x128x32 LDS-DMA) with the producing BN writing its input's three
     bf16 terms beside the fp32 tensor — the dilated 3x3 conv2 of layers 3-4 (Cin >= 256).  The
     forward runs without the weight-gradient stream beside it, so the kernel's one-block-per-CU
@@ -310,8 +311,13 @@ def x3_forward_terms(g) -> bool:
             and g.cin % 32 == 0)
 
 
-# (A/B switch) 0: layers 3-4 conv2 forward on the fp32 y1 (the x3h tile) instead of y1's term images
-X3_FWD_TERMS = _switch("ADAPTSEG_X3_FWD_TERMS", 1, (0, 1))
+# (A/B switch) 1: layers 3-4 conv2 forward on y1's term images (x3r), its backward per
+# X3_BWD_TERMS; 0 (default since round 6): no term images — conv2's forward and data gradient run
+# on the x3h tile over the fp32 tensors and its weight gradient on the staged kernel.  Same box:
+# c2 +1.5 % / +1.1 %, c3 +0.8 % / +0.6 % over the term-image program (two A/B runs,
+# profiles/r6/x3_terms_retune_ab.txt): x3h reads 4-B fp32 rows instead of 6-B term images and
+# BN1 / BN2's backward write no term copies
+X3_FWD_TERMS = _switch("ADAPTSEG_X3_FWD_TERMS", 0, (0, 1))
 
 
 # (A/B switch) 0: conv2 backward on fp32 operands; 1: its weight gradient on term images (y1's

@@ -186,17 +186,28 @@ def test_weight_pack_sizes_follow_the_plan():
         K.set_conv_math(prev)
 
 
-def test_f32x3_forward_term_images_only_for_the_wide_dilated_convs():
-    """Under the default F32X3 maths the engine writes one operand copy: y1's three bf16 terms,
-    for the forward of conv2 in layers 3-4 (dilated 3x3, Cin >= 256), which then runs on the
-    term-image kernel (selector 88, conv_x3r.hpp); every other product keeps the register-staged
-    kernel on fp32 operands.  bench.conv_inventory books those FLOPs under selector 88."""
+def test_f32x3_forward_term_images_only_for_the_wide_dilated_convs(monkeypatch):
+    """Under the default F32X3 maths the engine writes no operand copies (X3_FWD_TERMS 0 since
+    round 6: layers 3-4 conv2 run on the x3h tile over fp32 operands, selector 86).  With
+    X3_FWD_TERMS 1 it writes one: y1's three bf16 terms, for the forward of conv2 in layers 3-4
+    (dilated 3x3, Cin >= 256), which then runs on the term-image kernel (selector 88,
+    conv_x3r.hpp); every other product keeps the fp32 kernels.  bench.conv_inventory books
+    those FLOPs under the selector that runs."""
     import bench
     from adaptsegnet_amd import engine
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd.model import DeeplabMulti, FCDiscriminator
     assert K.get_conv_math() == K.MATH_F32X3 and not engine.bf16_operands()
     model, D = DeeplabMulti(num_classes=19), FCDiscriminator(num_classes=19)
+    convs2 = [b.conv2.geom() for b in list(model.layer3) + list(model.layer4)]
+    n, h, w = 4, 64, 128   # layers 3-4 at 1024x512 (stem /2, max-pool /2 floor, layer2 /2)
+    flops = 2 * sum(g.flops(n, h, w) for g in convs2)   # source + target forwards
+    assert engine.X3_FWD_TERMS == 0
+    assert not any(engine.x3_forward_terms(blk.conv2.geom()) for layer in (model.layer1, model.layer2,
+                   model.layer3, model.layer4) for blk in layer)
+    inv = bench.conv_inventory(model, D, "single-level", 4, (1024, 512), (1024, 512), (1024, 512))
+    assert inv.get(88, 0.0) == 0.0 and inv[86] >= flops
+    monkeypatch.setattr(engine, "X3_FWD_TERMS", 1)
     want = set()
     for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4), 1):
         for blk in layer:
@@ -206,9 +217,7 @@ def test_f32x3_forward_term_images_only_for_the_wide_dilated_convs():
                 if on:
                     want.add(conv.geom())
     inv = bench.conv_inventory(model, D, "single-level", 4, (1024, 512), (1024, 512), (1024, 512))
-    n, h, w = 4, 64, 128   # layers 3-4 at 1024x512 (stem /2, max-pool /2 floor, layer2 /2)
-    flops = 2 * sum(g.flops(n, h, w) for g in [b.conv2.geom() for b in list(model.layer3) + list(model.layer4)])
-    assert abs(inv[88] - flops) <= 1e-6 * flops   # source + target forwards
+    assert abs(inv[88] - flops) <= 1e-6 * flops
     K.set_conv_math(K.MATH_F32)
     try:
         assert not any(engine.x3_forward_terms(g) for g in want)
