@@ -162,7 +162,7 @@ WGRAD_STREAM = _switch("ADAPTSEG_WGRAD_STREAM", 1, (0, 1))
 # unfused results) and BN2's backward recomputes its ReLU mask from c2 as before.  Measured slower
 # (c2 -1.1 %, c3 -1.1 %, profiles/r6/bn_fold_ab.txt: the x3h forward and the staged weight
 # gradient lose more to the in-gather BN than the apply pass cost) — off by default
-BN_FOLD = _switch("ADAPTSEG_BN_FOLD", 0, (0, 1))
+BN_FOLD = _switch("ADAPTSEG_BN_FOLD", 0, (0, 1, 2, 3))   # bit 1: BN2 -> conv3; bit 2: BN1 -> conv2
 _FOLD_OK: dict = {}
 
 
@@ -281,7 +281,7 @@ def bn_sums_spec(bn, x, st, which=3):
 
 class BlockRec:
     __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
-                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3", "abn2")
+                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3", "abn1", "abn2")
 
 
 # (A/B switch) the Bottleneck's output ReLU mask as a bitmap (1 bit per element) instead of the
@@ -367,14 +367,25 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     # mask comes from x in train mode, from the terms' hi image in eval mode)
     keep1 = terms2 and save and X3_BWD_TERMS >= 1
     need1 = not terms2 or (save and not keep1)
-    y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2,
-                               fp32=not thin1 and need1)
-    c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
+    abn1 = None
+    if ((BN_FOLD & 2) and training and not sh and not terms2 and t1 is not None and _fold_ok(g2, n, oh, ow)
+            and c1.is_contiguous()):
+        # BN1 folded into conv2 (BN_FOLD bit 2): statistics only, y1 never written
+        bn1 = blk.bn1
+        mean1, is1 = K.bn_fwd_train_tiles_stats(c1, t1, bn1.running_mean, bn1.running_var, bn1.momentum, bn1.eps)
+        s1 = (mean1, is1, True)
+        abn1 = K.OperandBN(mean1, is1, bn1.weight, bn1.bias)
+        y1 = y1b = None
+        c2, t2 = K.conv_fwd_bnstats_abn(g2, c1, abn1, n, oh, ow, [blk.conv2.weight])
+    else:
+        y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2,
+                                   fp32=not thin1 and need1)
+        c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
     # conv3's backward on term images (X3_BWD_TERMS 3): BN2 also writes y2's terms for its weight
     # gradient (the forward still reads the fp32 y2)
     terms3 = not sh and save and X3_BWD_TERMS >= 3 and x3_forward_terms(g2) and g3.cin % 32 == 0
     abn2 = None
-    if (BN_FOLD and training and not sh and not terms3 and t2 is not None and _fold_ok(g3, n, oh, ow)
+    if ((BN_FOLD & 1) and training and not sh and not terms3 and t2 is not None and _fold_ok(g3, n, oh, ow)
             and c2.is_contiguous()):
         # BN2 folded into conv3 (BN_FOLD): statistics only, y2 never written
         bn2 = blk.bn2
@@ -407,7 +418,7 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec = BlockRec()
         rec.x, rec.c1, rec.y1, rec.s1, rec.c2, rec.y2, rec.s2 = x, c1, y1, s1, c2, y2, s2
         rec.c3, rec.s3, rec.out, rec.cd, rec.sd = c3, s3, (None if bits3 is not None else out), cd, sd
-        rec.abn2 = abn2
+        rec.abn1, rec.abn2 = abn1, abn2
         rec.bits3 = bits3
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
@@ -528,7 +539,10 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
                      bf16_only=lg, bnsum=bs1)
     dy1, sums1 = r if bs1 is not None else (r, None)
     if need_w and blk.conv2.weight.grad is not None:
-        _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
+        if rec.abn1 is not None:   # BN1 folded into conv2: its weight gradient reads c1 through BN1
+            _wgrad_abn(ws, g2, dy2, rec.c1, rec.abn1, n, oh, ow, [blk.conv2.weight.grad])
+        else:
+            _wgrad(ws, g2, dy2, rec.y1, n, oh, ow, [blk.conv2.weight.grad], dyb=dy2b, xb=rec.y1b)
     del dy2, dy2b
     r = bn_backward(blk.bn1, dy1, rec.y1b if (sh or rec.y1 is None) else rec.y1, rec.c1, rec.s1, relu=True,
                     dx=None if lg else dy1,

@@ -88,9 +88,10 @@ def test_operand_bn_eligibility(k):
 
 
 def test_training_steps_bit_identical_with_folded_bn(monkeypatch):
-    """engine.BN_FOLD 1 vs 0 (the default) over two single-level steps at the c2 bench shape (batch
-    4, 1024x512: conv2's unsplit plans carry the BN2 statistics tiles the fold needs; layers 3-4
-    fold BN2 into conv3 — counted): the same losses and parameters, bit for bit."""
+    """engine.BN_FOLD 3 (BN2 -> conv3 and BN1 -> conv2) vs 0 (the default) over two single-level
+    steps at the c2 bench shape (batch 4, 1024x512: the producing convs' unsplit plans carry the
+    statistics tiles the fold needs; layers 3-4 fold BN2, layers 1, 3, 4 BN1 — counted): the same
+    losses and parameters, bit for bit."""
     from adaptsegnet_amd import engine
     from adaptsegnet_amd import kernels as K
     from adaptsegnet_amd.train import AdaptSegTrainer, StepConfig
@@ -108,7 +109,7 @@ def test_training_steps_bit_identical_with_folded_bn(monkeypatch):
         return orig(*a, **kw)
     monkeypatch.setattr(K, "conv_fwd_bnstats_abn", counting)
     runs = []
-    for fold in (1, 0):
+    for fold in (3, 0):
         monkeypatch.setattr(engine, "BN_FOLD", fold)
         calls.clear()
         m, d2 = build_g(), build_d(2002)
@@ -117,7 +118,7 @@ def test_training_steps_bit_identical_with_folded_bn(monkeypatch):
         losses = [tr.step(it, batch).values() for it in range(2)]
         torch.cuda.synchronize()
         if fold:
-            assert len(calls) >= 2 * 26   # layers 3-4, both domains' forwards, per step
+            assert len(calls) >= 2 * 26 + 2 * 29   # BN2 of layers 3-4, BN1 of layers 1, 3, 4; per step
         else:
             assert not calls
         runs.append((losses, [{kk: v.detach().cpu().clone() for kk, v in mm.state_dict().items()}
