@@ -281,7 +281,7 @@ def bn_sums_spec(bn, x, st, which=3):
 
 class BlockRec:
     __slots__ = ("x", "c1", "y1", "s1", "c2", "y2", "s2", "c3", "s3", "out", "cd", "sd",
-                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3", "abn1", "abn2")
+                 "n", "h", "w", "oh", "ow", "xb", "y1b", "y2b", "bits3", "abn1", "abn2", "wt2")
 
 
 # (A/B switch) the Bottleneck's output ReLU mask as a bitmap (1 bit per element) instead of the
@@ -318,6 +318,20 @@ def x3_forward_terms(g) -> bool:
 # profiles/r6/x3_terms_retune_ab.txt): x3h reads 4-B fp32 rows instead of 6-B term images and
 # BN1 / BN2's backward write no term copies
 X3_FWD_TERMS = _switch("ADAPTSEG_X3_FWD_TERMS", 0, (0, 1))
+
+# (A/B switch) with X3_FWD_TERMS 0: conv2 of Cin >= this (layer 4: 512) keeps its WEIGHT gradient
+# on the term-image kernel (x3r_wgrad: 0.54 MFMA alone vs 0.36 for the staged kernel on layer4
+# conv2, profiles/r6/pmc/mfma_util_atrous_f32x3.txt) — BN1 writes y1's terms beside the fp32 y1
+# and BN2's backward dY2's beside the fp32 dY2, the forward and data gradient stay on x3h.
+# 0: off (every conv2 weight gradient on the staged kernel)
+X3_WGRAD_TERMS_MIN_C = _switch("ADAPTSEG_X3_WGRAD_TERMS_MIN_C", 512, (0, 256, 512, 1024))
+
+
+def x3_wgrad_terms(g) -> bool:
+    """conv2 ``g``'s weight gradient on term images while its forward reads fp32 (see
+    X3_WGRAD_TERMS_MIN_C)."""
+    return (X3_WGRAD_TERMS_MIN_C > 0 and not x3_forward_terms(g) and K.get_conv_math() == K.MATH_F32X3
+            and g.kh * g.kw > 1 and g.cin >= X3_WGRAD_TERMS_MIN_C and g.cin % 32 == 0)
 
 
 # (A/B switch) 0: conv2 backward on fp32 operands; 1: its weight gradient on term images (y1's
@@ -363,6 +377,7 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     thin2 = sh and bf16_only(g3, n, oh, ow, (0, 2))
     c1, t1 = conv(g1, x, n, h, w, blk.conv1.weight, xb=xb, bf16_only=lp)
     terms2 = not sh and x3_forward_terms(g2)   # conv2's forward on y1's term images
+    wt2 = not sh and save and training and x3_wgrad_terms(g2)   # ... or only its weight gradient
     # ... and its weight gradient: then no consumer reads the fp32 y1 (the BN1 backward's ReLU
     # mask comes from x in train mode, from the terms' hi image in eval mode)
     keep1 = terms2 and save and X3_BWD_TERMS >= 1
@@ -378,9 +393,9 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         y1 = y1b = None
         c2, t2 = K.conv_fwd_bnstats_abn(g2, c1, abn1, n, oh, ow, [blk.conv2.weight])
     else:
-        y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2,
+        y1, s1, y1b = bn_forward_b(blk.bn1, c1, None, True, training, t1, bf16=sh or terms2 or wt2,
                                    fp32=not thin1 and need1)
-        c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=y1b, bf16_only=lp)
+        c2, t2 = conv(g2, y1, n, oh, ow, blk.conv2.weight, xb=None if wt2 else y1b, bf16_only=lp)
     # conv3's backward on term images (X3_BWD_TERMS 3): BN2 also writes y2's terms for its weight
     # gradient (the forward still reads the fp32 y2)
     terms3 = not sh and save and X3_BWD_TERMS >= 3 and x3_forward_terms(g2) and g3.cin % 32 == 0
@@ -422,7 +437,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
         rec.bits3 = bits3
         rec.n, rec.h, rec.w, rec.oh, rec.ow = n, h, w, oh, ow
         # the weight gradients' operand copies (bf16 / term images) of x, y1, y2
-        rec.xb, rec.y1b, rec.y2b = xb, y1b if (sh or keep1) else None, y2b
+        rec.xb, rec.y1b, rec.y2b = xb, y1b if (sh or keep1 or wt2) else None, y2b
+        rec.wt2 = wt2
         if terms3:
             rec.y2 = None   # the backward reads y2's terms (weight gradient, eval-mode mask)
         if sh and bits3 is None:
@@ -525,7 +541,7 @@ def block_backward(blk, rec, gout, need_w, ws=None, dx_fp32=True):
     # and conv2's weight gradient (X3_BWD_TERMS 2: its data gradient too) runs on the
     # term-image kernel (conv_x3r.hpp) instead of splitting both fp32 operands in-kernel
     t2 = not sh and rec.y1b is not None
-    if t2 and X3_BWD_TERMS >= 2:
+    if t2 and X3_BWD_TERMS >= 2 and not rec.wt2:   # (wt2: the data gradient reads the fp32 dY2)
         f2 = False
     r = bn_backward(blk.bn2, dy2, rec.y2b if (sh or rec.y2 is None) else rec.y2, rec.c2, rec.s2, relu=True,
                     dx=None if lg else dy2,

@@ -148,8 +148,9 @@ def conv_inventory(model, D, level, batch, src_wh, tgt_wh, tsize, products=None,
                                engine.x3_forward_terms(blk.conv2.geom()) and conv.geom().cin % 32 == 0)
                         add(conv.geom(), batch, ch, cw, 1, cp=True,
                             terms=(fwd_terms and engine.X3_BWD_TERMS >= 2) or c3t)
+                        wt2 = conv is blk.conv2 and not copies and engine.x3_wgrad_terms(conv.geom())
                         add(conv.geom(), batch, ch, cw, 2, cp=xcp,
-                            terms=(fwd_terms and engine.X3_BWD_TERMS >= 1) or c3t)
+                            terms=(fwd_terms and engine.X3_BWD_TERMS >= 1) or c3t or wt2)
                 h, w = oh, ow
         g6 = engine.aspp_geom(model.layer6)
         add(g6, batch, h, w, 0)

@@ -152,7 +152,8 @@ def main():
         # X3_BWD_TERMS: the layer 3-4 conv2 forward, data and weight gradients), timed so
         tf = st is None and name.endswith("conv2") and engine.x3_forward_terms(g)
         tb = tf and engine.X3_BWD_TERMS >= 2
-        tw = tf and engine.X3_BWD_TERMS >= 1
+        tw = (tf and engine.X3_BWD_TERMS >= 1) or (st is None and name.endswith("conv2") and
+                                                    engine.x3_wgrad_terms(g))
         xt = _terms(x) if tf or tw else None
         dyt = _terms(dy) if tb or tw else None
         for op in ops:
