@@ -383,8 +383,8 @@ def block_forward(blk, x, n, h, w, training, save, xb=None, out_fp32=True):
     keep1 = terms2 and save and X3_BWD_TERMS >= 1
     need1 = not terms2 or (save and not keep1)
     abn1 = None
-    if ((BN_FOLD & 2) and training and not sh and not terms2 and t1 is not None and _fold_ok(g2, n, oh, ow)
-            and c1.is_contiguous()):
+    if ((BN_FOLD & 2) and training and not sh and not terms2 and not wt2 and t1 is not None
+            and _fold_ok(g2, n, oh, ow) and c1.is_contiguous()):
         # BN1 folded into conv2 (BN_FOLD bit 2): statistics only, y1 never written
         bn1 = blk.bn1
         mean1, is1 = K.bn_fwd_train_tiles_stats(c1, t1, bn1.running_mean, bn1.running_var, bn1.momentum, bn1.eps)
