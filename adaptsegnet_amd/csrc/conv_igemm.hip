@@ -844,8 +844,10 @@ static int splitk_sum(const ConvParams &q, const float *slab, int mode, hipStrea
   if (vec) {
     const FastDiv fdn4 = make_fastdiv((uint32_t)q.N / 4);
     const int G = q.splits >= 64 ? 16 : q.splits >= 16 ? 4 : 1;
-    // grid cap: 512 / 1024 / 8192 measured within +-0.2 %
-    const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), 8192);
+    // grid cap: 512 / 1024 / 8192 measured within +-0.2 % (round 3); ADAPTSEG_SPLITK_MAX_BLOCKS
+    // for A/B runs (the block-stride loop covers any cap)
+    static const int max_blocks = env_int("ADAPTSEG_SPLITK_MAX_BLOCKS", 8192);
+    const int blocks = (int)std::min<size_t>(ceil_div(total / 4, 256 / G), (size_t)std::max(1, max_blocks));
     if (G == 16) splitk_reduce4_kernel<16><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
     else if (G == 4) splitk_reduce4_kernel<4><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
     else splitk_reduce4_kernel<1><<<blocks, 256, 0, s>>>(q, slab, mode, fdn4);
