@@ -714,7 +714,8 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     // products with K = 64 / 128 run slower on the 256-row tile — two to four K steps against its
     // prologue and epilogue) and not on the stride-2 parity classes (D.conv2's data gradient 449 ->
     // 523 us); the larger products gain 4-12 % (l4.ds forward 854 -> 775 us).
-    const bool x3h_fd = p.K >= 256 && !(op == ADAPTSEG_CONV_BWD_DATA && d->stride == 2);
+    static const int x3h_min_k = env_int("ADAPTSEG_X3H_MIN_K", 256);   // (A/B runs)
+    const bool x3h_fd = p.K >= x3h_min_k && !(op == ADAPTSEG_CONV_BWD_DATA && d->stride == 2);
     if (pl.x3 && pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3 &&
         ((op == ADAPTSEG_CONV_FWD && (x3h_mode() & 1) && x3h_fd) ||
          (op == ADAPTSEG_CONV_BWD_DATA && (x3h_mode() & 2) && x3h_fd) ||
