@@ -710,11 +710,13 @@ int make_plan(const adaptseg_conv_desc *d, int op, Plan &pl) {
     if (pl.x3 && conv_math() == ADAPTSEG_MATH_F32X3_PRESPLIT) pl.x3g = pl.x3r = pl.x3r_ok;
     // F32X3: products on the x3r tiles with the fp32 operands split in-kernel (igemm_x3h_kernel,
     // igemm_x3hw_kernel), by ADAPTSEG_X3H bit 1 (forward) / 2 (data gradient) / 4 (weight gradient)
-    // Forward / data gradient only at K >= 256 (per shape, tools/conv_bench.py: the layer-1 1x1
+    // Forward / data gradient only at K >= 512 (256 until late round 6; per shape, tools/conv_bench.py: the layer-1 1x1
     // products with K = 64 / 128 run slower on the 256-row tile — two to four K steps against its
     // prologue and epilogue) and not on the stride-2 parity classes (D.conv2's data gradient 449 ->
     // 523 us); the larger products gain 4-12 % (l4.ds forward 854 -> 775 us).
-    static const int x3h_min_k = env_int("ADAPTSEG_X3H_MIN_K", 256);   // (A/B runs)
+    // (round-6 final program: 512 — the K 256 products back on the staged kernel averaged +0.4 %
+    // over 256 on two boxes, profiles/r6/x3h_min_k_ab.txt; ADAPTSEG_X3H_MIN_K for A/B runs)
+    static const int x3h_min_k = env_int("ADAPTSEG_X3H_MIN_K", 512);
     const bool x3h_fd = p.K >= x3h_min_k && !(op == ADAPTSEG_CONV_BWD_DATA && d->stride == 2);
     if (pl.x3 && pl.x3r_ok && conv_math() == ADAPTSEG_MATH_F32X3 &&
         ((op == ADAPTSEG_CONV_FWD && (x3h_mode() & 1) && x3h_fd) ||

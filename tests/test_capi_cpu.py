@@ -37,7 +37,7 @@ def test_default_conv_math_selects_f32x3():
     from adaptsegnet_amd import kernels as K
     assert K.get_conv_math() == K.MATH_F32X3
     g = K.ConvGeom(256, 256, 3, 3, 1, (2,), (2,))
-    # the default ADAPTSEG_OPT_X3H 3: forward / data gradients with K >= 256 on the 256x128x32
+    # the default ADAPTSEG_OPT_X3H 3: forward / data gradients with K >= 512 on the 256x128x32
     # tile splitting fp32 rows in-kernel (100*op + 86), weight gradients on the staged kernel
     assert K.get_x3h() == 3
     assert [K.conv_kernel_id(g, 4, 64, 128, op)[0] for op in (0, 1, 2)] == [86, 186, 295]

@@ -32,8 +32,9 @@ def k():
 
 
 def x3h_eligible(cin, cout, ks, stride, op):
-    """The library's x3h rule (conv_igemm.hip make_plan): K >= 256, no stride-2 data gradient."""
-    return ks * ks * (cin if op == 0 else cout) >= 256 and not (op == 1 and stride == 2)
+    """The library's x3h rule (conv_igemm.hip make_plan): K >= 512 (ADAPTSEG_X3H_MIN_K), no
+    stride-2 data gradient."""
+    return ks * ks * (cin if op == 0 else cout) >= 512 and not (op == 1 and stride == 2)
 
 
 # (n, cin, h, w, cout, ks, stride, pad, dil)
@@ -70,7 +71,7 @@ def test_x3h_matches_term_kernel_bitwise_and_fp64(k, shape):
             assert sel_h % 100 in (86, 87), (op, sel_h)
             assert sel_h % 100 - 86 == sel_t % 100 - 88 and sp_h == sp_t   # the same plan
             same[op] = True
-        else:   # K < 256 or a stride-2 data gradient: the register-staged kernel
+        else:   # K < 512 or a stride-2 data gradient: the register-staged kernel
             assert sel_h % 100 in (95, 96), (op, sel_h)
             same[op] = sp_h == 1 and sp_t == 1   # unsplit: bitwise equal as well
     ref = F.conv2d(x, wt, None, stride, pad, dil)
